@@ -1,0 +1,182 @@
+/*
+ * rtdm.h — C ABI of the MI355X-native two-stage aerial-frame inference path
+ * (ACFF classifier -> Darknet YOLO detector -> YOLO decode -> NMS).
+ *
+ * This is the drop-in boundary.  Every entry point replaces one call site of
+ * the reference (qazi0/real-time-disaster-management, paths relative to
+ * /root/reference/code):
+ *
+ *   rtdm_classifier_create   <- load_model()            disaster_detection/aider-predict.py:22-45
+ *                               (model ctor + load_state_dict; weights are the
+ *                                reference state-dict tensors, passed by name)
+ *   rtdm_classify            <- model(data)             disaster_detection/aider-predict.py:76
+ *                               Squeeze_ErNET.forward   disaster_detection/model/squeeze_ernet.py:24-45
+ *                               Squeeze_RedConv.forward disaster_detection/model/squeeze_ernet_redconv.py:27-52
+ *                               ErNET.forward           disaster_detection/model/ernet.py:25-49
+ *                               + (RTDM_INPUT_FRAME_U8) the CLI transform
+ *                               disaster_detection/dataloaders/aider.py:412-431
+ *   rtdm_detector_create     <- Darknet(cfg, img_size) + load_darknet_weights()
+ *                               victim_localization/yolov3/models.py:320-330, 439-486
+ *   rtdm_detect              <- model(img)[0]           victim_localization/yolov3/detect.py:87
+ *                               Darknet.forward         victim_localization/yolov3/models.py:332-395
+ *                               YOLOLayer.forward       victim_localization/yolov3/models.py:204-258
+ *   rtdm_yolo_decode         <- YOLOLayer inference branch (models.py:252-258) on raw
+ *                               head maps; also the TensorRT plugin enqueue
+ *                               victim_localization/tensorrt_inference/plugins/yolo_layer.cu:308-327
+ *   rtdm_nms                 <- non_max_suppression()   victim_localization/yolov3/utils/utils.py:488-557
+ *                               (+ torchvision.ops.boxes.nms, utils.py:552)
+ *
+ * Conventions
+ *   - Plain C types only.  Device pointers are HIP device pointers owned by the
+ *     caller (e.g. torch.empty(..., device='cuda').data_ptr()).
+ *   - Every launch is asynchronous on the given stream (hipStream_t passed as
+ *     void*; NULL = legacy default stream).  No host synchronisation inside.
+ *   - Errors are returned as rtdm_status; rtdm_last_error() gives a message
+ *     (thread-local).  Nothing aborts the process (the reference plugin's
+ *     CHECK()/abort(), yolo_layer.h:13-22, becomes a status code).
+ *   - A handle is bound to the device that was current at create time and must
+ *     not be used from two streams concurrently (one handle per rank/stream).
+ */
+#ifndef RTDM_H_
+#define RTDM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTDM_ABI_VERSION 1
+
+typedef enum rtdm_status {
+  RTDM_OK = 0,
+  RTDM_E_INVALID = 1,      /* bad argument / unknown parameter / shape mismatch   */
+  RTDM_E_HIP = 2,          /* a HIP runtime call failed                            */
+  RTDM_E_CAPACITY = 3,     /* batch larger than max_batch, workspace too small     */
+  RTDM_E_UNSUPPORTED = 4,  /* cfg layer / input size not supported                 */
+  RTDM_E_OOM = 5           /* device allocation failed                             */
+} rtdm_status;
+
+typedef enum rtdm_dtype {
+  RTDM_F32 = 0, /* fp32 activations/weights, fp32 FMA (parity mode)            */
+  RTDM_F16 = 1  /* fp16 activations/weights, fp32 accumulation on MFMA          */
+} rtdm_dtype;
+
+typedef enum rtdm_model_kind {
+  RTDM_SQUEEZE_ERNET = 0,  /* Squeeze_ErNET,   input 140x140 (squeeze_ernet.py:7)          */
+  RTDM_SQUEEZE_REDCONV = 1,/* Squeeze_RedConv, input 140x140 (squeeze_ernet_redconv.py:7)  */
+  RTDM_ERNET = 2           /* ErNET,           input 240x240 (ernet.py:6)                  */
+} rtdm_model_kind;
+
+typedef enum rtdm_input_kind {
+  RTDM_INPUT_NCHW_F32 = 0, /* model input tensor [n,3,H,W] fp32 (already transformed)        */
+  RTDM_INPUT_NCHW_F16 = 1, /* same, fp16 (the reference's --trt --quant fp16 .half() input)   */
+  RTDM_INPUT_FRAME_U8 = 2  /* raw RGB frames [n,H,W,3] uint8; transform fused on device:
+                              classifier: PIL-bilinear resize(int(1.14*S)) -> center crop S ->
+                              /255 -> ImageNet Normalize (aider.py:412-426);
+                              detector:   /255 (detect.py:80-82; frames must be img_size^2) */
+} rtdm_input_kind;
+
+/* One named parameter tensor: the reference state_dict key and its fp32 data
+ * (host memory, contiguous, the reference's own layout — OIHW for convs). */
+typedef struct rtdm_param {
+  const char* name;
+  const float* data;
+  int64_t numel;
+} rtdm_param;
+
+typedef struct rtdm_classifier_s* rtdm_classifier;
+typedef struct rtdm_detector_s* rtdm_detector;
+
+typedef struct rtdm_detector_info {
+  int img_h, img_w;     /* network input size                                     */
+  int n_layers;         /* number of cfg layers (module_defs minus [net])         */
+  int n_yolo;           /* number of [yolo] heads                                  */
+  int n_anchors_total;  /* rows of io per image (sum A*ny*nx, models.py:393-395)  */
+  int no;               /* 5 + nc                                                  */
+  int nc;               /* classes                                                 */
+  int64_t weight_floats;/* floats expected in the darknet weight stream            */
+  int64_t device_bytes; /* device memory held by the handle                        */
+  double flop_per_image;/* 2*MAC over conv layers (roofline numerator)             */
+} rtdm_detector_info;
+
+/* ---- library --------------------------------------------------------------- */
+int rtdm_abi_version(void);
+const char* rtdm_last_error(void);
+/* gfx arch string the code objects were built for ("gfx950"). */
+const char* rtdm_build_arch(void);
+
+/* ---- classifier ------------------------------------------------------------ */
+/* params: the reference state_dict (e.g. weights/squeeze-ernet-state_dict.pt),
+ * every key required by the model kind; num_batches_tracked may be omitted.     */
+rtdm_status rtdm_classifier_create(int kind, int dtype, const rtdm_param* params, int n_params,
+                                   int max_batch, rtdm_classifier* out);
+rtdm_status rtdm_classifier_destroy(rtdm_classifier h);
+/* Input side length the model expects (140 or 240). */
+int rtdm_classifier_input_size(rtdm_classifier h);
+/* x: see rtdm_input_kind.  For FRAME_U8, in_h/in_w are the frame size; for the
+ * NCHW kinds they must equal the model input size.
+ * logits: [n,5] fc output (pre-softmax) or NULL; probs: [n,5] softmax (the value
+ * the reference nn.Module returns) or NULL.                                      */
+rtdm_status rtdm_classify(rtdm_classifier h, const void* x, int x_kind, int n, int in_h, int in_w,
+                          float* logits, float* probs, void* stream);
+
+/* ---- detector -------------------------------------------------------------- */
+/* cfg_text: contents of a Darknet .cfg (victim_localization/yolov3/cfg/NAME.cfg),
+ * parsed like parse_model_cfg (utils/parse_config.py:6-52).
+ * weights: the float32 stream of a darknet .weights file after its 20-byte
+ * header (load_darknet_weights order, models.py:449-486); n_floats must equal
+ * rtdm_detector_info.weight_floats (query with weights=NULL first).
+ * If weights == NULL the handle is created for planning/introspection only
+ * (no device memory).                                                           */
+rtdm_status rtdm_detector_create(const char* cfg_text, int img_h, int img_w, int dtype,
+                                 const float* weights, int64_t n_floats, int max_batch,
+                                 rtdm_detector* out);
+rtdm_status rtdm_detector_destroy(rtdm_detector h);
+rtdm_status rtdm_detector_get_info(rtdm_detector h, rtdm_detector_info* info);
+/* Human-readable execution plan (kernels, fusions, buffers); returns bytes
+ * needed including the NUL when buf is too small.                               */
+int64_t rtdm_detector_describe(rtdm_detector h, char* buf, int64_t buf_len);
+/* io: [n, n_anchors_total, no] fp32, exactly the reference's torch.cat(io, 1). */
+rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float* io, void* stream);
+/* Debug/parity: copy cfg layer `layer`'s output of the LAST rtdm_detect call as
+ * NCHW fp32 [n,C,H,W] into out (only for layers whose full-resolution output is
+ * materialised; returns RTDM_E_UNSUPPORTED otherwise).                          */
+rtdm_status rtdm_detector_layer_output(rtdm_detector h, int layer, int n, float* out, int64_t out_numel,
+                                       int* c, int* hgt, int* wid, void* stream);
+
+/* ---- stand-alone YOLO decode (YOLOLayer inference branch) --------------------
+ * p: raw head map NCHW [n, na*no, ny, nx] fp32.  anchors: [na*2] pixels (host).
+ * Writes io rows [row_offset, row_offset + na*ny*nx) of io [n, io_rows, no].     */
+rtdm_status rtdm_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const float* anchors,
+                             int img_h, int img_w, float* io, int io_rows, int row_offset, void* stream);
+
+/* ---- NMS (non_max_suppression, utils.py:488-557, method 'vision_batch') -------
+ * io: [n, n_anchors, no] fp32 (no = 5 + nc).
+ * Semantics: obj > conf, 2 < w,h < 4096, cls *= obj, xywh->xyxy, multi-label
+ * ((cls > conf) pairs, in (anchor, class) order) if multi_label && nc > 1 else
+ * best class, optional class filter (class_mask bit c; ~0 = all), finite filter,
+ * boxes offset by class*4096 unless agnostic, greedy NMS in descending score
+ * (IoU > iou_thres suppresses, torchvision.ops.boxes.nms), ties -> lower
+ * candidate index first.
+ * det: [n, max_det, 6] rows (x1,y1,x2,y2,conf,cls) in descending score.
+ * idx: [n, max_det, 2] (anchor row, class) of each kept row, or NULL.
+ * count: [n] number of survivors (may exceed max_det; rows beyond are dropped).
+ * workspace: device scratch of rtdm_nms_workspace_size(n, n_anchors, nc) bytes. */
+size_t rtdm_nms_workspace_size(int n, int n_anchors, int nc);
+rtdm_status rtdm_nms(const float* io, int n, int n_anchors, int no, float conf_thres, double iou_thres,
+                     int multi_label, int agnostic, uint64_t class_mask, int max_det, void* workspace,
+                     size_t workspace_bytes, float* det, int32_t* idx, int32_t* count, void* stream);
+
+/* ---- pre-processing (CLI transform, aider.py:412-426) --------------------------
+ * frames: [n, in_h, in_w, 3] uint8 RGB.  out: [n, 3, S, S] fp32 (the tensor the
+ * reference feeds to model(), NCHW).  Resize shorter side to int(S*1.14) with
+ * Pillow's 8-bit antialiased BILINEAR, center crop S, ToTensor, Normalize.      */
+rtdm_status rtdm_preprocess_frames(const uint8_t* frames, int n, int in_h, int in_w, int out_size,
+                                   float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTDM_H_ */

@@ -1,0 +1,133 @@
+"""Darknet forward + YOLO decode, torch-CPU fp32 restatement (TEST INFRASTRUCTURE ONLY).
+
+Restates yolov3/utils/parse_config.py:6-52 (cfg parse), models.py:9-123
+(create_modules: conv(bias=!bn) + BN(eps 1e-4) + LeakyReLU(0.1)/Swish; maxpool
+with ZeroPad2d for size 2 / stride 1; nearest upsample; route concat; shortcut
+add), models.py:449-486 (weight stream order), models.py:332-395 (forward) and
+models.py:204-258 + 422-436 (YOLOLayer inference decode, create_grids).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def parse_cfg(text: str):
+    lines = [x for x in text.split("\n") if x and not x.startswith("#")]
+    lines = [x.rstrip().lstrip() for x in lines]
+    mdefs = []
+    for line in lines:
+        if line.startswith("["):
+            mdefs.append({"type": line[1:-1].rstrip()})
+            if mdefs[-1]["type"] == "convolutional":
+                mdefs[-1]["batch_normalize"] = 0
+        elif line:
+            key, val = line.split("=")
+            key = key.rstrip()
+            if key == "anchors":
+                mdefs[-1][key] = np.array([float(x) for x in val.split(",")]).reshape((-1, 2))
+            elif key in ("from", "layers", "mask"):
+                mdefs[-1][key] = [int(x) for x in val.split(",")]
+            else:
+                val = val.strip()
+                if val.isnumeric():
+                    mdefs[-1][key] = int(val) if (int(val) - float(val)) == 0 else float(val)
+                else:
+                    mdefs[-1][key] = val
+    return mdefs
+
+
+class DarknetRef:
+    def __init__(self, cfg_text: str, stream: np.ndarray):
+        self.mdefs = parse_cfg(cfg_text)
+        self.net = self.mdefs.pop(0)
+        self.params = {}
+        ptr = 0
+        cin = [int(self.net.get("channels", 3))]
+        self.routs = set()
+        for i, m in enumerate(self.mdefs):
+            t = m["type"]
+            if t == "convolutional":
+                f, k = int(m["filters"]), int(m["size"])
+                p = {}
+                if m["batch_normalize"]:
+                    for name in ("beta", "gamma", "mean", "var"):
+                        p[name] = torch.from_numpy(stream[ptr:ptr + f].copy())
+                        ptr += f
+                else:
+                    p["bias"] = torch.from_numpy(stream[ptr:ptr + f].copy())
+                    ptr += f
+                nw = f * cin[-1] * k * k
+                p["w"] = torch.from_numpy(stream[ptr:ptr + nw].copy()).view(f, cin[-1], k, k)
+                ptr += nw
+                self.params[i] = p
+            elif t == "route":
+                f = sum(cin[l + 1 if l > 0 else l] for l in m["layers"])
+                self.routs.update(i + l if l < 0 else l for l in m["layers"])
+            elif t == "shortcut":
+                f = cin[-1]
+                self.routs.update(i + l if l < 0 else l for l in m["from"])
+            else:
+                f = cin[-1]
+            cin.append(f)
+        assert ptr == stream.size, (ptr, stream.size)
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, keep_layers=False):
+        """x: [N,3,H,W] fp32 in [0,1] -> io [N, sum(A*ny*nx), 5+nc] (and per-layer outputs)."""
+        img_size = x.shape[-2:]
+        out, io_list = [], []
+        for i, m in enumerate(self.mdefs):
+            t = m["type"]
+            if t == "convolutional":
+                p = self.params[i]
+                k = int(m["size"])
+                s = int(m["stride"])
+                pad = (k - 1) // 2 if m["pad"] else 0
+                x = F.conv2d(x, p["w"], p.get("bias"), s, pad)
+                if "gamma" in p:
+                    x = F.batch_norm(x, p["mean"], p["var"], p["gamma"], p["beta"], False, 0.003, 1e-4)
+                if m["activation"] == "leaky":
+                    x = F.leaky_relu(x, 0.1)
+                elif m["activation"] == "swish":
+                    x = x * torch.sigmoid(x)
+            elif t == "maxpool":
+                k, s = int(m["size"]), int(m["stride"])
+                if k == 2 and s == 1:
+                    x = F.max_pool2d(F.pad(x, (0, 1, 0, 1)), k, s, (k - 1) // 2)
+                else:
+                    x = F.max_pool2d(x, k, s, (k - 1) // 2)
+            elif t == "upsample":
+                x = F.interpolate(x, scale_factor=int(m["stride"]), mode="nearest")
+            elif t == "route":
+                ls = m["layers"]
+                x = out[ls[0]] if len(ls) == 1 else torch.cat([out[l] for l in ls], 1)
+            elif t == "shortcut":
+                x = x + out[m["from"][0]]
+            elif t == "yolo":
+                io_list.append(self._yolo(m, x, img_size))
+            else:
+                raise ValueError(t)
+            out.append(x if (keep_layers or i in self.routs) else [])
+        io = torch.cat(io_list, 1)
+        return (io, out) if keep_layers else io
+
+    @staticmethod
+    def _yolo(m, p, img_size):
+        anchors = torch.Tensor(m["anchors"][m["mask"]])
+        na, nc = len(m["mask"]), int(m["classes"])
+        no = nc + 5
+        bs, _, ny, nx = p.shape
+        isz = max(img_size)
+        stride = isz / max((nx, ny))
+        yv, xv = torch.meshgrid([torch.arange(ny), torch.arange(nx)], indexing="ij")
+        grid_xy = torch.stack((xv, yv), 2).float().view((1, 1, ny, nx, 2))
+        anchor_wh = (anchors / stride).view(1, na, 1, 1, 2)
+        p = p.view(bs, na, no, ny, nx).permute(0, 1, 3, 4, 2).contiguous()
+        io = p.clone()
+        io[..., :2] = torch.sigmoid(io[..., :2]) + grid_xy
+        io[..., 2:4] = torch.exp(io[..., 2:4]) * anchor_wh
+        io[..., :4] *= stride
+        torch.sigmoid_(io[..., 4:])
+        return io.view(bs, -1, no)

@@ -1,0 +1,132 @@
+"""non_max_suppression restatement in numpy (TEST INFRASTRUCTURE ONLY).
+
+Follows yolov3/utils/utils.py:488-557 (method 'vision_batch') step by step in
+fp32, and restates the third-party kernel it calls at utils.py:552,
+torchvision.ops.boxes.nms — torchvision 0.8.2 (requirements-fyp.txt:198), CPU
+nms_kernel: order = scores sorted descending; areas = (x2-x1)*(y2-y1);
+for each i in order not yet suppressed: keep i; for each later j not
+suppressed: inter = max(0, min(x2)-max(x1)) * max(0, min(y2)-max(y1)),
+ovr = inter / (area_i + area_j - inter) (fp32), suppressed if
+(double)ovr > iou_threshold.  Ties in score are broken by candidate index
+(stable sort) — torchvision 0.8.2's sort is not specified as stable, so the
+fixtures assert no exact score ties.  Parity of this kernel is UNPINNED
+(torchvision is absent here and the reference ships no NMS test vectors).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def nms_kernel(boxes: np.ndarray, scores: np.ndarray, iou_thres: float) -> np.ndarray:
+    boxes = boxes.astype(np.float32)
+    scores = scores.astype(np.float32)
+    n = boxes.shape[0]
+    if n == 0:
+        return np.zeros(0, np.int64)
+    x1, y1, x2, y2 = boxes[:, 0], boxes[:, 1], boxes[:, 2], boxes[:, 3]
+    areas = ((x2 - x1) * (y2 - y1)).astype(np.float32)
+    order = np.argsort(-scores, kind="stable")
+    suppressed = np.zeros(n, bool)
+    keep = []
+    for _i in range(n):
+        i = order[_i]
+        if suppressed[i]:
+            continue
+        keep.append(i)
+        rest = order[_i + 1:]
+        rest = rest[~suppressed[rest]]
+        if rest.size == 0:
+            continue
+        xx1 = np.maximum(x1[i], x1[rest])
+        yy1 = np.maximum(y1[i], y1[rest])
+        xx2 = np.minimum(x2[i], x2[rest])
+        yy2 = np.minimum(y2[i], y2[rest])
+        w = np.maximum(np.float32(0), (xx2 - xx1).astype(np.float32))
+        h = np.maximum(np.float32(0), (yy2 - yy1).astype(np.float32))
+        inter = (w * h).astype(np.float32)
+        denom = ((areas[i] + areas[rest]).astype(np.float32) - inter).astype(np.float32)
+        ovr = (inter / denom).astype(np.float32)
+        suppressed[rest[ovr.astype(np.float64) > iou_thres]] = True
+    return np.asarray(keep, np.int64)
+
+
+def non_max_suppression(prediction: np.ndarray, conf_thres=0.1, iou_thres=0.6, multi_label=True, classes=None,
+                        agnostic=False, return_index=False):
+    """prediction: [N, A, 5+nc] float32 -> list of [k, 6] float32 arrays or None
+    (and, with return_index, [k, 2] int arrays of (anchor row, class))."""
+    min_wh, max_wh = 2, 4096
+    prediction = np.asarray(prediction, np.float32)
+    nc = prediction.shape[2] - 5
+    multi_label = multi_label and nc > 1
+    conf = np.float32(conf_thres)
+    output, index = [None] * len(prediction), [None] * len(prediction)
+    for image_i, pred in enumerate(prediction):
+        rows = np.arange(pred.shape[0])
+        sel = pred[:, 4] > conf
+        pred, rows = pred[sel], rows[sel]
+        sel = ((pred[:, 2:4] > min_wh) & (pred[:, 2:4] < max_wh)).all(1)
+        pred, rows = pred[sel], rows[sel]
+        if not pred.shape[0]:
+            continue
+        pred = pred.copy()
+        pred[:, 5:] *= pred[:, 4:5]
+        box = np.empty((pred.shape[0], 4), np.float32)
+        box[:, 0] = pred[:, 0] - pred[:, 2] / np.float32(2)
+        box[:, 1] = pred[:, 1] - pred[:, 3] / np.float32(2)
+        box[:, 2] = pred[:, 0] + pred[:, 2] / np.float32(2)
+        box[:, 3] = pred[:, 1] + pred[:, 3] / np.float32(2)
+        if multi_label:
+            i, j = np.nonzero(pred[:, 5:] > conf)
+            det = np.concatenate((box[i], pred[i, j + 5][:, None], j.astype(np.float32)[:, None]), 1)
+            src = np.stack((rows[i], j), 1)
+        else:
+            j = pred[:, 5:].argmax(1)
+            cf = pred[np.arange(len(j)), j + 5]
+            det = np.concatenate((box, cf[:, None], j.astype(np.float32)[:, None]), 1)
+            src = np.stack((rows, j), 1)
+        if classes:
+            sel = np.isin(j, np.asarray(classes))
+            det, src, j = det[sel], src[sel], j[sel]
+        fin = np.isfinite(det).all(1)
+        det, src = det[fin], src[fin]
+        if not det.shape[0]:
+            continue
+        c = det[:, 5] * 0 if agnostic else det[:, 5]
+        boxes = (det[:, :4] + (c[:, None] * np.float32(max_wh))).astype(np.float32)
+        keep = nms_kernel(boxes, det[:, 4], iou_thres)
+        output[image_i] = det[keep].astype(np.float32)
+        index[image_i] = src[keep].astype(np.int64)
+    return (output, index) if return_index else output
+
+
+def score_ties(prediction: np.ndarray, conf_thres: float, iou_thres: float):
+    """(tied candidate scores, harmful ties): a tie is harmful when two equal-score
+    candidates of the same class overlap with IoU > iou_thres, i.e. when the
+    unspecified tie order of the sort could change which survives."""
+    p = np.asarray(prediction, np.float32)
+    ties = harmful = 0
+    for pred in p:
+        pred = pred[pred[:, 4] > np.float32(conf_thres)]
+        s = pred[:, 5:] * pred[:, 4:5]
+        i, j = np.nonzero(s > np.float32(conf_thres))
+        sc = s[i, j]
+        vals, inv, cnt = np.unique(sc, return_inverse=True, return_counts=True)
+        ties += int((cnt - 1).sum())
+        for g in np.nonzero(cnt > 1)[0]:
+            members = np.nonzero(inv == g)[0]
+            for a in range(len(members)):
+                for b in range(a + 1, len(members)):
+                    ma, mb = members[a], members[b]
+                    if j[ma] != j[mb]:
+                        continue
+                    ba = pred[i[ma], :4]
+                    bb = pred[i[mb], :4]
+                    box = lambda r: (r[0] - r[2] / 2, r[1] - r[3] / 2, r[0] + r[2] / 2, r[1] + r[3] / 2)
+                    xa, xb = box(ba), box(bb)
+                    iw = max(0.0, min(xa[2], xb[2]) - max(xa[0], xb[0]))
+                    ih = max(0.0, min(xa[3], xb[3]) - max(xa[1], xb[1]))
+                    inter = iw * ih
+                    ua = (xa[2] - xa[0]) * (xa[3] - xa[1]) + (xb[2] - xb[0]) * (xb[3] - xb[1]) - inter
+                    if ua > 0 and inter / ua > iou_thres:
+                        harmful += 1
+    return ties, harmful

@@ -1,0 +1,437 @@
+// ACFF classifier runtime: Squeeze-ErNET / Squeeze-ErNET-RedConv / ErNET.
+//
+// Mirrors disaster_detection/model/{squeeze_ernet,squeeze_ernet_redconv,ernet}.py
+// forward passes as a fixed launch sequence over NHWC device buffers:
+//   [preprocess] -> stem conv 3x3/s2 (VALU, Cin=3) -> per ACFF block:
+//   dw3 (three dilated depthwise branches, concat layout) -> 1x1 GEMM with
+//   epilogue bias -> LeakyReLU(0.01) -> BN affine (-> fused 2x2 floor maxpool)
+//   -> tail (1x1 ->5, AvgPool 5, NCHW flatten, Linear, Softmax).
+// RedConv's conv_red1 is folded into the stem (linear o linear); conv_red2
+// absorbs acff2's BN affine.
+#include <map>
+
+#include "weights.h"
+
+namespace rtdm {
+
+struct AcffStage {
+  int cin = 0, cout = 0, h = 0, w = 0;  // input geometry
+  bool pool = false;                    // 2x2 floor maxpool after the block
+  bool affine = true;                   // BN as post-activation affine in epilogue
+  size_t dw_w = 0, dw_b = 0;            // [3][cin][9], [3][cin]
+  PackedConv pw;                        // fused 1x1 conv
+  size_t d_buf = 0, out_buf = 0;        // arena offsets (elements) per image
+  int oh = 0, ow = 0;                   // dw/1x1 output geometry
+  int out_h = 0, out_w = 0;             // after optional pool
+  // optional trailing 1x1 reducer (RedConv): conv_red2 / conv_red3
+  bool red = false;
+  bool red_pool = false;
+  PackedConv redw;
+  size_t red_buf = 0;
+  int red_h = 0, red_w = 0;
+  size_t mid_buf = 0;  // ACFF output before the reducer (when red)
+};
+
+}  // namespace rtdm
+
+struct rtdm_classifier_s {
+  int kind = 0, dtype = 0, S = 0, max_batch = 0, dev = 0;
+  rtdm::DevBlob blob;
+  rtdm::PackedConv stem;
+  int stem_oh = 0, stem_cout = 0;
+  std::vector<rtdm::AcffStage> stages;
+  size_t tail_w2 = 0, tail_fcw = 0, tail_fcb = 0;
+  int tail_pool_pad = 0, tail_ph = 0, tail_pw = 0, tail_h = 0, tail_c = 0;
+  // arena (elements of dtype per image)
+  size_t x0_buf = 0, stem_buf = 0, per_image = 0;
+  rtdm::DevBuf arena;
+  // preprocessing plans per frame size
+  std::map<std::pair<int, int>, std::unique_ptr<rtdm::ResizePlan>> resize;
+  rtdm::DevBuf resize_tmp;
+  size_t resize_tmp_bytes = 0;
+};
+
+namespace rtdm {
+
+namespace {
+
+struct ParamMap {
+  std::map<std::string, const rtdm_param*> m;
+  ParamMap(const rtdm_param* p, int n) {
+    for (int i = 0; i < n; ++i) {
+      RTDM_REQUIRE(p[i].name, RTDM_E_INVALID, "classifier: parameter with NULL name");
+      m[p[i].name] = &p[i];
+    }
+  }
+  const float* get(const std::string& k, int64_t numel) const {
+    auto it = m.find(k);
+    RTDM_REQUIRE(it != m.end(), RTDM_E_INVALID, "classifier: missing parameter '" + k + "'");
+    RTDM_REQUIRE(it->second->numel == numel, RTDM_E_INVALID,
+                 "classifier: parameter '" + k + "' has " + std::to_string(it->second->numel) + " elements, expected " +
+                     std::to_string(numel));
+    RTDM_REQUIRE(it->second->data, RTDM_E_INVALID, "classifier: parameter '" + k + "' has NULL data");
+    return it->second->data;
+  }
+};
+
+size_t esize(int dtype) { return dtype == RTDM_F16 ? 2 : 4; }
+
+// BN eval affine y = (x - mean) / sqrt(var + eps) * g + b  ==  x*s + t
+void bn_affine(const float* g, const float* b, const float* mean, const float* var, int c, double eps,
+               std::vector<double>& s, std::vector<double>& t) {
+  s.resize(c);
+  t.resize(c);
+  for (int i = 0; i < c; ++i) {
+    s[i] = (double)g[i] / std::sqrt((double)var[i] + eps);
+    t[i] = (double)b[i] - (double)mean[i] * s[i];
+  }
+}
+
+std::vector<float> to_f32(const std::vector<double>& v) { return std::vector<float>(v.begin(), v.end()); }
+
+}  // namespace
+
+static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
+  Blob blob;
+  const bool f16 = h.dtype == RTDM_F16;
+  const int S = h.S;
+  // ---- stem (squeeze_ernet.py:11 / ernet.py:10) ----
+  const float* w1 = pm.get("conv1.weight", 16 * 3 * 9);
+  h.stem_oh = (S - 3) / 2 + 1;
+  if (h.kind == RTDM_SQUEEZE_REDCONV) {
+    // conv_red1 (squeeze_ernet_redconv.py:12) folded: W' = Wr . W1, b' = br
+    const float* wr = pm.get("conv_red1.weight", 8 * 16);
+    const float* br = pm.get("conv_red1.bias", 8);
+    std::vector<float> wf(8 * 27);
+    for (int o = 0; o < 8; ++o)
+      for (int q = 0; q < 27; ++q) {
+        double acc = 0.0;
+        for (int k = 0; k < 16; ++k) acc += (double)wr[o * 16 + k] * w1[k * 27 + q];
+        wf[o * 27 + q] = (float)acc;
+      }
+    h.stem = pack_conv(blob, wf.data(), 8, 3, 3, nullptr, false);
+    h.stem.b_off = blob.add(br, 8 * sizeof(float));
+    h.stem_cout = 8;
+  } else {
+    h.stem = pack_conv(blob, w1, 16, 3, 3, nullptr, false);
+    h.stem_cout = 16;
+  }
+
+  // ---- ACFF stages ----
+  struct Spec {
+    const char* name;
+    int cin, cout;
+    bool pool;
+    const char* red;  // reducer module name or nullptr
+    int red_out;
+    bool red_before_pool;  // conv_red2 sits between acff2 and pool2
+  };
+  std::vector<Spec> specs;
+  if (h.kind == RTDM_SQUEEZE_ERNET) {
+    specs = {{"acff1", 16, 64, true, nullptr, 0, false},
+             {"acff2", 64, 96, true, nullptr, 0, false},
+             {"acff3", 96, 128, true, nullptr, 0, false},
+             {"acff4", 128, 256, false, nullptr, 0, false}};
+  } else if (h.kind == RTDM_SQUEEZE_REDCONV) {
+    specs = {{"acff1", 8, 64, true, nullptr, 0, false},
+             {"acff2", 64, 96, true, "conv_red2", 48, true},
+             {"acff3", 48, 128, true, "conv_red3", 64, false},
+             {"acff4", 64, 256, false, nullptr, 0, false}};
+  } else {
+    specs = {{"acff1", 16, 64, true, nullptr, 0, false},  {"acff2", 64, 96, true, nullptr, 0, false},
+             {"acff3", 96, 128, true, nullptr, 0, false}, {"acff4", 128, 128, false, nullptr, 0, false},
+             {"acff5", 128, 128, false, nullptr, 0, false}, {"acff6", 128, 256, false, nullptr, 0, false}};
+  }
+  size_t off = 0;
+  auto take = [&](size_t elems) {
+    const size_t o = off;
+    off += (size_t)round_up((int64_t)elems, 64);
+    return o;
+  };
+  h.x0_buf = take((size_t)S * S * 3);
+  h.stem_buf = take((size_t)h.stem_oh * h.stem_oh * h.stem_cout);
+  int ch = h.stem_oh, cc = h.stem_cout;
+  for (const Spec& sp : specs) {
+    AcffStage st;
+    st.cin = sp.cin;
+    st.cout = sp.cout;
+    RTDM_REQUIRE(cc == sp.cin, RTDM_E_INVALID, "classifier: channel mismatch at " + std::string(sp.name));
+    st.h = st.w = ch;
+    st.oh = st.ow = ch - 2;
+    const std::string p = sp.name;
+    // depthwise branches (acff.py:25-30)
+    std::vector<float> dww(3 * sp.cin * 9), dwb(3 * sp.cin);
+    for (int br = 0; br < 3; ++br) {
+      const std::string cn = p + ".conv" + std::to_string(br + 1);
+      const float* w = pm.get(cn + ".weight", (int64_t)sp.cin * 9);
+      const float* b = pm.get(cn + ".bias", sp.cin);
+      std::memcpy(&dww[(size_t)br * sp.cin * 9], w, sizeof(float) * sp.cin * 9);
+      std::memcpy(&dwb[(size_t)br * sp.cin], b, sizeof(float) * sp.cin);
+    }
+    st.dw_w = blob.add_f32(dww);
+    st.dw_b = blob.add_f32(dwb);
+    // fused 1x1 conv + BN (acff.py:31-34)
+    const float* fw = pm.get(p + ".fused_conv.weight", (int64_t)sp.cout * 3 * sp.cin);
+    const float* fb = pm.get(p + ".fused_conv.bias", sp.cout);
+    std::vector<double> bs, bt;
+    bn_affine(pm.get(p + ".batch_norm.weight", sp.cout), pm.get(p + ".batch_norm.bias", sp.cout),
+              pm.get(p + ".batch_norm.running_mean", sp.cout), pm.get(p + ".batch_norm.running_var", sp.cout), sp.cout,
+              1e-5, bs, bt);
+    st.pw = pack_conv(blob, fw, sp.cout, 3 * sp.cin, 1, nullptr, f16);
+    st.pw.b_off = blob.add(fb, sizeof(float) * sp.cout);
+    st.d_buf = take((size_t)st.oh * st.ow * 3 * sp.cin);
+    if (sp.red && sp.red_before_pool) {
+      // acff2 -> conv_red2 -> pool2: BN affine folded into conv_red2
+      st.affine = false;
+      st.red = true;
+      st.red_pool = sp.pool;
+      st.pool = false;
+      st.mid_buf = take((size_t)st.oh * st.ow * sp.cout);
+      const std::string rn = sp.red;
+      const float* rw = pm.get(rn + ".weight", (int64_t)sp.red_out * sp.cout);
+      const float* rb = pm.get(rn + ".bias", sp.red_out);
+      std::vector<float> wf((size_t)sp.red_out * sp.cout), bf(sp.red_out);
+      for (int o = 0; o < sp.red_out; ++o) {
+        double acc = rb[o];
+        for (int c = 0; c < sp.cout; ++c) {
+          wf[(size_t)o * sp.cout + c] = (float)((double)rw[(size_t)o * sp.cout + c] * bs[c]);
+          acc += (double)rw[(size_t)o * sp.cout + c] * bt[c];
+        }
+        bf[o] = (float)acc;
+      }
+      st.redw = pack_conv(blob, wf.data(), sp.red_out, sp.cout, 1, nullptr, f16);
+      st.redw.b_off = blob.add_f32(bf);
+      st.red_h = st.red_w = st.oh / 2;
+      st.red_buf = take((size_t)st.red_h * st.red_w * sp.red_out);
+      st.out_h = st.out_w = st.red_h;
+      ch = st.red_h;
+      cc = sp.red_out;
+    } else {
+      st.affine = true;
+      st.pw.s_off = blob.add_f32(to_f32(bs));
+      st.pw.t_off = blob.add_f32(to_f32(bt));
+      st.pool = sp.pool;
+      st.out_h = st.out_w = sp.pool ? st.oh / 2 : st.oh;
+      st.out_buf = take((size_t)st.out_h * st.out_w * sp.cout);
+      ch = st.out_h;
+      cc = sp.cout;
+      if (sp.red) {  // acff3 -> pool3 -> conv_red3
+        st.red = true;
+        st.red_pool = false;
+        const std::string rn = sp.red;
+        const float* rw = pm.get(rn + ".weight", (int64_t)sp.red_out * sp.cout);
+        const float* rb = pm.get(rn + ".bias", sp.red_out);
+        st.redw = pack_conv(blob, rw, sp.red_out, sp.cout, 1, nullptr, f16);
+        st.redw.b_off = blob.add(rb, sizeof(float) * sp.red_out);
+        st.red_h = st.red_w = st.out_h;
+        st.red_buf = take((size_t)st.red_h * st.red_w * sp.red_out);
+        cc = sp.red_out;
+      }
+    }
+    h.stages.push_back(st);
+  }
+  // ---- tail (squeeze_ernet.py:19-22 / ernet.py:19-22) ----
+  RTDM_REQUIRE(cc == 256, RTDM_E_INVALID, "classifier: tail expects 256 channels");
+  h.tail_h = ch;
+  h.tail_c = cc;
+  h.tail_pool_pad = h.kind == RTDM_ERNET ? 0 : 1;
+  h.tail_ph = h.tail_pw = (ch + 2 * h.tail_pool_pad - 5) + 1;
+  const int nf = 5 * h.tail_ph * h.tail_pw;
+  h.tail_w2 = blob.add(pm.get("conv2.weight", 5 * 256), 5 * 256 * sizeof(float));
+  h.tail_fcw = blob.add(pm.get("fc.weight", 5 * nf), (size_t)5 * nf * sizeof(float));
+  h.tail_fcb = blob.add(pm.get("fc.bias", 5), 5 * sizeof(float));
+  h.per_image = off;
+  h.blob.upload(blob);
+  h.arena.alloc(h.per_image * esize(h.dtype) * h.max_batch);
+}
+
+static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int n, int in_h, int in_w, float* logits,
+                           float* probs, hipStream_t s) {
+  RTDM_REQUIRE(n >= 0 && n <= h.max_batch, RTDM_E_CAPACITY,
+               "classify: batch " + std::to_string(n) + " exceeds max_batch " + std::to_string(h.max_batch));
+  if (n == 0) return;
+  RTDM_REQUIRE(x, RTDM_E_INVALID, "classify: NULL input");
+  const size_t es = esize(h.dtype);
+  char* base = h.arena.as<char>();
+  auto buf = [&](size_t off) { return (void*)(base + off * es * h.max_batch); };
+  const int S = h.S;
+  // ---- input ----
+  ConvArgs a;
+  if (x_kind == RTDM_INPUT_FRAME_U8) {
+    auto key = std::make_pair(in_h, in_w);
+    auto it = h.resize.find(key);
+    if (it == h.resize.end()) {
+      auto p = std::make_unique<ResizePlan>();
+      build_resize_plan(*p, in_h, in_w, S, true);
+      it = h.resize.emplace(key, std::move(p)).first;
+    }
+    const ResizePlan& rp = *it->second;
+    const size_t need = (size_t)h.max_batch * rp.rows * rp.out * 3;
+    if (need > h.resize_tmp_bytes) {
+      RTDM_HIP(hipStreamSynchronize(s));
+      h.resize_tmp.alloc(need);
+      h.resize_tmp_bytes = need;
+    }
+    launch_preprocess(rp, (const uint8_t*)x, n, h.resize_tmp.as<uint8_t>(), buf(h.x0_buf), 0, h.dtype, s);
+    a.in = buf(h.x0_buf);
+    a.in_kind = IN_NHWC;
+    a.in_cs = 3;
+    a.in_co = 0;
+  } else if (x_kind == RTDM_INPUT_NCHW_F32 || x_kind == RTDM_INPUT_NCHW_F16) {
+    RTDM_REQUIRE(in_h == S && in_w == S, RTDM_E_UNSUPPORTED,
+                 "classify: model expects " + std::to_string(S) + "x" + std::to_string(S) + " input, got " +
+                     std::to_string(in_h) + "x" + std::to_string(in_w));
+    a.in = x;
+    a.in_kind = x_kind == RTDM_INPUT_NCHW_F32 ? IN_NCHW_F32 : IN_NCHW_F16;
+  } else {
+    throw Error{RTDM_E_INVALID, "classify: unknown input kind"};
+  }
+  // ---- stem ----
+  a.n = n;
+  a.ih = a.iw = S;
+  a.cin = 3;
+  a.ks = 3;
+  a.stride = 2;
+  a.pad = 0;
+  a.oh = a.ow = h.stem_oh;
+  a.cout = h.stem_cout;
+  a.quad = 0;
+  conv_set_rows(a);
+  a.w = h.blob.at<void>(h.stem.w_off);
+  a.kpad = h.stem.kpad;
+  a.cout_pad = h.stem.cout_pad;
+  a.w_f32 = h.stem.mfma ? 0 : 1;
+  a.e.bias = h.blob.at<float>(h.stem.b_off);
+  a.e.full = View{buf(h.stem_buf), h.stem_cout, 0};
+  launch_conv(a, h.dtype, s);
+
+  View cur{buf(h.stem_buf), h.stem_cout, 0};
+  for (const AcffStage& st : h.stages) {
+    const int lim = st.pool || st.red_pool ? (st.oh / 2) * 2 : st.oh;
+    launch_dw3_acff(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_w),
+                    h.blob.at<float>(st.dw_b), buf(st.d_buf), h.dtype, s);
+    ConvArgs g;
+    g.in = buf(st.d_buf);
+    g.in_cs = 3 * st.cin;
+    g.in_kind = IN_NHWC;
+    g.n = n;
+    g.ih = st.oh;
+    g.iw = st.ow;
+    g.cin = 3 * st.cin;
+    g.ks = 1;
+    g.oh = st.oh;
+    g.ow = st.ow;
+    g.cout = st.cout;
+    g.w = h.blob.at<void>(st.pw.w_off);
+    g.kpad = st.pw.kpad;
+    g.cout_pad = st.pw.cout_pad;
+    g.w_f32 = st.pw.mfma ? 0 : 1;
+    g.e.bias = h.blob.at<float>(st.pw.b_off);
+    g.e.act = ACT_LEAKY;
+    g.e.slope = 0.01f;
+    if (st.affine) {
+      g.e.scale = h.blob.at<float>(st.pw.s_off);
+      g.e.shift = h.blob.at<float>(st.pw.t_off);
+    }
+    if (st.red && st.red_pool) {
+      // acff2 (-> mid, full) ; conv_red2 (+BN folded) with fused pool
+      g.quad = 1;  // only the even region is consumed by the pooled reducer
+      conv_set_rows(g);
+      g.e.full = View{buf(st.mid_buf), st.cout, 0};
+      launch_conv(g, h.dtype, s);
+      ConvArgs r;
+      r.in = buf(st.mid_buf);
+      r.in_cs = st.cout;
+      r.n = n;
+      r.ih = r.iw = st.oh;
+      r.cin = st.cout;
+      r.ks = 1;
+      r.oh = r.ow = st.oh;
+      r.cout = st.redw.cout;
+      r.quad = 1;
+      conv_set_rows(r);
+      r.w = h.blob.at<void>(st.redw.w_off);
+      r.kpad = st.redw.kpad;
+      r.cout_pad = st.redw.cout_pad;
+      r.w_f32 = st.redw.mfma ? 0 : 1;
+      r.e.bias = h.blob.at<float>(st.redw.b_off);
+      r.e.pool = View{buf(st.red_buf), st.redw.cout, 0};
+      launch_conv(r, h.dtype, s);
+      cur = View{buf(st.red_buf), st.redw.cout, 0};
+      continue;
+    }
+    g.quad = st.pool ? 1 : 0;
+    conv_set_rows(g);
+    if (st.pool)
+      g.e.pool = View{buf(st.out_buf), st.cout, 0};
+    else
+      g.e.full = View{buf(st.out_buf), st.cout, 0};
+    launch_conv(g, h.dtype, s);
+    cur = View{buf(st.out_buf), st.cout, 0};
+    if (st.red) {  // conv_red3 on the pooled output
+      ConvArgs r;
+      r.in = cur.ptr;
+      r.in_cs = st.cout;
+      r.n = n;
+      r.ih = r.iw = st.out_h;
+      r.cin = st.cout;
+      r.ks = 1;
+      r.oh = r.ow = st.out_h;
+      r.cout = st.redw.cout;
+      conv_set_rows(r);
+      r.w = h.blob.at<void>(st.redw.w_off);
+      r.kpad = st.redw.kpad;
+      r.cout_pad = st.redw.cout_pad;
+      r.w_f32 = st.redw.mfma ? 0 : 1;
+      r.e.bias = h.blob.at<float>(st.redw.b_off);
+      r.e.full = View{buf(st.red_buf), st.redw.cout, 0};
+      launch_conv(r, h.dtype, s);
+      cur = View{buf(st.red_buf), st.redw.cout, 0};
+    }
+  }
+  launch_cls_tail(cur.ptr, n, h.tail_h, h.tail_h, h.tail_c, h.blob.at<float>(h.tail_w2), h.tail_pool_pad, h.tail_ph,
+                  h.tail_pw, h.blob.at<float>(h.tail_fcw), h.blob.at<float>(h.tail_fcb), logits, probs, h.dtype, s);
+}
+
+}  // namespace rtdm
+
+using namespace rtdm;
+
+extern "C" {
+
+rtdm_status rtdm_classifier_create(int kind, int dtype, const rtdm_param* params, int n_params, int max_batch,
+                                   rtdm_classifier* out) {
+  return guard([&] {
+    RTDM_REQUIRE(out, RTDM_E_INVALID, "classifier_create: NULL out");
+    *out = nullptr;
+    RTDM_REQUIRE(kind >= RTDM_SQUEEZE_ERNET && kind <= RTDM_ERNET, RTDM_E_INVALID, "classifier_create: bad kind");
+    RTDM_REQUIRE(dtype == RTDM_F32 || dtype == RTDM_F16, RTDM_E_INVALID, "classifier_create: bad dtype");
+    RTDM_REQUIRE(max_batch > 0, RTDM_E_INVALID, "classifier_create: max_batch must be > 0");
+    RTDM_REQUIRE(params && n_params > 0, RTDM_E_INVALID, "classifier_create: no parameters");
+    auto h = std::make_unique<rtdm_classifier_s>();
+    h->kind = kind;
+    h->dtype = dtype;
+    h->S = kind == RTDM_ERNET ? 240 : 140;
+    h->max_batch = max_batch;
+    RTDM_HIP(hipGetDevice(&h->dev));
+    ParamMap pm(params, n_params);
+    build_classifier(*h, pm);
+    *out = h.release();
+  });
+}
+
+rtdm_status rtdm_classifier_destroy(rtdm_classifier h) {
+  return guard([&] { delete h; });
+}
+
+int rtdm_classifier_input_size(rtdm_classifier h) { return h ? h->S : 0; }
+
+rtdm_status rtdm_classify(rtdm_classifier h, const void* x, int x_kind, int n, int in_h, int in_w, float* logits,
+                          float* probs, void* stream) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "classify: NULL handle");
+    run_classifier(*h, x, x_kind, n, in_h, in_w, logits, probs, (hipStream_t)stream);
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,189 @@
+// Shared definitions for the rtdm HIP runtime (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/rtdm.h"
+
+namespace rtdm {
+
+// ---------------------------------------------------------------- errors ----
+void set_error(const std::string& msg);
+const char* get_error();
+
+struct Error {
+  rtdm_status code;
+  std::string msg;
+};
+
+#define RTDM_HIP(expr)                                                                     \
+  do {                                                                                     \
+    hipError_t e__ = (expr);                                                               \
+    if (e__ != hipSuccess)                                                                 \
+      throw ::rtdm::Error{RTDM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e__)}; \
+  } while (0)
+
+#define RTDM_REQUIRE(cond, code, msg)                       \
+  do {                                                      \
+    if (!(cond)) throw ::rtdm::Error{(code), (msg)};        \
+  } while (0)
+
+// Runs f, converting exceptions into a status + thread-local message.
+template <class F>
+rtdm_status guard(F&& f) {
+  try {
+    f();
+    return RTDM_OK;
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("host allocation failed");
+    return RTDM_E_OOM;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return RTDM_E_INVALID;
+  }
+}
+
+// ------------------------------------------------------------- device mem ----
+// Owning device allocation (hipMalloc); freed in the destructor.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  void reset() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  void alloc(size_t n) {
+    reset();
+    if (n == 0) n = 16;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) throw Error{RTDM_E_OOM, "hipMalloc(" + std::to_string(n) + ") failed"};
+    bytes = n;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// ------------------------------------------------------------ activations ----
+enum Act : int { ACT_LINEAR = 0, ACT_LEAKY = 1, ACT_SWISH = 2 };
+
+// Input element kinds for conv / stem kernels.
+enum InKind : int {
+  IN_NHWC = 0,     // activation buffer, NHWC with channel stride/offset, element = dtype
+  IN_FRAME_U8 = 1, // uint8 NHWC RGB frame, value = u8 / 255.f   (detect.py:80-82)
+  IN_NCHW_F32 = 2, // fp32 NCHW model input tensor
+  IN_NCHW_F16 = 3  // fp16 NCHW model input tensor
+};
+
+// A view of an NHWC activation tensor living inside a (possibly wider) buffer:
+// element (n,y,x,c) is at ptr[((n*H + y)*W + x)*cs + co + c].
+struct View {
+  void* ptr = nullptr;
+  int cs = 0;  // channel stride (elements per pixel in the buffer)
+  int co = 0;  // channel offset inside the pixel
+};
+
+// Epilogue of a convolution-as-GEMM.  Per output element (pixel m, channel c):
+//   v = acc + bias[c]; v = act(v); v = v*scale[c] + shift[c] (opt);
+//   v += residual(m, c) (opt); store to full / 2x2-max-pooled / x2-upsampled
+//   views and/or YOLO-decode it into io.
+struct Epilogue {
+  const float* bias = nullptr;
+  const float* scale = nullptr;
+  const float* shift = nullptr;
+  int act = ACT_LINEAR;
+  float slope = 0.f;
+  View res;   // residual (shortcut), same geometry as the full-res output
+  View full;  // full-resolution output
+  View pool;  // 2x2 stride-2 max pooled output (requires quad ordering)
+  View up;    // nearest x2 upsampled output
+  // YOLO decode into io [n, io_rows, no] (YOLOLayer inference branch, models.py:252-258)
+  float* io = nullptr;
+  int io_rows = 0, io_off = 0, na = 0, no = 0;
+  float ystride = 0.f;
+  float anchor_vec[16];  // (w,h) pairs, anchors / stride, fp32 like models.py:431
+};
+
+struct ConvArgs {
+  const void* in = nullptr;
+  int in_cs = 0, in_co = 0, in_kind = IN_NHWC;
+  int n = 0, ih = 0, iw = 0, cin = 0;
+  int ks = 1, stride = 1, pad = 0;
+  int oh = 0, ow = 0, cout = 0;
+  int quad = 0;  // M ordering: 1 => groups of 4 rows are 2x2 pixel quads
+  int qh = 0, qw = 0;
+  int M = 0;     // rows of the implicit GEMM
+  const void* w = nullptr;  // packed weights [cout_pad][kpad], k = (kh*ks+kw)*cin + c
+  int kpad = 0, cout_pad = 0;
+  int w_f32 = 0;            // weights packed fp32 for the VALU body (else fp16 MFMA layout)
+  Epilogue e;
+};
+
+// Launchers (conv.hip).  dtype = RTDM_F16 / RTDM_F32 (activation + weight type).
+void launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
+// Row geometry helpers shared by host planners.
+inline void conv_set_rows(ConvArgs& a) {
+  if (a.quad) {
+    a.qh = a.oh / 2;
+    a.qw = a.ow / 2;
+    a.M = a.n * a.qh * a.qw * 4;
+  } else {
+    a.M = a.n * a.oh * a.ow;
+  }
+}
+
+// ----------------------------------------------------------- other ops ----
+// ops.hip
+void launch_dw3_acff(const void* in, int in_cs, int in_co, int n, int h, int w, int c, int lim_h, int lim_w,
+                     const float* wts /*[3][c][9]*/, const float* bias /*[3][c]*/, void* out /*[n,h-2,w-2,3c]*/,
+                     int dtype, hipStream_t s);
+void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, int stride, int pad, int zero_pad_rb,
+                    View ov, int oh, int ow, int dtype, hipStream_t s);
+void launch_upsample(View iv, int n, int h, int w, int c, int f, View ov, int dtype, hipStream_t s);
+void launch_copy_slice(View iv, int n, int h, int w, int c, View ov, int dtype, hipStream_t s);
+void launch_cls_tail(const void* in, int n, int h, int w, int c, const float* w2 /*[5][c]*/, int pool_pad,
+                     int ph, int pw, const float* fcw /*[5][5*ph*pw]*/, const float* fcb, float* logits,
+                     float* probs, int dtype, hipStream_t s);
+void launch_to_nchw_f32(View iv, int n, int h, int w, int c, float* out, int dtype, hipStream_t s);
+
+struct ResizePlan {  // Pillow 8bpc antialiased bilinear, restricted to a center crop
+  int in_h = 0, in_w = 0, rs_h = 0, rs_w = 0, out = 0;
+  int crop_top = 0, crop_left = 0;
+  int ksize_h = 0, ksize_v = 0;
+  int row_first = 0, rows = 0;  // input rows needed by the vertical pass
+  DevBuf bounds_h, coef_h, bounds_v, coef_v;  // int32 device arrays
+};
+void build_resize_plan(ResizePlan& p, int in_h, int in_w, int out_size, bool upload);
+// frames -> tmp (horizontal pass) -> out (vertical pass + crop + ToTensor + Normalize)
+void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_t* tmp, void* out,
+                       int out_layout /*0: NHWC dtype, 1: NCHW f32*/, int dtype, hipStream_t s);
+
+void launch_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const float* anchor_vec, float ystride,
+                        float* io, int io_rows, int row_off, hipStream_t s);
+
+size_t nms_workspace_size(int n, int n_anchors, int nc);
+void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label,
+                int agnostic, uint64_t class_mask, int max_det, void* ws, float* det, int32_t* idx,
+                int32_t* count, hipStream_t s);
+
+}  // namespace rtdm

@@ -1,0 +1,727 @@
+// Darknet (cfg-driven YOLO) detector runtime.
+//
+// Parses a Darknet .cfg like parse_model_cfg (yolov3/utils/parse_config.py:6-52),
+// infers shapes like create_modules (yolov3/models.py:9-123), loads the darknet
+// weight stream like load_darknet_weights (models.py:449-486, BN folded into
+// the conv: eps 1e-4), and plans Darknet.forward (models.py:332-395) as a
+// sequence of kernel launches over NHWC buffers with these fusions:
+//   conv -> maxpool(2,2)         : 2x2 max in the conv epilogue (quad rows)
+//   conv -> upsample(2)          : x2 nearest stores in the conv epilogue
+//   conv -> shortcut             : residual add in the conv epilogue
+//   conv -> yolo                 : YOLOLayer decode in the conv epilogue -> io
+//   route (concat)               : producers write straight into channel
+//                                  slices of the concat buffer (zero copy)
+// Anything else runs as its own kernel (maxpool k/s, upsample, slice copy).
+#include <map>
+#include <sstream>
+
+#include "weights.h"
+
+namespace rtdm {
+
+struct CfgBlock {
+  std::string type;
+  std::map<std::string, std::string> kv;
+  bool has(const std::string& k) const { return kv.count(k) != 0; }
+  std::string str(const std::string& k, const std::string& def = "") const {
+    auto it = kv.find(k);
+    return it == kv.end() ? def : it->second;
+  }
+  int i(const std::string& k, int def) const {
+    auto it = kv.find(k);
+    if (it == kv.end()) return def;
+    try {
+      return std::stoi(it->second);
+    } catch (...) {
+      throw Error{RTDM_E_INVALID, "cfg: [" + type + "] " + k + "=" + it->second + " is not an integer"};
+    }
+  }
+  std::vector<int> ints(const std::string& k) const {
+    std::vector<int> out;
+    std::stringstream ss(str(k));
+    std::string tok;
+    while (std::getline(ss, tok, ',')) out.push_back(std::stoi(tok));
+    return out;
+  }
+  std::vector<double> floats(const std::string& k) const {
+    std::vector<double> out;
+    std::stringstream ss(str(k));
+    std::string tok;
+    while (std::getline(ss, tok, ',')) out.push_back(std::stod(tok));
+    return out;
+  }
+};
+
+static std::string strip(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b && isspace((unsigned char)s[a])) ++a;
+  while (b > a && isspace((unsigned char)s[b - 1])) --b;
+  return s.substr(a, b - a);
+}
+
+// parse_config.py:6-52
+static std::vector<CfgBlock> parse_cfg(const std::string& text) {
+  std::vector<CfgBlock> defs;
+  std::stringstream ss(text);
+  std::string line;
+  while (std::getline(ss, line)) {
+    if (line.empty() || line[0] == '#') continue;
+    line = strip(line);
+    if (line.empty()) continue;
+    if (line[0] == '[') {
+      CfgBlock b;
+      b.type = strip(line.substr(1, line.size() - 2));
+      if (b.type == "convolutional") b.kv["batch_normalize"] = "0";
+      defs.push_back(b);
+    } else {
+      const size_t eq = line.find('=');
+      RTDM_REQUIRE(eq != std::string::npos, RTDM_E_INVALID, "cfg: line without '=': " + line);
+      RTDM_REQUIRE(!defs.empty(), RTDM_E_INVALID, "cfg: key before first [section]");
+      defs.back().kv[strip(line.substr(0, eq))] = strip(line.substr(eq + 1));
+    }
+  }
+  RTDM_REQUIRE(!defs.empty() && (defs[0].type == "net" || defs[0].type == "network"), RTDM_E_INVALID,
+               "cfg: first section must be [net]");
+  return defs;
+}
+
+enum StepKind { ST_CONV = 0, ST_MAXPOOL = 1, ST_UPSAMPLE = 2, ST_COPY = 3 };
+
+struct Tensor {
+  int c = 0, h = 0, w = 0;
+  int home = -1;         // concat tensor id this one lives in (slice), or -1
+  int home_co = 0;       // channel offset inside home
+  bool own = false;      // has its own buffer
+  size_t off = 0;        // arena offset (elements per image) of own buffer
+  bool materialised = false;
+  std::string what;
+};
+
+struct Step {
+  int kind = ST_CONV;
+  int layer = -1;
+  int in_t = -1;  // -1 = network input
+  // conv
+  PackedConv pc;
+  int ks = 1, stride = 1, pad = 0, act = ACT_LINEAR, cin = 0, cout = 0;
+  int ih = 0, iw = 0, oh = 0, ow = 0;
+  int full_t = -1, pool_t = -1, up_t = -1, res_t = -1;
+  int yolo = -1;  // index into yolo heads
+  bool quad = false;
+  bool bn = false;  // raw darknet weights (host), packed after planning
+  const float *w_beta = nullptr, *w_gamma = nullptr, *w_mean = nullptr, *w_var = nullptr, *w_bias = nullptr,
+              *w_W = nullptr;
+  // maxpool / upsample / copy
+  int out_t = -1;
+  int k = 0, s = 0, p = 0, zero_rb = 0, f = 0;
+};
+
+struct YoloHead {
+  int layer = 0, na = 0, no = 0, ny = 0, nx = 0, io_off = 0;
+  float ystride = 0.f;
+  std::vector<float> anchor_vec;
+};
+
+}  // namespace rtdm
+
+struct rtdm_detector_s {
+  int img_h = 0, img_w = 0, dtype = 0, max_batch = 0, dev = 0;
+  bool planning_only = true;
+  std::vector<rtdm::CfgBlock> defs;  // without [net]
+  std::vector<rtdm::Tensor> tensors;
+  std::vector<rtdm::Step> steps;
+  std::vector<rtdm::YoloHead> heads;
+  std::vector<int> layer_tensor;  // cfg layer -> tensor id
+  int n_anchors_total = 0, no = 0, nc = 0;
+  int64_t weight_floats = 0;
+  double flop = 0.0;
+  size_t per_image = 0;  // arena elements per image
+  rtdm::DevBlob blob;
+  rtdm::DevBuf arena;
+  int last_n = 0;
+};
+
+namespace rtdm {
+
+static size_t esize_of(int dtype) { return dtype == RTDM_F16 ? 2 : 4; }
+
+static bool implicit_input(const std::string& t) {
+  return t == "convolutional" || t == "maxpool" || t == "upsample" || t == "shortcut" || t == "yolo";
+}
+
+static int resolve_ref(int layer, int l) { return l < 0 ? layer + l : l; }
+
+static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
+  auto& defs = h.defs;
+  const int L = (int)defs.size();
+  const bool f16 = h.dtype == RTDM_F16;
+  // ---- consumers (who reads out[i]) ----
+  std::vector<std::vector<int>> consumers(L);
+  for (int j = 0; j < L; ++j) {
+    const std::string& t = defs[j].type;
+    if (j > 0 && implicit_input(t)) consumers[j - 1].push_back(j);
+    if (t == "route")
+      for (int l : defs[j].ints("layers")) {
+        const int s = resolve_ref(j, l);
+        RTDM_REQUIRE(s >= 0 && s < j, RTDM_E_INVALID, "cfg: route " + std::to_string(j) + " references bad layer");
+        consumers[s].push_back(j);
+      }
+    if (t == "shortcut")
+      for (int l : defs[j].ints("from")) {
+        const int s = resolve_ref(j, l);
+        RTDM_REQUIRE(s >= 0 && s < j, RTDM_E_INVALID, "cfg: shortcut " + std::to_string(j) + " references bad layer");
+        consumers[s].push_back(j);
+      }
+  }
+  auto new_tensor = [&](int c, int hh, int ww, const std::string& what) {
+    Tensor t;
+    t.c = c;
+    t.h = hh;
+    t.w = ww;
+    t.what = what;
+    h.tensors.push_back(t);
+    return (int)h.tensors.size() - 1;
+  };
+  h.layer_tensor.assign(L, -1);
+  std::vector<bool> fused(L, false);
+  int cur_c = 3, cur_h = h.img_h, cur_w = h.img_w;  // shape of x
+  int cur_t = -1;
+  int64_t wptr = 0;
+  Blob blob;
+  auto take_w = [&](int64_t n) -> const float* {
+    const int64_t at = wptr;
+    wptr += n;
+    if (!weights) return nullptr;
+    RTDM_REQUIRE(wptr <= n_floats, RTDM_E_INVALID,
+                 "darknet weights: stream too short (" + std::to_string(n_floats) + " floats)");
+    return weights + at;
+  };
+  std::vector<int> out_c(L), out_h(L), out_w(L);
+  int nc_all = -1;
+  for (int i = 0; i < L; ++i) {
+    const CfgBlock& d = defs[i];
+    const std::string& t = d.type;
+    if (fused[i]) {  // produced by the previous conv's epilogue; shape already set
+      out_c[i] = cur_c;
+      out_h[i] = cur_h;
+      out_w[i] = cur_w;
+      continue;
+    }
+    if (t == "convolutional") {
+      const int bn = d.i("batch_normalize", 0);
+      const int filters = d.i("filters", 0);
+      const int size = d.i("size", 1);
+      RTDM_REQUIRE(d.has("stride"), RTDM_E_UNSUPPORTED, "cfg: conv without stride (stride_x/stride_y) unsupported");
+      const int stride = d.i("stride", 1);
+      const int pad = d.i("pad", 0) ? (size - 1) / 2 : 0;
+      RTDM_REQUIRE(d.i("groups", 1) == 1, RTDM_E_UNSUPPORTED, "cfg: grouped conv unsupported");
+      const std::string actn = d.str("activation", "linear");
+      int act = ACT_LINEAR;
+      if (actn == "leaky")
+        act = ACT_LEAKY;
+      else if (actn == "swish")
+        act = ACT_SWISH;
+      // create_modules adds no module for any other activation (models.py:40-44): identity
+      Step s;
+      s.kind = ST_CONV;
+      s.layer = i;
+      s.in_t = cur_t;
+      s.ks = size;
+      s.stride = stride;
+      s.pad = pad;
+      s.act = act;
+      s.cin = cur_c;
+      s.cout = filters;
+      s.ih = cur_h;
+      s.iw = cur_w;
+      s.oh = (cur_h + 2 * pad - size) / stride + 1;
+      s.ow = (cur_w + 2 * pad - size) / stride + 1;
+      RTDM_REQUIRE(s.oh > 0 && s.ow > 0, RTDM_E_UNSUPPORTED, "cfg: conv output empty at layer " + std::to_string(i));
+      h.flop += 2.0 * s.oh * s.ow * (double)filters * cur_c * size * size;
+      // weights: [bn: beta gamma mean var | bias] then W
+      const float *beta = nullptr, *gamma = nullptr, *mean = nullptr, *var = nullptr, *bias = nullptr;
+      if (bn) {
+        beta = take_w(filters);
+        gamma = take_w(filters);
+        mean = take_w(filters);
+        var = take_w(filters);
+      } else {
+        bias = take_w(filters);
+      }
+      const float* W = take_w((int64_t)filters * cur_c * size * size);
+      s.bn = bn != 0;
+      s.w_beta = beta;
+      s.w_gamma = gamma;
+      s.w_mean = mean;
+      s.w_var = var;
+      s.w_bias = bias;
+      s.w_W = W;
+      const int full = new_tensor(filters, s.oh, s.ow, "conv" + std::to_string(i));
+      s.full_t = full;
+      h.layer_tensor[i] = full;
+      cur_c = filters;
+      cur_h = s.oh;
+      cur_w = s.ow;
+      cur_t = full;
+      // ---- epilogue fusion with layer i+1 ----
+      std::vector<int> others;
+      for (int c : consumers[i])
+        if (c != i + 1) others.push_back(c);
+      bool need_full = !others.empty();
+      if (i + 1 < L) {
+        const CfgBlock& nx = defs[i + 1];
+        const bool only_next = consumers[i].size() == 1 && consumers[i][0] == i + 1;
+        if (nx.type == "maxpool" && nx.i("size", 0) == 2 && nx.i("stride", 0) == 2 && s.oh % 2 == 0 &&
+            s.ow % 2 == 0) {
+          s.quad = true;
+          s.pool_t = new_tensor(filters, s.oh / 2, s.ow / 2, "pool" + std::to_string(i + 1));
+          h.tensors[s.pool_t].materialised = true;
+          fused[i + 1] = true;
+          h.layer_tensor[i + 1] = s.pool_t;
+          cur_t = s.pool_t;
+          cur_h = s.oh / 2;
+          cur_w = s.ow / 2;
+        } else if (nx.type == "upsample" && nx.i("stride", 0) == 2 && only_next) {
+          s.up_t = new_tensor(filters, s.oh * 2, s.ow * 2, "up" + std::to_string(i + 1));
+          h.tensors[s.up_t].materialised = true;
+          fused[i + 1] = true;
+          h.layer_tensor[i + 1] = s.up_t;
+          cur_t = s.up_t;
+          cur_h = s.oh * 2;
+          cur_w = s.ow * 2;
+        } else if (nx.type == "shortcut" && only_next && nx.ints("from").size() == 1 &&
+                   resolve_ref(i + 1, nx.ints("from")[0]) != i && !nx.has("weights_type")) {
+          const int src = resolve_ref(i + 1, nx.ints("from")[0]);
+          const int st = h.layer_tensor[src];
+          RTDM_REQUIRE(st >= 0, RTDM_E_UNSUPPORTED, "cfg: shortcut source not materialisable");
+          RTDM_REQUIRE(h.tensors[st].c == filters && h.tensors[st].h == s.oh && h.tensors[st].w == s.ow,
+                       RTDM_E_UNSUPPORTED, "cfg: shortcut with channel/shape mismatch unsupported");
+          s.res_t = st;
+          fused[i + 1] = true;
+          h.layer_tensor[i + 1] = full;  // conv output with the residual added
+          need_full = !consumers[i + 1].empty();
+        } else if (nx.type == "yolo" && only_next) {
+          // YOLOLayer (models.py:185-258) fused into this head conv
+          YoloHead yh;
+          yh.layer = i + 1;
+          const std::vector<int> mask = nx.ints("mask");
+          const std::vector<double> anc = nx.floats("anchors");
+          const int ncls = nx.i("classes", 0);
+          yh.na = (int)mask.size();
+          yh.no = ncls + 5;
+          yh.ny = s.oh;
+          yh.nx = s.ow;
+          RTDM_REQUIRE(yh.na > 0 && yh.na <= 8, RTDM_E_UNSUPPORTED, "cfg: yolo with more than 8 anchors");
+          RTDM_REQUIRE(filters == yh.na * yh.no, RTDM_E_INVALID,
+                       "cfg: yolo head conv has " + std::to_string(filters) + " filters, expected na*(nc+5)");
+          RTDM_REQUIRE(nc_all < 0 || nc_all == ncls, RTDM_E_UNSUPPORTED, "cfg: yolo heads disagree on classes");
+          nc_all = ncls;
+          // create_grids: img_size = max(img), stride = img_size / max(ng) (models.py:424-425)
+          const double isz = std::max(h.img_h, h.img_w);
+          const double ystride = isz / (double)std::max(s.oh, s.ow);
+          yh.ystride = (float)ystride;
+          for (int a : mask) {
+            RTDM_REQUIRE(2 * a + 1 < (int)anc.size(), RTDM_E_INVALID, "cfg: yolo mask out of range");
+            yh.anchor_vec.push_back((float)anc[2 * a] / (float)ystride);
+            yh.anchor_vec.push_back((float)anc[2 * a + 1] / (float)ystride);
+          }
+          yh.io_off = h.n_anchors_total;
+          h.n_anchors_total += yh.na * yh.ny * yh.nx;
+          s.yolo = (int)h.heads.size();
+          h.heads.push_back(yh);
+          fused[i + 1] = true;
+          h.layer_tensor[i + 1] = full;
+          need_full = need_full || !consumers[i + 1].empty();
+        }
+      }
+      h.tensors[full].materialised = need_full || (s.pool_t < 0 && s.up_t < 0 && s.yolo < 0);
+      if (!h.tensors[full].materialised) s.full_t = -1;
+      if (s.quad && h.tensors[full].materialised) {
+        RTDM_REQUIRE(s.oh % 2 == 0 && s.ow % 2 == 0, RTDM_E_INVALID, "internal: quad with odd full output");
+      }
+      h.steps.push_back(s);
+    } else if (t == "maxpool") {
+      const int k = d.i("size", 2), st = d.i("stride", 2);
+      Step s;
+      s.kind = ST_MAXPOOL;
+      s.layer = i;
+      s.in_t = cur_t;
+      s.k = k;
+      s.s = st;
+      s.cin = cur_c;
+      s.ih = cur_h;
+      s.iw = cur_w;
+      if (k == 2 && st == 1) {  // ZeroPad2d((0,1,0,1)) + MaxPool2d(2,1) (models.py:62-64)
+        s.zero_rb = 1;
+        s.p = 0;
+        s.oh = (cur_h + 1 - k) / st + 1;
+        s.ow = (cur_w + 1 - k) / st + 1;
+      } else {
+        s.p = (k - 1) / 2;
+        s.oh = (cur_h + 2 * s.p - k) / st + 1;
+        s.ow = (cur_w + 2 * s.p - k) / st + 1;
+      }
+      RTDM_REQUIRE(cur_t >= 0, RTDM_E_UNSUPPORTED, "cfg: maxpool on the network input");
+      s.out_t = new_tensor(cur_c, s.oh, s.ow, "maxpool" + std::to_string(i));
+      h.tensors[s.out_t].materialised = true;
+      h.layer_tensor[i] = s.out_t;
+      cur_h = s.oh;
+      cur_w = s.ow;
+      cur_t = s.out_t;
+      h.steps.push_back(s);
+    } else if (t == "upsample") {
+      Step s;
+      s.kind = ST_UPSAMPLE;
+      s.layer = i;
+      s.in_t = cur_t;
+      s.f = d.i("stride", 2);
+      s.cin = cur_c;
+      s.ih = cur_h;
+      s.iw = cur_w;
+      s.oh = cur_h * s.f;
+      s.ow = cur_w * s.f;
+      RTDM_REQUIRE(cur_t >= 0, RTDM_E_UNSUPPORTED, "cfg: upsample on the network input");
+      s.out_t = new_tensor(cur_c, s.oh, s.ow, "upsample" + std::to_string(i));
+      h.tensors[s.out_t].materialised = true;
+      h.layer_tensor[i] = s.out_t;
+      cur_h = s.oh;
+      cur_w = s.ow;
+      cur_t = s.out_t;
+      h.steps.push_back(s);
+    } else if (t == "route") {
+      const std::vector<int> ls = d.ints("layers");
+      RTDM_REQUIRE(!ls.empty(), RTDM_E_INVALID, "cfg: route without layers");
+      if (ls.size() == 1) {
+        const int src = resolve_ref(i, ls[0]);
+        const int tt = h.layer_tensor[src];
+        RTDM_REQUIRE(tt >= 0, RTDM_E_UNSUPPORTED, "cfg: route to a layer without output");
+        h.layer_tensor[i] = tt;
+        cur_t = tt;
+        cur_c = h.tensors[tt].c;
+        cur_h = h.tensors[tt].h;
+        cur_w = h.tensors[tt].w;
+      } else {
+        int csum = 0, hh = -1, ww = -1;
+        for (int l : ls) {
+          const int tt = h.layer_tensor[resolve_ref(i, l)];
+          RTDM_REQUIRE(tt >= 0, RTDM_E_UNSUPPORTED, "cfg: route to a layer without output");
+          if (hh < 0) {
+            hh = h.tensors[tt].h;
+            ww = h.tensors[tt].w;
+          }
+          RTDM_REQUIRE(h.tensors[tt].h == hh && h.tensors[tt].w == ww, RTDM_E_UNSUPPORTED,
+                       "cfg: route of differently sized maps (reorg) unsupported");
+          csum += h.tensors[tt].c;
+        }
+        const int ct = new_tensor(csum, hh, ww, "route" + std::to_string(i));
+        h.tensors[ct].materialised = true;
+        h.tensors[ct].own = true;
+        // home sources inside the concat buffer where possible, else copy
+        int co = 0;
+        for (int l : ls) {
+          const int tt = h.layer_tensor[resolve_ref(i, l)];
+          Tensor& src = h.tensors[tt];
+          src.materialised = true;
+          if (src.home < 0 && !src.own) {
+            src.home = ct;
+            src.home_co = co;
+          } else {
+            Step s;
+            s.kind = ST_COPY;
+            s.layer = i;
+            s.in_t = tt;
+            s.out_t = ct;
+            s.k = co;  // channel offset in the concat
+            s.cin = src.c;
+            s.ih = hh;
+            s.iw = ww;
+            h.steps.push_back(s);
+          }
+          co += src.c;
+        }
+        h.layer_tensor[i] = ct;
+        cur_t = ct;
+        cur_c = csum;
+        cur_h = hh;
+        cur_w = ww;
+      }
+    } else if (t == "shortcut") {
+      throw Error{RTDM_E_UNSUPPORTED, "cfg: shortcut not preceded by a fusable conv (layer " + std::to_string(i) + ")"};
+    } else if (t == "yolo") {
+      throw Error{RTDM_E_UNSUPPORTED, "cfg: yolo not preceded by a fusable head conv (layer " + std::to_string(i) + ")"};
+    } else {
+      throw Error{RTDM_E_UNSUPPORTED, "cfg: unsupported layer type [" + t + "] at layer " + std::to_string(i)};
+    }
+    out_c[i] = cur_c;
+    out_h[i] = cur_h;
+    out_w[i] = cur_w;
+  }
+  RTDM_REQUIRE(!h.heads.empty(), RTDM_E_UNSUPPORTED, "cfg: no [yolo] layers");
+  h.nc = nc_all;
+  h.no = nc_all + 5;
+  h.weight_floats = wptr;
+  if (weights)
+    RTDM_REQUIRE(wptr == n_floats, RTDM_E_INVALID,
+                 "darknet weights: stream has " + std::to_string(n_floats) + " floats, cfg needs " +
+                     std::to_string(wptr));
+  // ---- own buffers for materialised tensors that are not homed in a concat ----
+  size_t off = 0;
+  for (Tensor& t : h.tensors) {
+    if (!t.materialised) continue;
+    if (t.home >= 0) continue;
+    t.own = true;
+    t.off = off;
+    off += (size_t)round_up((int64_t)t.c * t.h * t.w, 64);
+  }
+  h.per_image = off;
+  // ---- pack conv weights: MFMA layout iff the input view is 16-byte aligned NHWC ----
+  for (Step& st : h.steps) {
+    if (st.kind != ST_CONV) continue;
+    bool use_mfma = f16 && st.in_t >= 0 && st.cin % 8 == 0;
+    if (use_mfma) {
+      const Tensor& it = h.tensors[st.in_t];
+      const int cs = it.home >= 0 ? h.tensors[it.home].c : it.c;
+      const int co = it.home >= 0 ? it.home_co : 0;
+      use_mfma = cs % 8 == 0 && co % 8 == 0;
+    }
+    const int filters = st.cout, size = st.ks;
+    if (weights) {
+      std::vector<double> sc(filters, 1.0);
+      std::vector<float> b(filters);
+      for (int o = 0; o < filters; ++o) {
+        if (st.bn) {
+          sc[o] = (double)st.w_gamma[o] / std::sqrt((double)st.w_var[o] + 1e-4);
+          b[o] = (float)((double)st.w_beta[o] - (double)st.w_mean[o] * sc[o]);
+        } else {
+          b[o] = st.w_bias[o];
+        }
+      }
+      st.pc = pack_conv(blob, st.w_W, filters, st.cin, size, st.bn ? sc.data() : nullptr, use_mfma);
+      st.pc.b_off = blob.add_f32(b);
+    } else {
+      st.pc.cout = filters;
+      st.pc.cin = st.cin;
+      st.pc.ks = size;
+      st.pc.mfma = use_mfma;
+      st.pc.kpad = (int)round_up((int64_t)size * size * st.cin, 64);
+      st.pc.cout_pad = cout_pad_for(filters);
+    }
+    st.w_beta = st.w_gamma = st.w_mean = st.w_var = st.w_bias = st.w_W = nullptr;
+  }
+  if (weights) {
+    h.blob.upload(blob);
+    h.arena.alloc(h.per_image * esize_of(h.dtype) * h.max_batch);
+  }
+}
+
+// View of tensor t for a batch arena.
+static View tensor_view(const rtdm_detector_s& h, int t) {
+  if (t < 0) return View{};
+  const Tensor& x = h.tensors[t];
+  if (!x.materialised) return View{};
+  const size_t es = esize_of(h.dtype);
+  char* base = h.arena.as<char>();
+  if (x.home >= 0) {
+    const Tensor& c = h.tensors[x.home];
+    return View{base + c.off * es * h.max_batch, c.c, x.home_co};
+  }
+  return View{base + x.off * es * h.max_batch, x.c, 0};
+}
+
+static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, float* io, hipStream_t s) {
+  RTDM_REQUIRE(!h.planning_only, RTDM_E_INVALID, "detect: handle was created without weights");
+  RTDM_REQUIRE(n >= 0 && n <= h.max_batch, RTDM_E_CAPACITY,
+               "detect: batch " + std::to_string(n) + " exceeds max_batch " + std::to_string(h.max_batch));
+  if (n == 0) return;
+  RTDM_REQUIRE(x && io, RTDM_E_INVALID, "detect: NULL input or io");
+  int in_kind;
+  if (x_kind == RTDM_INPUT_FRAME_U8)
+    in_kind = IN_FRAME_U8;
+  else if (x_kind == RTDM_INPUT_NCHW_F32)
+    in_kind = IN_NCHW_F32;
+  else if (x_kind == RTDM_INPUT_NCHW_F16)
+    in_kind = IN_NCHW_F16;
+  else
+    throw Error{RTDM_E_INVALID, "detect: unknown input kind"};
+  for (const Step& st : h.steps) {
+    if (st.kind == ST_CONV) {
+      ConvArgs a;
+      if (st.in_t < 0) {
+        a.in = x;
+        a.in_kind = in_kind;
+      } else {
+        const View v = tensor_view(h, st.in_t);
+        a.in = v.ptr;
+        a.in_cs = v.cs;
+        a.in_co = v.co;
+        a.in_kind = IN_NHWC;
+      }
+      a.n = n;
+      a.ih = st.ih;
+      a.iw = st.iw;
+      a.cin = st.cin;
+      a.ks = st.ks;
+      a.stride = st.stride;
+      a.pad = st.pad;
+      a.oh = st.oh;
+      a.ow = st.ow;
+      a.cout = st.cout;
+      a.quad = st.quad ? 1 : 0;
+      conv_set_rows(a);
+      a.w = h.blob.at<void>(st.pc.w_off);
+      a.kpad = st.pc.kpad;
+      a.cout_pad = st.pc.cout_pad;
+      a.e.bias = h.blob.at<float>(st.pc.b_off);
+      a.e.act = st.act;
+      a.e.slope = 0.1f;
+      a.e.full = tensor_view(h, st.full_t);
+      a.e.pool = tensor_view(h, st.pool_t);
+      a.e.up = tensor_view(h, st.up_t);
+      a.e.res = tensor_view(h, st.res_t);
+      if (st.yolo >= 0) {
+        const YoloHead& y = h.heads[st.yolo];
+        a.e.io = io;
+        a.e.io_rows = h.n_anchors_total;
+        a.e.io_off = y.io_off;
+        a.e.na = y.na;
+        a.e.no = y.no;
+        a.e.ystride = y.ystride;
+        for (size_t q = 0; q < y.anchor_vec.size(); ++q) a.e.anchor_vec[q] = y.anchor_vec[q];
+      }
+      // the mfma/valu choice was fixed when the weights were packed
+      a.w_f32 = st.pc.mfma ? 0 : 1;
+      launch_conv(a, h.dtype, s);
+    } else if (st.kind == ST_MAXPOOL) {
+      launch_maxpool(nullptr, tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, st.k, st.s, st.p, st.zero_rb,
+                     tensor_view(h, st.out_t), st.oh, st.ow, h.dtype, s);
+    } else if (st.kind == ST_UPSAMPLE) {
+      launch_upsample(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, st.f, tensor_view(h, st.out_t), h.dtype, s);
+    } else if (st.kind == ST_COPY) {
+      View o = tensor_view(h, st.out_t);
+      o.co += st.k;
+      launch_copy_slice(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, o, h.dtype, s);
+    }
+  }
+  h.last_n = n;
+}
+
+static std::string describe(const rtdm_detector_s& h) {
+  std::ostringstream o;
+  o << "darknet plan: img " << h.img_h << "x" << h.img_w << " dtype " << (h.dtype == RTDM_F16 ? "f16" : "f32")
+    << " layers " << h.defs.size() << " steps " << h.steps.size() << " anchors " << h.n_anchors_total << " no " << h.no
+    << " GFLOP/img " << h.flop * 1e-9 << " arena/img " << h.per_image << " elems\n";
+  auto tn = [&](int t) -> std::string {
+    if (t < 0) return "-";
+    const Tensor& x = h.tensors[t];
+    std::ostringstream s;
+    s << x.what << "[" << x.c << "x" << x.h << "x" << x.w;
+    if (x.home >= 0) s << " @" << h.tensors[x.home].what << "+" << x.home_co;
+    s << "]";
+    return s.str();
+  };
+  for (const Step& st : h.steps) {
+    o << "  L" << st.layer << " ";
+    if (st.kind == ST_CONV) {
+      o << "conv" << st.ks << "x" << st.ks << "/" << st.stride << " " << st.cin << "->" << st.cout << " "
+        << (st.pc.mfma ? "mfma" : "valu") << (st.quad ? " quad" : "") << " in=" << (st.in_t < 0 ? "input" : tn(st.in_t))
+        << " full=" << tn(st.full_t) << " pool=" << tn(st.pool_t) << " up=" << tn(st.up_t) << " res=" << tn(st.res_t);
+      if (st.yolo >= 0) o << " yolo" << st.yolo << "(off " << h.heads[st.yolo].io_off << ")";
+    } else if (st.kind == ST_MAXPOOL) {
+      o << "maxpool k" << st.k << " s" << st.s << (st.zero_rb ? " zeropad" : "") << " " << tn(st.in_t) << " -> "
+        << tn(st.out_t);
+    } else if (st.kind == ST_UPSAMPLE) {
+      o << "upsample x" << st.f << " " << tn(st.in_t) << " -> " << tn(st.out_t);
+    } else {
+      o << "copy " << tn(st.in_t) << " -> " << tn(st.out_t) << "+" << st.k;
+    }
+    o << "\n";
+  }
+  return o.str();
+}
+
+}  // namespace rtdm
+
+using namespace rtdm;
+
+extern "C" {
+
+rtdm_status rtdm_detector_create(const char* cfg_text, int img_h, int img_w, int dtype, const float* weights,
+                                 int64_t n_floats, int max_batch, rtdm_detector* out) {
+  return guard([&] {
+    RTDM_REQUIRE(out, RTDM_E_INVALID, "detector_create: NULL out");
+    *out = nullptr;
+    RTDM_REQUIRE(cfg_text, RTDM_E_INVALID, "detector_create: NULL cfg");
+    RTDM_REQUIRE(img_h > 0 && img_w > 0, RTDM_E_INVALID, "detector_create: bad image size");
+    RTDM_REQUIRE(dtype == RTDM_F32 || dtype == RTDM_F16, RTDM_E_INVALID, "detector_create: bad dtype");
+    RTDM_REQUIRE(max_batch > 0, RTDM_E_INVALID, "detector_create: max_batch must be > 0");
+    auto h = std::make_unique<rtdm_detector_s>();
+    h->img_h = img_h;
+    h->img_w = img_w;
+    h->dtype = dtype;
+    h->max_batch = max_batch;
+    h->planning_only = weights == nullptr;
+    if (!h->planning_only) RTDM_HIP(hipGetDevice(&h->dev));
+    std::vector<CfgBlock> defs = parse_cfg(cfg_text);
+    const CfgBlock& net = defs[0];
+    RTDM_REQUIRE(net.i("channels", 3) == 3, RTDM_E_UNSUPPORTED, "cfg: only 3-channel input supported");
+    h->defs.assign(defs.begin() + 1, defs.end());
+    plan(*h, weights, n_floats);
+    *out = h.release();
+  });
+}
+
+rtdm_status rtdm_detector_destroy(rtdm_detector h) {
+  return guard([&] { delete h; });
+}
+
+rtdm_status rtdm_detector_get_info(rtdm_detector h, rtdm_detector_info* info) {
+  return guard([&] {
+    RTDM_REQUIRE(h && info, RTDM_E_INVALID, "detector_get_info: NULL argument");
+    info->img_h = h->img_h;
+    info->img_w = h->img_w;
+    info->n_layers = (int)h->defs.size();
+    info->n_yolo = (int)h->heads.size();
+    info->n_anchors_total = h->n_anchors_total;
+    info->no = h->no;
+    info->nc = h->nc;
+    info->weight_floats = h->weight_floats;
+    info->device_bytes = (int64_t)(h->blob.buf.bytes + h->arena.bytes);
+    info->flop_per_image = h->flop;
+  });
+}
+
+int64_t rtdm_detector_describe(rtdm_detector h, char* buf, int64_t buf_len) {
+  if (!h) return 0;
+  const std::string s = describe(*h);
+  const int64_t need = (int64_t)s.size() + 1;
+  if (buf && buf_len >= need) std::memcpy(buf, s.c_str(), need);
+  return need;
+}
+
+rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float* io, void* stream) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "detect: NULL handle");
+    run_detector(*h, x, x_kind, n, io, (hipStream_t)stream);
+  });
+}
+
+rtdm_status rtdm_detector_layer_output(rtdm_detector h, int layer, int n, float* out, int64_t out_numel, int* c,
+                                       int* hgt, int* wid, void* stream) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "layer_output: NULL handle");
+    RTDM_REQUIRE(layer >= 0 && layer < (int)h->defs.size(), RTDM_E_INVALID, "layer_output: bad layer");
+    const int t = h->layer_tensor[layer];
+    RTDM_REQUIRE(t >= 0 && h->tensors[t].materialised, RTDM_E_UNSUPPORTED,
+                 "layer_output: layer " + std::to_string(layer) + " output is fused away (not materialised)");
+    const Tensor& x = h->tensors[t];
+    if (c) *c = x.c;
+    if (hgt) *hgt = x.h;
+    if (wid) *wid = x.w;
+    if (!out) return;
+    RTDM_REQUIRE(n > 0 && n <= h->last_n, RTDM_E_INVALID, "layer_output: n exceeds the last detect batch");
+    RTDM_REQUIRE(out_numel >= (int64_t)n * x.c * x.h * x.w, RTDM_E_CAPACITY, "layer_output: out too small");
+    launch_to_nchw_f32(tensor_view(*h, t), n, x.h, x.w, x.c, out, h->dtype, (hipStream_t)stream);
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,726 @@
+// Non-GEMM kernels of the hot path (gfx950): ACFF dilated depthwise branches,
+// max pooling, upsample / route copies, the classifier tail, the CLI
+// pre-processing (Pillow 8-bit antialiased bilinear resize + crop + normalize),
+// the stand-alone YOLO decode, and per-image greedy NMS.
+#include "common.h"
+
+#include <cmath>
+
+namespace rtdm {
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p) {
+  return (float)(*p);
+}
+
+// ------------------------------------------------------------------ ACFF dw --
+// The three depthwise branches of ACFF (acff.py:25-30): 3x3 dilation 1/2/3,
+// padding 0/1/2, +bias each, concatenated along channels (acff.py:46) into an
+// NHWC [n, h-2, w-2, 3c] buffer: channel b*c + ch holds branch b.  All three
+// windows are centred on input pixel (oy+1, ox+1) with radius 1/2/3; only the
+// dilated branches ever read zero padding.  Only the top-left lim_h x lim_w
+// outputs are produced (the rest is dropped by the following floor maxpool).
+template <typename T>
+__global__ __launch_bounds__(256) void dw3_acff_kernel(const T* __restrict__ in, int in_cs, int in_co, int n, int h,
+                                                       int w, int c, int lim_h, int lim_w,
+                                                       const float* __restrict__ wts, const float* __restrict__ bias,
+                                                       T* __restrict__ out) {
+  const int oh = h - 2, ow = w - 2;
+  const int64_t total = (int64_t)n * lim_h * lim_w * c;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(idx % c);
+    int64_t p = idx / c;
+    const int ox = (int)(p % lim_w);
+    p /= lim_w;
+    const int oy = (int)(p % lim_h);
+    const int b = (int)(p / lim_h);
+    const T* src = in + (size_t)b * h * w * in_cs + in_co + ch;
+    T* dst = out + (((size_t)b * oh + oy) * ow + ox) * (3 * c) + ch;
+#pragma unroll
+    for (int br = 0; br < 3; ++br) {
+      const int d = br + 1;
+      const float* wk = wts + ((size_t)br * c + ch) * 9;
+      float acc = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int iy = oy + 1 + (kh - 1) * d;
+        if ((unsigned)iy >= (unsigned)h) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int ix = ox + 1 + (kw - 1) * d;
+          if ((unsigned)ix >= (unsigned)w) continue;
+          acc = fmaf(wk[kh * 3 + kw], ldf(src + ((size_t)iy * w + ix) * in_cs), acc);
+        }
+      }
+      dst[br * c] = (T)(acc + bias[br * c + ch]);
+    }
+  }
+}
+
+static inline int grid_for(int64_t total, int block) {
+  int64_t g = (total + block - 1) / block;
+  if (g > 2048 * 4) g = 2048 * 4;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+void launch_dw3_acff(const void* in, int in_cs, int in_co, int n, int h, int w, int c, int lim_h, int lim_w,
+                     const float* wts, const float* bias, void* out, int dtype, hipStream_t s) {
+  const int64_t total = (int64_t)n * lim_h * lim_w * c;
+  if (total <= 0) return;
+  const int g = grid_for(total, 256);
+  if (dtype == RTDM_F16)
+    hipLaunchKernelGGL(dw3_acff_kernel<_Float16>, dim3(g), dim3(256), 0, s, (const _Float16*)in, in_cs, in_co, n, h,
+                       w, c, lim_h, lim_w, wts, bias, (_Float16*)out);
+  else
+    hipLaunchKernelGGL(dw3_acff_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)in, in_cs, in_co, n, h, w, c,
+                       lim_h, lim_w, wts, bias, (float*)out);
+  RTDM_HIP(hipGetLastError());
+}
+
+// ----------------------------------------------------------------- maxpool --
+// nn.MaxPool2d(k, s, padding=pad) (implicit -inf padding), or, for the
+// Darknet size-2/stride-1 case, ZeroPad2d((0,1,0,1)) + MaxPool2d(2,1)
+// (models.py:57-64): padded cells read as 0.
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ in, int in_cs, int in_co, int n, int h,
+                                                      int w, int c, int k, int stride, int pad, int zero_rb,
+                                                      T* __restrict__ out, int out_cs, int out_co, int oh, int ow) {
+  const int64_t total = (int64_t)n * oh * ow * c;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(idx % c);
+    int64_t p = idx / c;
+    const int ox = (int)(p % ow);
+    p /= ow;
+    const int oy = (int)(p % oh);
+    const int b = (int)(p / oh);
+    float m = -INFINITY;
+    const int y0 = oy * stride - pad, x0 = ox * stride - pad;
+    for (int dy = 0; dy < k; ++dy) {
+      const int iy = y0 + dy;
+      for (int dx = 0; dx < k; ++dx) {
+        const int ix = x0 + dx;
+        float v;
+        if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w)
+          v = ldf(in + (((size_t)b * h + iy) * w + ix) * in_cs + in_co + ch);
+        else if (zero_rb)
+          v = 0.f;
+        else
+          continue;
+        m = fmaxf(m, v);
+      }
+    }
+    out[(((size_t)b * oh + oy) * ow + ox) * out_cs + out_co + ch] = (T)m;
+  }
+}
+
+void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, int stride, int pad, int zero_rb,
+                    View ov, int oh, int ow, int dtype, hipStream_t s) {
+  (void)in;
+  const int64_t total = (int64_t)n * oh * ow * c;
+  if (total <= 0) return;
+  const int g = grid_for(total, 256);
+  if (dtype == RTDM_F16)
+    hipLaunchKernelGGL(maxpool_kernel<_Float16>, dim3(g), dim3(256), 0, s, (const _Float16*)iv.ptr, iv.cs, iv.co, n,
+                       h, w, c, k, stride, pad, zero_rb, (_Float16*)ov.ptr, ov.cs, ov.co, oh, ow);
+  else
+    hipLaunchKernelGGL(maxpool_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)iv.ptr, iv.cs, iv.co, n, h, w,
+                       c, k, stride, pad, zero_rb, (float*)ov.ptr, ov.cs, ov.co, oh, ow);
+  RTDM_HIP(hipGetLastError());
+}
+
+// ----------------------------------------------------- upsample / route copy --
+template <typename T>
+__global__ __launch_bounds__(256) void upsample_kernel(const T* __restrict__ in, int in_cs, int in_co, int n, int h,
+                                                       int w, int c, int f, T* __restrict__ out, int out_cs,
+                                                       int out_co) {
+  const int oh = h * f, ow = w * f;
+  const int64_t total = (int64_t)n * oh * ow * c;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(idx % c);
+    int64_t p = idx / c;
+    const int ox = (int)(p % ow);
+    p /= ow;
+    const int oy = (int)(p % oh);
+    const int b = (int)(p / oh);
+    out[(((size_t)b * oh + oy) * ow + ox) * out_cs + out_co + ch] =
+        in[(((size_t)b * h + oy / f) * w + ox / f) * in_cs + in_co + ch];
+  }
+}
+
+void launch_upsample(View iv, int n, int h, int w, int c, int f, View ov, int dtype, hipStream_t s) {
+  const int64_t total = (int64_t)n * h * f * w * f * c;
+  if (total <= 0) return;
+  const int g = grid_for(total, 256);
+  if (dtype == RTDM_F16)
+    hipLaunchKernelGGL(upsample_kernel<_Float16>, dim3(g), dim3(256), 0, s, (const _Float16*)iv.ptr, iv.cs, iv.co, n,
+                       h, w, c, f, (_Float16*)ov.ptr, ov.cs, ov.co);
+  else
+    hipLaunchKernelGGL(upsample_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)iv.ptr, iv.cs, iv.co, n, h, w,
+                       c, f, (float*)ov.ptr, ov.cs, ov.co);
+  RTDM_HIP(hipGetLastError());
+}
+
+void launch_copy_slice(View iv, int n, int h, int w, int c, View ov, int dtype, hipStream_t s) {
+  launch_upsample(iv, n, h, w, c, 1, ov, dtype, s);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void to_nchw_kernel(const T* __restrict__ in, int cs, int co, int n, int h, int w,
+                                                      int c, float* __restrict__ out) {
+  const int64_t total = (int64_t)n * c * h * w;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(idx % w);
+    int64_t p = idx / w;
+    const int y = (int)(p % h);
+    p /= h;
+    const int ch = (int)(p % c);
+    const int b = (int)(p / c);
+    out[idx] = ldf(in + (((size_t)b * h + y) * w + x) * cs + co + ch);
+  }
+}
+
+void launch_to_nchw_f32(View iv, int n, int h, int w, int c, float* out, int dtype, hipStream_t s) {
+  const int64_t total = (int64_t)n * c * h * w;
+  if (total <= 0) return;
+  const int g = grid_for(total, 256);
+  if (dtype == RTDM_F16)
+    hipLaunchKernelGGL(to_nchw_kernel<_Float16>, dim3(g), dim3(256), 0, s, (const _Float16*)iv.ptr, iv.cs, iv.co, n,
+                       h, w, c, out);
+  else
+    hipLaunchKernelGGL(to_nchw_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)iv.ptr, iv.cs, iv.co, n, h, w,
+                       c, out);
+  RTDM_HIP(hipGetLastError());
+}
+
+// --------------------------------------------------------- classifier tail --
+// conv2 1x1 C->5 (no bias) -> AvgPool2d(5, 1, pool_pad) (count_include_pad:
+// divisor 25) -> view(-1, 5*ph*pw) in NCHW order -> Linear -> Softmax
+// (squeeze_ernet.py:33-41, ernet.py:38-45).  One 256-thread block per image.
+template <typename T>
+__global__ __launch_bounds__(256) void cls_tail_kernel(const T* __restrict__ in, int h, int w, int c,
+                                                       const float* __restrict__ w2, int pool_pad, int ph, int pw,
+                                                       const float* __restrict__ fcw, const float* __restrict__ fcb,
+                                                       float* __restrict__ logits, float* __restrict__ probs) {
+  __shared__ float conv[5 * 64];  // [o][y*w+x], h*w <= 64
+  __shared__ float feat[5 * 16];
+  __shared__ float lg[5];
+  const int b = blockIdx.x;
+  const int hw = h * w;
+  const T* src = in + (size_t)b * hw * c;
+  for (int t = threadIdx.x; t < 5 * hw; t += blockDim.x) {
+    const int o = t / hw, p = t - o * hw;
+    const T* x = src + (size_t)p * c;
+    const float* wr = w2 + (size_t)o * c;
+    float acc = 0.f;
+    for (int ch = 0; ch < c; ++ch) acc = fmaf(ldf(x + ch), wr[ch], acc);
+    conv[o * hw + p] = acc;
+  }
+  __syncthreads();
+  const int nf = 5 * ph * pw;
+  for (int t = threadIdx.x; t < nf; t += blockDim.x) {
+    const int o = t / (ph * pw);
+    const int r = t - o * ph * pw;
+    const int i = r / pw, j = r - (r / pw) * pw;
+    float s = 0.f;
+    for (int dy = 0; dy < 5; ++dy) {
+      const int y = i - pool_pad + dy;
+      if ((unsigned)y >= (unsigned)h) continue;
+      for (int dx = 0; dx < 5; ++dx) {
+        const int x = j - pool_pad + dx;
+        if ((unsigned)x >= (unsigned)w) continue;
+        s += conv[o * hw + y * w + x];
+      }
+    }
+    feat[t] = s / 25.f;
+  }
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    const int k = threadIdx.x;
+    float acc = 0.f;
+    for (int q = 0; q < nf; ++q) acc = fmaf(feat[q], fcw[k * nf + q], acc);
+    acc += fcb[k];
+    lg[k] = acc;
+    if (logits) logits[b * 5 + k] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < 5 && probs) {
+    float mx = lg[0];
+    for (int k = 1; k < 5; ++k) mx = fmaxf(mx, lg[k]);
+    float sum = 0.f;
+    for (int k = 0; k < 5; ++k) sum += expf(lg[k] - mx);
+    probs[b * 5 + threadIdx.x] = expf(lg[threadIdx.x] - mx) / sum;
+  }
+}
+
+void launch_cls_tail(const void* in, int n, int h, int w, int c, const float* w2, int pool_pad, int ph, int pw,
+                     const float* fcw, const float* fcb, float* logits, float* probs, int dtype, hipStream_t s) {
+  RTDM_REQUIRE(h * w <= 64 && ph * pw <= 16, RTDM_E_UNSUPPORTED, "classifier tail: feature map too large");
+  if (n <= 0) return;
+  if (dtype == RTDM_F16)
+    hipLaunchKernelGGL(cls_tail_kernel<_Float16>, dim3(n), dim3(256), 0, s, (const _Float16*)in, h, w, c, w2,
+                       pool_pad, ph, pw, fcw, fcb, logits, probs);
+  else
+    hipLaunchKernelGGL(cls_tail_kernel<float>, dim3(n), dim3(256), 0, s, (const float*)in, h, w, c, w2, pool_pad, ph,
+                       pw, fcw, fcb, logits, probs);
+  RTDM_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------- preprocess --
+// Pillow's antialiased BILINEAR resize for 8-bit images (Resample.c:
+// precompute_coeffs + normalize_coeffs_8bpc, horizontal pass then vertical
+// pass, PRECISION_BITS = 22, clip8), as torchvision.transforms.Resize calls
+// it, followed by CenterCrop, ToTensor and Normalize (aider.py:421-426).
+static constexpr int kPrecisionBits = 32 - 8 - 2;
+
+static int precompute_coeffs(int in_size, int out_size, std::vector<int>& bounds, std::vector<double>& kk) {
+  const double in0 = 0.0, in1 = (double)(float)in_size;
+  double scale = (in1 - in0) / out_size;
+  double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 1.0 * filterscale;  // bilinear support = 1
+  const int ksize = (int)std::ceil(support) * 2 + 1;
+  bounds.assign(out_size * 2, 0);
+  kk.assign((size_t)out_size * ksize, 0.0);
+  for (int xx = 0; xx < out_size; ++xx) {
+    const double center = in0 + (xx + 0.5) * scale;
+    double ww = 0.0;
+    const double ss = 1.0 / filterscale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    double* k = &kk[(size_t)xx * ksize];
+    for (int x = 0; x < xmax; ++x) {
+      double t = (x + xmin - center + 0.5) * ss;
+      if (t < 0.0) t = -t;
+      const double wv = t < 1.0 ? 1.0 - t : 0.0;
+      k[x] = wv;
+      ww += wv;
+    }
+    for (int x = 0; x < xmax; ++x)
+      if (ww != 0.0) k[x] /= ww;
+    bounds[xx * 2 + 0] = xmin;
+    bounds[xx * 2 + 1] = xmax;
+  }
+  return ksize;
+}
+
+static std::vector<int> normalize_coeffs_8bpc(const std::vector<double>& kk) {
+  std::vector<int> out(kk.size());
+  for (size_t i = 0; i < kk.size(); ++i) {
+    const double v = kk[i] * (double)(1 << kPrecisionBits);
+    out[i] = kk[i] < 0 ? (int)(-0.5 + v) : (int)(0.5 + v);
+  }
+  return out;
+}
+
+void build_resize_plan(ResizePlan& p, int in_h, int in_w, int out_size, bool upload) {
+  RTDM_REQUIRE(in_h > 0 && in_w > 0 && out_size > 0, RTDM_E_INVALID, "preprocess: bad sizes");
+  p.in_h = in_h;
+  p.in_w = in_w;
+  p.out = out_size;
+  // torchvision Resize(int): shorter side -> size, long side int(size * long / short)
+  const int size = (int)(out_size * 1.14);
+  if (in_w <= in_h) {
+    p.rs_w = size;
+    p.rs_h = (int)((double)size * in_h / in_w);
+  } else {
+    p.rs_h = size;
+    p.rs_w = (int)((double)size * in_w / in_h);
+  }
+  RTDM_REQUIRE(p.rs_h >= out_size && p.rs_w >= out_size, RTDM_E_INVALID, "preprocess: crop larger than image");
+  // CenterCrop: int(round((dim - crop) / 2.))  (Python round = half to even)
+  auto pyround_half = [](int twice) {  // round(twice / 2)
+    if (twice % 2 == 0) return twice / 2;
+    const int lo = twice / 2;  // x.5 -> even
+    return (lo % 2 == 0) ? lo : lo + 1;
+  };
+  p.crop_top = pyround_half(p.rs_h - out_size);
+  p.crop_left = pyround_half(p.rs_w - out_size);
+
+  std::vector<int> bh, bv;
+  std::vector<double> kh, kv;
+  const bool need_h = p.rs_w != in_w;
+  const bool need_v = p.rs_h != in_h;
+  if (need_h) {
+    p.ksize_h = precompute_coeffs(in_w, p.rs_w, bh, kh);
+  } else {  // identity pass: one tap of weight 1
+    p.ksize_h = 1;
+    bh.resize(p.rs_w * 2);
+    kh.assign(p.rs_w, 1.0);
+    for (int x = 0; x < p.rs_w; ++x) { bh[2 * x] = x; bh[2 * x + 1] = 1; }
+  }
+  if (need_v) {
+    p.ksize_v = precompute_coeffs(in_h, p.rs_h, bv, kv);
+  } else {
+    p.ksize_v = 1;
+    bv.resize(p.rs_h * 2);
+    kv.assign(p.rs_h, 1.0);
+    for (int y = 0; y < p.rs_h; ++y) { bv[2 * y] = y; bv[2 * y + 1] = 1; }
+  }
+  // restrict to the crop window
+  std::vector<int> ch(out_size * 2), cv(out_size * 2);
+  std::vector<int> kh8 = normalize_coeffs_8bpc(kh), kv8 = normalize_coeffs_8bpc(kv);
+  std::vector<int> kch((size_t)out_size * p.ksize_h), kcv((size_t)out_size * p.ksize_v);
+  int rmin = 1 << 30, rmax = 0;
+  for (int i = 0; i < out_size; ++i) {
+    const int x = p.crop_left + i;
+    ch[2 * i] = bh[2 * x];
+    ch[2 * i + 1] = bh[2 * x + 1];
+    for (int k = 0; k < p.ksize_h; ++k) kch[(size_t)i * p.ksize_h + k] = kh8[(size_t)x * p.ksize_h + k];
+    const int y = p.crop_top + i;
+    cv[2 * i] = bv[2 * y];
+    cv[2 * i + 1] = bv[2 * y + 1];
+    for (int k = 0; k < p.ksize_v; ++k) kcv[(size_t)i * p.ksize_v + k] = kv8[(size_t)y * p.ksize_v + k];
+    rmin = std::min(rmin, bv[2 * y]);
+    rmax = std::max(rmax, bv[2 * y] + bv[2 * y + 1]);
+  }
+  p.row_first = rmin;
+  p.rows = rmax - rmin;
+  for (int i = 0; i < out_size; ++i) cv[2 * i] -= rmin;
+  if (!upload) return;
+  auto up = [](DevBuf& d, const std::vector<int>& v) {
+    d.alloc(v.size() * sizeof(int));
+    RTDM_HIP(hipMemcpy(d.p, v.data(), v.size() * sizeof(int), hipMemcpyHostToDevice));
+  };
+  up(p.bounds_h, ch);
+  up(p.coef_h, kch);
+  up(p.bounds_v, cv);
+  up(p.coef_v, kcv);
+}
+
+__device__ __forceinline__ int clip8(int v) {
+  v >>= kPrecisionBits;
+  return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+// horizontal pass: frames [n,in_h,in_w,3] -> tmp [n,rows,out,3] (crop columns only)
+__global__ __launch_bounds__(256) void resize_h_kernel(const uint8_t* __restrict__ frames, int n, int in_h, int in_w,
+                                                       int row_first, int rows, int out, int ksize,
+                                                       const int* __restrict__ bounds, const int* __restrict__ coef,
+                                                       uint8_t* __restrict__ tmp) {
+  const int64_t total = (int64_t)n * rows * out;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int xx = (int)(idx % out);
+    int64_t p = idx / out;
+    const int r = (int)(p % rows);
+    const int b = (int)(p / rows);
+    const int xmin = bounds[2 * xx], xmax = bounds[2 * xx + 1];
+    const int* k = coef + (size_t)xx * ksize;
+    const uint8_t* src = frames + (((size_t)b * in_h + row_first + r) * in_w + xmin) * 3;
+    int s0 = 1 << (kPrecisionBits - 1), s1 = s0, s2 = s0;
+    for (int x = 0; x < xmax; ++x) {
+      s0 += src[x * 3 + 0] * k[x];
+      s1 += src[x * 3 + 1] * k[x];
+      s2 += src[x * 3 + 2] * k[x];
+    }
+    uint8_t* dst = tmp + idx * 3;
+    dst[0] = (uint8_t)clip8(s0);
+    dst[1] = (uint8_t)clip8(s1);
+    dst[2] = (uint8_t)clip8(s2);
+  }
+}
+
+// vertical pass + ToTensor + Normalize: tmp -> out [n,out,out,3] NHWC (dtype) or NCHW f32
+template <typename T>
+__global__ __launch_bounds__(256) void resize_v_kernel(const uint8_t* __restrict__ tmp, int n, int rows, int out,
+                                                       int ksize, const int* __restrict__ bounds,
+                                                       const int* __restrict__ coef, T* __restrict__ dst, int nchw) {
+  const float mean[3] = {0.485f, 0.456f, 0.406f};
+  const float stdv[3] = {0.229f, 0.224f, 0.225f};
+  const int64_t total = (int64_t)n * out * out;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int xx = (int)(idx % out);
+    int64_t p = idx / out;
+    const int yy = (int)(p % out);
+    const int b = (int)(p / out);
+    const int ymin = bounds[2 * yy], ymax = bounds[2 * yy + 1];
+    const int* k = coef + (size_t)yy * ksize;
+    int s[3] = {1 << (kPrecisionBits - 1), 1 << (kPrecisionBits - 1), 1 << (kPrecisionBits - 1)};
+    for (int y = 0; y < ymax; ++y) {
+      const uint8_t* src = tmp + (((size_t)b * rows + ymin + y) * out + xx) * 3;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) s[ch] += src[ch] * k[y];
+    }
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float v = ((float)clip8(s[ch]) / 255.f - mean[ch]) / stdv[ch];
+      if (nchw)
+        dst[(((size_t)b * 3 + ch) * out + yy) * out + xx] = (T)v;
+      else
+        dst[idx * 3 + ch] = (T)v;
+    }
+  }
+}
+
+void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_t* tmp, void* out, int out_layout,
+                       int dtype, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t th = (int64_t)n * p.rows * p.out;
+  hipLaunchKernelGGL(resize_h_kernel, dim3(grid_for(th, 256)), dim3(256), 0, s, frames, n, p.in_h, p.in_w,
+                     p.row_first, p.rows, p.out, p.ksize_h, p.bounds_h.as<int>(), p.coef_h.as<int>(), tmp);
+  const int64_t tv = (int64_t)n * p.out * p.out;
+  if (out_layout == 1 || dtype == RTDM_F32)
+    hipLaunchKernelGGL(resize_v_kernel<float>, dim3(grid_for(tv, 256)), dim3(256), 0, s, tmp, n, p.rows, p.out,
+                       p.ksize_v, p.bounds_v.as<int>(), p.coef_v.as<int>(), (float*)out, out_layout == 1 ? 1 : 0);
+  else
+    hipLaunchKernelGGL(resize_v_kernel<_Float16>, dim3(grid_for(tv, 256)), dim3(256), 0, s, tmp, n, p.rows, p.out,
+                       p.ksize_v, p.bounds_v.as<int>(), p.coef_v.as<int>(), (_Float16*)out, 0);
+  RTDM_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------ YOLO decode --
+// YOLOLayer inference branch (models.py:252-258) on a raw NCHW head map.
+__global__ __launch_bounds__(256) void yolo_decode_kernel(const float* __restrict__ p, int n, int na, int no, int ny,
+                                                          int nx, const float* __restrict__ anchor_vec, float ystride,
+                                                          float* __restrict__ io, int io_rows, int row_off) {
+  const int64_t total = (int64_t)n * na * ny * nx * no;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(idx % no);
+    int64_t q = idx / no;
+    const int x = (int)(q % nx);
+    q /= nx;
+    const int y = (int)(q % ny);
+    q /= ny;
+    const int a = (int)(q % na);
+    const int b = (int)(q / na);
+    const float v = p[((((size_t)b * na + a) * no + k) * ny + y) * nx + x];
+    float o;
+    if (k < 2)
+      o = (1.f / (1.f + expf(-v)) + (float)(k == 0 ? x : y)) * ystride;
+    else if (k < 4)
+      o = (expf(v) * anchor_vec[2 * a + (k - 2)]) * ystride;
+    else
+      o = 1.f / (1.f + expf(-v));
+    const size_t row = (size_t)row_off + ((size_t)a * ny + y) * nx + x;
+    io[((size_t)b * io_rows + row) * no + k] = o;
+  }
+}
+
+void launch_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const float* anchor_vec, float ystride,
+                        float* io, int io_rows, int row_off, hipStream_t s) {
+  const int64_t total = (int64_t)n * na * ny * nx * no;
+  if (total <= 0) return;
+  hipLaunchKernelGGL(yolo_decode_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, p, n, na, no, ny, nx,
+                     anchor_vec, ystride, io, io_rows, row_off);
+  RTDM_HIP(hipGetLastError());
+}
+
+// -------------------------------------------------------------------- NMS --
+// non_max_suppression (utils.py:488-557, method 'vision_batch') with the
+// greedy kernel of torchvision.ops.boxes.nms (CPU: descending score order,
+// IoU = inter / (area_i + area_j - inter) in fp32, suppress if IoU > thr with
+// the fp32 IoU promoted to double).  One 1024-thread workgroup per image.
+//
+// Candidate key = (~score_bits << 32) | (anchor * nc + class): ascending key
+// order = descending score, ties -> lower (anchor, class) index, which is the
+// row-major order of the reference's multi-label expansion (utils.py:524).
+static constexpr int kNmsThreads = 1024;
+static constexpr int kNmsLdsCap = 4096;
+
+struct NmsWs {  // per-image slice of the workspace
+  uint64_t* keys;
+  float4* box;
+  float* area;
+  uint32_t* supp;
+  int* keep;
+};
+
+static inline size_t nms_cap(int n_anchors, int nc) {
+  size_t c = 1;
+  while (c < (size_t)n_anchors * (size_t)(nc > 1 ? nc : 1)) c <<= 1;
+  return c < 64 ? 64 : c;
+}
+
+size_t nms_workspace_size(int n, int n_anchors, int nc) {
+  const size_t cap = nms_cap(n_anchors, nc);
+  const size_t per = cap * (8 + 16 + 4 + 4) + (cap / 32 + 1) * 4 + 256;
+  return per * (size_t)n;
+}
+
+__device__ __forceinline__ NmsWs nms_ws(void* ws, int img, size_t cap) {
+  const size_t per = cap * (8 + 16 + 4 + 4) + (cap / 32 + 1) * 4 + 256;
+  char* base = (char*)ws + per * img;
+  NmsWs w;
+  w.keys = (uint64_t*)base;
+  w.box = (float4*)(base + cap * 8);
+  w.area = (float*)(base + cap * 24);
+  w.keep = (int*)(base + cap * 28);
+  w.supp = (uint32_t*)(base + cap * 32);
+  return w;
+}
+
+__global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restrict__ io, int n_anchors, int no,
+                                                          float conf, double iou_thr, int multi_label, int agnostic,
+                                                          uint64_t class_mask, int max_det, void* ws, size_t cap,
+                                                          float* __restrict__ det, int32_t* __restrict__ idx_out,
+                                                          int32_t* __restrict__ count) {
+#pragma clang fp contract(off)
+  __shared__ uint64_t s_keys[kNmsLdsCap];
+  __shared__ float4 s_box[kNmsLdsCap];
+  __shared__ float s_area[kNmsLdsCap];
+  __shared__ uint32_t s_supp[kNmsLdsCap / 32];
+  __shared__ int s_n;
+  const int img = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int nc = no - 5;
+  const bool ml = multi_label && nc > 1;
+  const float* P = io + (size_t)img * n_anchors * no;
+  NmsWs g = nms_ws(ws, img, cap);
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+
+  // 1. candidates (utils.py:505-536)
+  for (int a = tid; a < n_anchors; a += kNmsThreads) {
+    const float* r = P + (size_t)a * no;
+    const float obj = r[4];
+    if (!(obj > conf)) continue;
+    const float w = r[2], h = r[3];
+    if (!((w > 2.f) && (h > 2.f) && (w < 4096.f) && (h < 4096.f))) continue;
+    const float x = r[0], y = r[1];
+    const float hw = w / 2.f, hh = h / 2.f;
+    const bool box_finite = isfinite(x - hw) && isfinite(y - hh) && isfinite(x + hw) && isfinite(y + hh);
+    if (ml) {
+      for (int j = 0; j < nc; ++j) {
+        const float sc = r[5 + j] * obj;
+        if (!(sc > conf)) continue;
+        if (!((class_mask >> (j & 63)) & 1ull)) continue;
+        if (!box_finite || !isfinite(sc)) continue;
+        const int pos = atomicAdd(&s_n, 1);
+        g.keys[pos] = ((uint64_t)(~__float_as_uint(sc)) << 32) | (uint32_t)(a * nc + j);
+      }
+    } else {
+      float best = r[5] * obj;
+      int bj = 0;
+      for (int j = 1; j < nc; ++j) {
+        const float sc = r[5 + j] * obj;
+        if (sc > best) { best = sc; bj = j; }
+      }
+      if (!((class_mask >> (bj & 63)) & 1ull)) continue;
+      if (!box_finite || !isfinite(best)) continue;
+      const int pos = atomicAdd(&s_n, 1);
+      g.keys[pos] = ((uint64_t)(~__float_as_uint(best)) << 32) | (uint32_t)(a * (nc > 1 ? nc : 1) + bj);
+    }
+  }
+  __syncthreads();
+  const int n = s_n;
+  int npow = 1;
+  while (npow < n) npow <<= 1;
+  const bool lds = npow <= kNmsLdsCap;
+  uint64_t* K = lds ? s_keys : g.keys;
+  for (int i = tid; i < npow; i += kNmsThreads) {
+    uint64_t v = i < n ? g.keys[i] : ~0ull;
+    if (lds) s_keys[i] = v;
+    else if (i >= n) g.keys[i] = v;
+  }
+  __syncthreads();
+
+  // 2. bitonic sort, ascending key
+  for (int k = 2; k <= npow; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < npow; i += kNmsThreads) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = K[i], b = K[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            K[i] = b;
+            K[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // 3. offset boxes + areas (utils.py:547-552; torchvision areas)
+  float4* B = lds ? s_box : g.box;
+  float* A = lds ? s_area : g.area;
+  uint32_t* S = lds ? s_supp : g.supp;
+  const int cls_div = nc > 1 ? nc : 1;
+  for (int i = tid; i < n; i += kNmsThreads) {
+    const uint32_t cand = (uint32_t)K[i];
+    const int a = cand / cls_div, j = cand - (cand / cls_div) * cls_div;
+    const float* r = P + (size_t)a * no;
+    const float x = r[0], y = r[1], w = r[2], h = r[3];
+    const float off = agnostic ? 0.f : (float)j * 4096.f;
+    float4 bx;
+    bx.x = (x - w / 2.f) + off;
+    bx.y = (y - h / 2.f) + off;
+    bx.z = (x + w / 2.f) + off;
+    bx.w = (y + h / 2.f) + off;
+    B[i] = bx;
+    A[i] = (bx.z - bx.x) * (bx.w - bx.y);
+  }
+  for (int i = tid; i < (n + 31) / 32; i += kNmsThreads) S[i] = 0u;
+  __syncthreads();
+
+  // 4. greedy suppression
+  int nkeep = 0;
+  for (int i = 0; i < n; ++i) {
+    if ((S[i >> 5] >> (i & 31)) & 1u) continue;
+    if (tid == 0) g.keep[nkeep] = i;
+    ++nkeep;
+    const float4 bi = B[i];
+    const float ai = A[i];
+    for (int j = i + 1 + tid; j < n; j += kNmsThreads) {
+      if ((S[j >> 5] >> (j & 31)) & 1u) continue;
+      const float4 bj = B[j];
+      const float xx1 = fmaxf(bi.x, bj.x);
+      const float yy1 = fmaxf(bi.y, bj.y);
+      const float xx2 = fminf(bi.z, bj.z);
+      const float yy2 = fminf(bi.w, bj.w);
+      const float w = fmaxf(0.f, xx2 - xx1);
+      const float h = fmaxf(0.f, yy2 - yy1);
+      const float inter = w * h;
+      const float ovr = inter / ((ai + A[j]) - inter);
+      if ((double)ovr > iou_thr) atomicOr(&S[j >> 5], 1u << (j & 31));
+    }
+    __syncthreads();
+  }
+
+  // 5. rows [x1,y1,x2,y2,conf,cls] in kept (descending score) order
+  const int nout = nkeep < max_det ? nkeep : max_det;
+  for (int r = tid; r < nout; r += kNmsThreads) {
+    const int i = g.keep[r];
+    const uint64_t key = K[i];
+    const uint32_t cand = (uint32_t)key;
+    const int a = cand / cls_div, j = cand - (cand / cls_div) * cls_div;
+    const float* rr = P + (size_t)a * no;
+    const float x = rr[0], y = rr[1], w = rr[2], h = rr[3];
+    float* d = det + ((size_t)img * max_det + r) * 6;
+    d[0] = x - w / 2.f;
+    d[1] = y - h / 2.f;
+    d[2] = x + w / 2.f;
+    d[3] = y + h / 2.f;
+    d[4] = __uint_as_float(~(uint32_t)(key >> 32));
+    d[5] = (float)j;
+    if (idx_out) {
+      idx_out[((size_t)img * max_det + r) * 2 + 0] = a;
+      idx_out[((size_t)img * max_det + r) * 2 + 1] = j;
+    }
+  }
+  if (tid == 0) count[img] = nkeep;
+}
+
+void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label, int agnostic,
+                uint64_t class_mask, int max_det, void* ws, float* det, int32_t* idx, int32_t* count,
+                hipStream_t s) {
+  if (n <= 0) return;
+  RTDM_REQUIRE(no >= 6, RTDM_E_INVALID, "nms: no must be >= 6 (5 + nc)");
+  RTDM_REQUIRE(max_det >= 0, RTDM_E_INVALID, "nms: max_det < 0");
+  const size_t cap = nms_cap(n_anchors, no - 5);
+  hipLaunchKernelGGL(nms_kernel, dim3(n), dim3(kNmsThreads), 0, s, io, n_anchors, no, conf, iou, multi_label,
+                     agnostic, class_mask, max_det, ws, cap, det, idx, count);
+  RTDM_HIP(hipGetLastError());
+}
+
+}  // namespace rtdm

@@ -1,0 +1,200 @@
+"""ACFF classifiers (Squeeze-ErNET, Squeeze-ErNET-RedConv, ErNET) on the HIP runtime.
+
+Drop-in for disaster_detection/model/{squeeze_ernet,squeeze_ernet_redconv,ernet}.py
+and the CLIs' ``load_model`` (aider-predict.py:22-45): same class names, same
+state_dict keys, ``model(x)`` returns the [N, 5] softmax the reference returns.
+The forward runs entirely in librtdm.so (rtdm_classify); nothing here computes.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .synth import classifier_param_shapes
+
+CLASSES = ['collapsed building', 'fire', 'flooded areas', 'normal', 'traffic incident']  # aider-predict.py:83
+
+_KINDS = {"squeeze-ernet": L.RTDM_SQUEEZE_ERNET, "squeeze-redconv": L.RTDM_SQUEEZE_REDCONV, "ernet": L.RTDM_ERNET}
+
+
+def _to_numpy_sd(sd) -> dict:
+    out = {}
+    for k, v in sd.items():
+        if k.endswith("num_batches_tracked"):
+            continue
+        if isinstance(v, torch.Tensor):
+            v = v.detach().to("cpu", torch.float32).numpy()
+        out[k] = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
+    return out
+
+
+class _ACFFClassifier(torch.nn.Module):
+    MODEL = ""
+    INPUT = 140
+
+    def __init__(self):
+        super().__init__()
+        self._params = None
+        self._handle = None
+        self._handle_key = None
+        self._dtype = L.RTDM_F32
+        self.logits = None  # fc output of the last forward (pre-softmax)
+
+    # ---------------------------------------------------------------- weights --
+    def load_state_dict(self, state_dict, strict: bool = True):
+        sd = _to_numpy_sd(state_dict)
+        shapes = classifier_param_shapes(self.MODEL)
+        missing = [k for k in shapes if k not in sd]
+        unexpected = [k for k in sd if k not in shapes]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"Error(s) in loading state_dict for {type(self).__name__}: "
+                               f"missing {missing}, unexpected {unexpected}")
+        for k, shp in shapes.items():
+            if k in sd and tuple(sd[k].shape) != tuple(shp):
+                raise RuntimeError(f"size mismatch for {k}: checkpoint {tuple(sd[k].shape)}, model {tuple(shp)}")
+        self._params = {k: sd[k] for k in shapes if k in sd}
+        self._release()
+        return torch.nn.modules.module._IncompatibleKeys(missing, unexpected)
+
+    def state_dict(self, *args, **kwargs):
+        return {k: torch.from_numpy(v.copy()) for k, v in (self._params or {}).items()}
+
+    # ------------------------------------------------------------- precision --
+    def half(self):
+        self._dtype = L.RTDM_F16
+        self._release()
+        return self
+
+    def float(self):
+        self._dtype = L.RTDM_F32
+        self._release()
+        return self
+
+    def _release(self):
+        if self._handle is not None:
+            L.lib().rtdm_classifier_destroy(self._handle)
+            self._handle = None
+            self._handle_key = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    def _get_handle(self, n: int):
+        if self._params is None:
+            raise RuntimeError(f"{type(self).__name__}: load_state_dict() before calling the model")
+        dev = torch.cuda.current_device()
+        cap = max(64, 1 << max(0, int(n - 1).bit_length()))
+        key = (dev, self._dtype)
+        if self._handle is not None and self._handle_key[0] == key and self._handle_key[1] >= n:
+            return self._handle
+        self._release()
+        names = list(self._params.keys())
+        arr = (L.rtdm_param * len(names))()
+        keep = []
+        for i, k in enumerate(names):
+            a = self._params[k]
+            keep.append(a)
+            arr[i].name = k.encode()
+            arr[i].data = a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+            arr[i].numel = a.size
+        h = ctypes.c_void_p()
+        L.check(L.lib().rtdm_classifier_create(_KINDS[self.MODEL], self._dtype, arr, len(names), cap,
+                                               ctypes.byref(h)))
+        self._handle = h
+        self._handle_key = (key, cap)
+        return h
+
+    # ---------------------------------------------------------------- forward --
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """x: [N,3,S,S] fp32/fp16 CUDA tensor (the transformed image batch) -> softmax [N,5]."""
+        if not x.is_cuda:
+            raise RuntimeError("rtdm classifier runs on the GPU: move the input to a cuda device")
+        if x.dim() != 4 or x.shape[1] != 3 or x.shape[2] != self.INPUT or x.shape[3] != self.INPUT:
+            raise ValueError(f"{type(self).__name__} expects [N,3,{self.INPUT},{self.INPUT}] input, got "
+                             f"{list(x.shape)} (the reference silently regroups rows for other sizes; "
+                             f"not reproduced)")
+        if x.dtype == torch.float32:
+            kind = L.RTDM_INPUT_NCHW_F32
+        elif x.dtype == torch.float16:
+            kind = L.RTDM_INPUT_NCHW_F16
+        else:
+            raise TypeError("input must be float32 or float16")
+        x = x.contiguous()
+        return self._run(x, kind, x.shape[0], self.INPUT, self.INPUT)
+
+    def classify_frames(self, frames: torch.Tensor) -> torch.Tensor:
+        """frames: [N,H,W,3] uint8 RGB CUDA tensor; runs the CLI transform (aider.py:421-426) on
+        device, then the model.  Returns softmax [N,5]; logits in self.logits."""
+        if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3:
+            raise ValueError("frames must be uint8 [N,H,W,3]")
+        frames = frames.contiguous()
+        return self._run(frames, L.RTDM_INPUT_FRAME_U8, frames.shape[0], frames.shape[1], frames.shape[2])
+
+    def _run(self, x, kind, n, h, w, stream=None):
+        with torch.cuda.device(x.device):
+            handle = self._get_handle(n)
+            logits = torch.empty((n, 5), device=x.device, dtype=torch.float32)
+            probs = torch.empty((n, 5), device=x.device, dtype=torch.float32)
+            L.check(L.lib().rtdm_classify(handle, L.ptr(x), kind, n, h, w, L.ptr(logits), L.ptr(probs),
+                                          L.stream_ptr(stream)))
+        self.logits = logits
+        return probs
+
+
+class Squeeze_ErNET(_ACFFClassifier):
+    """disaster_detection/model/squeeze_ernet.py:7 — 140x140 input."""
+    MODEL = "squeeze-ernet"
+    INPUT = 140
+
+
+class Squeeze_RedConv(_ACFFClassifier):
+    """disaster_detection/model/squeeze_ernet_redconv.py:7 — 140x140 input."""
+    MODEL = "squeeze-redconv"
+    INPUT = 140
+
+
+class ErNET(_ACFFClassifier):
+    """disaster_detection/model/ernet.py:6 — 240x240 input."""
+    MODEL = "ernet"
+    INPUT = 240
+
+
+def build_model(model_name: str) -> _ACFFClassifier:
+    if model_name == "ernet":
+        return ErNET()
+    if model_name == "squeeze-ernet":
+        return Squeeze_ErNET()
+    if model_name == "squeeze-redconv":
+        return Squeeze_RedConv()
+    raise ValueError(f"Unsupported model: {model_name}")
+
+
+def read_weights(weights_path: str) -> dict:
+    """State dict from a reference checkpoint: plain state dict or {'model_state_dict': ...}
+    (.pt via torch.load(weights_only=True)), or an .npz of arrays."""
+    if not os.path.exists(weights_path):
+        raise FileNotFoundError(f"No weights found at {weights_path}")
+    if weights_path.endswith(".npz"):
+        z = np.load(weights_path, allow_pickle=False)
+        return {k: z[k] for k in z.files}
+    ckpt = torch.load(weights_path, map_location="cpu", weights_only=True)
+    if isinstance(ckpt, dict) and "model_state_dict" in ckpt:
+        return ckpt["model_state_dict"]
+    return ckpt
+
+
+def load_model(model_name: str, weights_path: str, device: torch.device, half: bool = False) -> _ACFFClassifier:
+    """aider-predict.py:22-45 / evaluate-classification-metrics.py:24-47 counterpart."""
+    model = build_model(model_name)
+    model.load_state_dict(read_weights(weights_path))
+    if half:
+        model.half()
+    model.eval()
+    return model

@@ -1,0 +1,211 @@
+"""Deterministic synthetic inputs and weights (no network: no datasets, no checkpoints).
+
+* ``synth_frames``: uint8 RGB aerial-like frames [n, h, w, 3] — smooth random
+  terrain + random rectangles ("buildings / vehicles") + sensor noise.  Frame i of
+  a global batch depends only on (seed, i), so any frame sharding reproduces the
+  same global batch.
+* ``synth_darknet_weights``: a darknet weight stream (load_darknet_weights order,
+  victim_localization/yolov3/models.py:449-486) for a cfg: He-scaled conv
+  weights, BN gamma=1/beta=0 with running statistics calibrated once on
+  synthetic frames (``data/synth_<cfg>.npz``, produced by
+  tests/golden/make_synth.py from the reference model itself) so activations stay
+  O(1), and head objectness biases set for a realistic detection rate.
+* ``synth_classifier_state_dict``: random-init state dict of the ACFF models.
+"""
+from __future__ import annotations
+
+import os
+import re
+
+import numpy as np
+
+DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+BASE_SEED = 20251015
+
+
+def synth_frames(n: int, h: int, w: int, seed: int = BASE_SEED, first: int = 0) -> np.ndarray:
+    out = np.empty((n, h, w, 3), np.uint8)
+    for k in range(n):
+        rng = np.random.default_rng(seed + first + k)
+        # low-frequency terrain: bilinear upsample of a coarse random grid per channel
+        gh, gw = max(2, h // 64), max(2, w // 64)
+        coarse = rng.uniform(40, 200, size=(gh, gw, 3)).astype(np.float32)
+        ys = np.linspace(0, gh - 1, h, dtype=np.float32)
+        xs = np.linspace(0, gw - 1, w, dtype=np.float32)
+        y0 = np.floor(ys).astype(int).clip(0, gh - 2)
+        x0 = np.floor(xs).astype(int).clip(0, gw - 2)
+        fy = (ys - y0)[:, None, None]
+        fx = (xs - x0)[None, :, None]
+        a = coarse[y0][:, x0]
+        b = coarse[y0][:, x0 + 1]
+        c = coarse[y0 + 1][:, x0]
+        d = coarse[y0 + 1][:, x0 + 1]
+        img = (a * (1 - fy) * (1 - fx) + b * (1 - fy) * fx + c * fy * (1 - fx) + d * fy * fx)
+        # objects
+        for _ in range(int(rng.integers(8, 24))):
+            oh, ow = int(rng.integers(6, max(7, h // 8))), int(rng.integers(6, max(7, w // 8)))
+            oy, ox = int(rng.integers(0, h - oh)), int(rng.integers(0, w - ow))
+            img[oy:oy + oh, ox:ox + ow] = rng.uniform(0, 255, size=3)
+        img += rng.normal(0, 6, size=img.shape).astype(np.float32)
+        out[k] = np.clip(img, 0, 255).astype(np.uint8)
+    return out
+
+
+# ------------------------------------------------------------------ darknet --
+def parse_cfg_text(text: str):
+    """parse_model_cfg (yolov3/utils/parse_config.py:6-52) on cfg text."""
+    lines = [x for x in text.split("\n") if x and not x.startswith("#")]
+    lines = [x.strip() for x in lines]
+    mdefs = []
+    for line in lines:
+        if not line:
+            continue
+        if line.startswith("["):
+            mdefs.append({"type": line[1:-1].rstrip()})
+            if mdefs[-1]["type"] == "convolutional":
+                mdefs[-1]["batch_normalize"] = 0
+        else:
+            key, val = line.split("=")
+            key = key.rstrip()
+            if key == "anchors":
+                mdefs[-1][key] = np.array([float(x) for x in val.split(",")]).reshape((-1, 2))
+            elif key in ("from", "layers", "mask"):
+                mdefs[-1][key] = [int(x) for x in val.split(",")]
+            else:
+                val = val.strip()
+                if val.isnumeric():
+                    mdefs[-1][key] = int(val) if (int(val) - float(val)) == 0 else float(val)
+                else:
+                    mdefs[-1][key] = val
+    return mdefs
+
+
+def conv_layers(cfg_text: str):
+    """[(layer_idx, cin, cout, k, bn, head_no)] in weight-stream order (head_no = nc+5 for a
+    conv feeding a [yolo] layer, else 0)."""
+    mdefs = parse_cfg_text(cfg_text)
+    net = mdefs.pop(0)
+    filters_out = [int(net.get("channels", 3))]
+    convs = []
+    for i, m in enumerate(mdefs):
+        t = m["type"]
+        if t == "convolutional":
+            f = int(m["filters"])
+            nxt = mdefs[i + 1] if i + 1 < len(mdefs) else {"type": ""}
+            head_no = int(nxt["classes"]) + 5 if nxt["type"] == "yolo" else 0
+            convs.append((i, filters_out[-1], f, int(m["size"]), int(m["batch_normalize"]), head_no))
+        elif t == "route":
+            f = sum(filters_out[l + 1 if l > 0 else l] for l in m["layers"])
+        elif t in ("shortcut", "maxpool", "upsample", "yolo"):
+            f = filters_out[-1]
+        else:
+            raise ValueError(f"unsupported layer type {t}")
+        filters_out.append(f)
+    return convs
+
+
+def cfg_name(cfg_path_or_name: str) -> str:
+    return re.sub(r"\.cfg$", "", os.path.basename(cfg_path_or_name))
+
+
+def load_calibration(name: str):
+    path = os.path.join(DATA_DIR, f"synth_{name}.npz")
+    if not os.path.exists(path):
+        return None
+    z = np.load(path, allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def synth_darknet_weights(cfg_text: str, seed: int = 7, calib: dict | None = None,
+                          obj_bias: float = -3.5) -> np.ndarray:
+    """Float32 darknet weight stream (after the 20-byte header) for cfg_text."""
+    rng = np.random.default_rng(seed)
+    parts = []
+    for (i, cin, cout, k, bn, head) in conv_layers(cfg_text):
+        fan_in = cin * k * k
+        w = rng.standard_normal((cout, cin, k, k), dtype=np.float32) * np.float32(np.sqrt(2.0 / fan_in))
+        if bn:
+            beta = np.zeros(cout, np.float32)
+            gamma = np.ones(cout, np.float32)
+            mean = np.zeros(cout, np.float32)
+            var = np.ones(cout, np.float32)
+            if calib is not None and f"mean{i}" in calib:
+                mean = calib[f"mean{i}"].astype(np.float32)
+                var = calib[f"var{i}"].astype(np.float32)
+            parts += [beta, gamma, mean, var]
+        else:
+            bias = np.zeros(cout, np.float32)
+            if head:
+                w *= np.float32(np.sqrt(0.5))  # head: unit-variance logits
+                ob = float(calib[f"objbias{i}"]) if calib is not None and f"objbias{i}" in calib else obj_bias
+                for a in range(cout // head):
+                    bias[a * head + 4] = ob
+            parts.append(bias)
+        parts.append(w.reshape(-1))
+    return np.concatenate(parts).astype(np.float32)
+
+
+def write_darknet_weights(path: str, stream: np.ndarray) -> None:
+    """models.py:489-512 format: int32[3] version, int64 seen, float32 stream."""
+    with open(path, "wb") as f:
+        np.array([0, 2, 5], dtype=np.int32).tofile(f)
+        np.array([0], dtype=np.int64).tofile(f)
+        np.asarray(stream, np.float32).tofile(f)
+
+
+def read_darknet_weights(path: str) -> np.ndarray:
+    """load_darknet_weights header handling (models.py:449-455)."""
+    with open(path, "rb") as f:
+        np.fromfile(f, dtype=np.int32, count=3)
+        np.fromfile(f, dtype=np.int64, count=1)
+        return np.fromfile(f, dtype=np.float32)
+
+
+# --------------------------------------------------------------- classifier --
+def classifier_param_shapes(kind: str):
+    """state_dict key -> shape for 'squeeze-ernet' | 'squeeze-redconv' | 'ernet'."""
+    shapes = {"conv1.weight": (16, 3, 3, 3)}
+    if kind == "squeeze-ernet":
+        blocks = [("acff1", 16, 64), ("acff2", 64, 96), ("acff3", 96, 128), ("acff4", 128, 256)]
+        fc_in = 20
+    elif kind == "squeeze-redconv":
+        blocks = [("acff1", 8, 64), ("acff2", 64, 96), ("acff3", 48, 128), ("acff4", 64, 256)]
+        shapes.update({"conv_red1.weight": (8, 16, 1, 1), "conv_red1.bias": (8,),
+                       "conv_red2.weight": (48, 96, 1, 1), "conv_red2.bias": (48,),
+                       "conv_red3.weight": (64, 128, 1, 1), "conv_red3.bias": (64,)})
+        fc_in = 20
+    elif kind == "ernet":
+        blocks = [("acff1", 16, 64), ("acff2", 64, 96), ("acff3", 96, 128), ("acff4", 128, 128),
+                  ("acff5", 128, 128), ("acff6", 128, 256)]
+        fc_in = 45
+    else:
+        raise ValueError(f"Unsupported model: {kind}")
+    for name, cin, cout in blocks:
+        for b in (1, 2, 3):
+            shapes[f"{name}.conv{b}.weight"] = (cin, 1, 3, 3)
+            shapes[f"{name}.conv{b}.bias"] = (cin,)
+        shapes[f"{name}.fused_conv.weight"] = (cout, 3 * cin, 1, 1)
+        shapes[f"{name}.fused_conv.bias"] = (cout,)
+        for k in ("weight", "bias", "running_mean", "running_var"):
+            shapes[f"{name}.batch_norm.{k}"] = (cout,)
+    shapes["conv2.weight"] = (5, 256, 1, 1)
+    shapes["fc.weight"] = (5, fc_in)
+    shapes["fc.bias"] = (5,)
+    return shapes
+
+
+def synth_classifier_state_dict(kind: str, seed: int = 11):
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for k, shp in classifier_param_shapes(kind).items():
+        if k.endswith("running_var"):
+            v = rng.uniform(0.5, 2.0, size=shp)
+        elif k.endswith("running_mean") or k.endswith(".bias"):
+            v = rng.normal(0, 0.1, size=shp)
+        elif k.endswith("batch_norm.weight"):
+            v = rng.uniform(0.8, 1.2, size=shp)
+        else:
+            fan_in = int(np.prod(shp[1:]))
+            v = rng.normal(0, np.sqrt(2.0 / fan_in), size=shp)
+        sd[k] = v.astype(np.float32)
+    return sd

@@ -1,0 +1,84 @@
+"""Calibrate the synthetic Darknet weights with the REFERENCE model (build container only).
+
+For each cfg of record: conv weights from rtdm.synth (He-scaled, seeded); every
+BatchNorm's running mean/var set from its conv's output statistics on synthetic
+frames (one forward of the reference Darknet, calibrating layer by layer in a
+conv forward hook), and each yolo head's objectness bias set so ~2% of anchors
+pass obj > 0.3.  Writes real-time-disaster-management_amd/rtdm/data/synth_<cfg>.npz.
+Run: python tests/golden/make_synth.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "real-time-disaster-management_amd"))
+sys.path.insert(0, HERE)
+
+from rtdm import synth  # noqa: E402
+from refimport import DET_DIR, import_darknet  # noqa: E402
+
+CFGS = ["yolov4-tiny-aider-416", "yolov3-aider-416", "yolov3-spp-aider", "yolov3-tiny-aider-416"]
+
+
+def calibrate(name: str, size: int = 416):
+    models, _ = import_darknet()
+    cfg_path = os.path.join(DET_DIR, "cfg", name + ".cfg")
+    text = open(cfg_path).read()
+    stream = synth.synth_darknet_weights(text, calib=None)
+    model = models.Darknet(cfg_path, (size, size))
+    with tempfile.NamedTemporaryFile(suffix=".weights") as f:
+        synth.write_darknet_weights(f.name, stream)
+        models.load_darknet_weights(model, f.name)
+    model.eval()
+    calib = {}
+    heads = {}
+    mdefs = model.module_defs
+    for i, (mdef, mod) in enumerate(zip(mdefs, model.module_list)):
+        if mdef["type"] != "convolutional":
+            continue
+        conv = mod[0]
+        if mdef["batch_normalize"]:
+            bn = mod[1]
+
+            def hook(m, inp, out, bn=bn, i=i):
+                x = out.detach().double()
+                mean = x.mean(dim=(0, 2, 3))
+                var = x.var(dim=(0, 2, 3), unbiased=False) + 1e-6
+                bn.running_mean.copy_(mean.float())
+                bn.running_var.copy_(var.float())
+                calib[f"mean{i}"] = mean.float().numpy()
+                calib[f"var{i}"] = var.float().numpy()
+            conv.register_forward_hook(hook)
+        elif i + 1 < len(mdefs) and mdefs[i + 1]["type"] == "yolo":
+            def hhook(m, inp, out, i=i):
+                heads[i] = out.detach()
+            conv.register_forward_hook(hhook)
+    frames = synth.synth_frames(2, size, size, seed=synth.BASE_SEED + 1000)
+    x = torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0
+    with torch.no_grad():
+        model(x)
+    logit03 = float(np.log(0.3 / 0.7))
+    for i, p in heads.items():
+        no = int(mdefs[i + 1]["classes"]) + 5
+        na = p.shape[1] // no
+        obj = p.view(p.shape[0], na, no, *p.shape[2:])[:, :, 4] - (-3.5)  # remove the default bias
+        q = float(np.quantile(obj.numpy().reshape(-1), 0.98))
+        calib[f"objbias{i}"] = np.array(logit03 - q, np.float32)
+    os.makedirs(synth.DATA_DIR, exist_ok=True)
+    out = os.path.join(synth.DATA_DIR, f"synth_{name}.npz")
+    np.savez_compressed(out, **calib)
+    print(name, "->", out, len(calib), "arrays; obj biases",
+          {k: float(v) for k, v in calib.items() if k.startswith("objbias")})
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    for n in (sys.argv[1:] or CFGS):
+        calibrate(n)

@@ -1,0 +1,304 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+reference's golden vectors.  Tolerances:
+  fp32  class id exact; logits <= 1e-4 * max|logit| per row; io boxes <= 1e-3 px
+        (+1e-5 rel), io probabilities <= 1e-5; NMS survivors exact when fed the
+        same io.
+  fp16  class id exact where the top-2 logit gap >= 0.5; logits <= 2e-2*max|logit|;
+        boxes <= 0.5 px, probabilities <= 2e-2.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import cfg_text
+
+pytestmark = pytest.mark.gpu
+
+MODELS = ["squeeze-ernet", "squeeze-redconv", "ernet"]
+SIZE = {"squeeze-ernet": 140, "squeeze-redconv": 140, "ernet": 240}
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+def _model(name, sd, half=False):
+    from rtdm.classifier import build_model
+    m = build_model(name)
+    m.load_state_dict(sd)
+    if half:
+        m.half()
+    return m
+
+
+# ------------------------------------------------------------- preprocess --
+def test_preprocess_bit_exact_vs_pillow(dev, cls_golden):
+    from oracle import preprocess as P
+    from rtdm.preprocess import preprocess_frames
+    from rtdm.synth import synth_frames
+    frames = [synth_frames(3, 608, 608, seed=5), synth_frames(2, 224, 224, seed=6), synth_frames(2, 300, 451, seed=7),
+              cls_golden["src0"][None]]
+    for f in frames:
+        for s in (140, 240):
+            if min(f.shape[1:3]) < int(s * 1.14):
+                continue
+            got = preprocess_frames(torch.from_numpy(f).to(dev), s).cpu().numpy()
+            for i in range(f.shape[0]):
+                rs = P.pil_resize_shorter(f[i], int(s * 1.14))
+                want = P.to_tensor_normalize(P.center_crop(rs, s))
+                assert np.array_equal(got[i], want), (f.shape, s, i, np.abs(got[i] - want).max())
+
+
+# ------------------------------------------------------------- classifier --
+@pytest.mark.parametrize("name", MODELS)
+def test_classifier_fp32_golden(dev, name, cls_golden, cls_weights):
+    from oracle import preprocess as P
+    m = _model(name, cls_weights[name])
+    crops = cls_golden[f"{name}/crops"]
+    x = torch.from_numpy(np.stack([P.to_tensor_normalize(c) for c in crops])).to(dev)
+    probs = m(x).cpu().numpy()
+    logits = m.logits.cpu().numpy()
+    ref = cls_golden[f"{name}/logits"]
+    tol = 1e-4 * np.abs(ref).max(1, keepdims=True)
+    assert np.all(np.abs(logits - ref) <= tol), np.abs(logits - ref).max()
+    assert np.array_equal(logits.argmax(1), cls_golden[f"{name}/argmax"])
+    assert np.allclose(probs, cls_golden[f"{name}/probs"], atol=1e-5)
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_classifier_fp32_random_inputs(dev, name, cls_golden, cls_weights):
+    m = _model(name, cls_weights[name])
+    s = SIZE[name]
+    g = torch.Generator().manual_seed(1234)
+    xr = torch.randn(3, 3, s, s, generator=g)
+    m(xr.to(dev))
+    logits = m.logits.cpu().numpy()
+    ref = cls_golden[f"{name}/rand_logits"]
+    tol = 1e-4 * np.abs(ref).max(1, keepdims=True)
+    assert np.all(np.abs(logits - ref) <= tol), np.abs(logits - ref).max()
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_classifier_fp16(dev, name, cls_golden, cls_weights):
+    from oracle import preprocess as P
+    m = _model(name, cls_weights[name], half=True)
+    crops = cls_golden[f"{name}/crops"]
+    x = torch.from_numpy(np.stack([P.to_tensor_normalize(c) for c in crops])).to(dev)
+    m(x)
+    logits = m.logits.cpu().numpy()
+    ref = cls_golden[f"{name}/logits"]
+    gap = cls_golden[f"{name}/top2gap"]
+    assert np.all(np.abs(logits - ref) <= 2e-2 * np.abs(ref).max(1, keepdims=True)), np.abs(logits - ref).max()
+    sure = gap >= 0.5
+    assert np.array_equal(logits.argmax(1)[sure], cls_golden[f"{name}/argmax"][sure])
+    # fp16 input tensor (the reference's --trt --quant fp16 .half() path)
+    m(x.half())
+    assert np.all(np.abs(m.logits.cpu().numpy() - ref) <= 2e-2 * np.abs(ref).max(1, keepdims=True))
+
+
+@pytest.mark.parametrize("name", MODELS)
+@pytest.mark.parametrize("half", [False, True])
+def test_classifier_frames_vs_oracle(dev, name, half, cls_weights):
+    """uint8 frames -> fused transform + model, against oracle transform + oracle model."""
+    from oracle import classifier as OC
+    from oracle import preprocess as P
+    from rtdm.synth import synth_frames
+    m = _model(name, cls_weights[name], half=half)
+    frames = synth_frames(5, 608, 608, seed=99)
+    m.classify_frames(torch.from_numpy(frames).to(dev))
+    logits = m.logits.cpu().numpy()
+    s = SIZE[name]
+    x = torch.from_numpy(np.stack([P.cli_transform(f, s) for f in frames]))
+    ref, _, _ = OC.forward(name, cls_weights[name], x)
+    ref = ref.numpy()
+    tol = (2e-2 if half else 1e-4) * np.abs(ref).max(1, keepdims=True)
+    assert np.all(np.abs(logits - ref) <= tol), np.abs(logits - ref).max()
+
+
+def test_classifier_batch_edges(dev, cls_weights):
+    """n = 0, 1 and a batch larger than the first handle capacity."""
+    m = _model("squeeze-ernet", cls_weights["squeeze-ernet"])
+    x = torch.randn(0, 3, 140, 140, device=dev)
+    assert m(x).shape == (0, 5)
+    from oracle import classifier as OC
+    xs = torch.randn(70, 3, 140, 140)
+    p = m(xs.to(dev)).cpu()
+    ref, _, _ = OC.forward("squeeze-ernet", cls_weights["squeeze-ernet"], xs)
+    assert torch.equal(p.argmax(1), torch.softmax(ref, 1).argmax(1))
+    with pytest.raises(ValueError):
+        m(torch.randn(1, 3, 224, 224, device=dev))
+
+
+# --------------------------------------------------------------- detector --
+def _darknet(cfg, size, half=False):
+    from rtdm.darknet import Darknet
+    from rtdm.synth import load_calibration, synth_darknet_weights
+    text = cfg_text(cfg)
+    m = Darknet(text, (size, size))
+    stream = synth_darknet_weights(text, calib=load_calibration(cfg))
+    m.load_weight_stream(stream)
+    if half:
+        m.half()
+    return m, text, stream
+
+
+def _check_io(io, ref, half):
+    box_tol = 0.5 if half else 1e-3
+    p_tol = 2e-2 if half else 1e-5
+    d = np.abs(io - ref)
+    rel = 1e-5 * np.abs(ref)
+    assert np.all(d[..., :4] <= box_tol + (0 if half else rel[..., :4])), d[..., :4].max()
+    assert np.all(d[..., 4:] <= p_tol), d[..., 4:].max()
+
+
+@pytest.mark.parametrize("half", [False, True])
+def test_detector_golden_small(dev, det_golden, half):
+    from rtdm.synth import synth_frames
+    key = "yolov4-tiny-aider-416@256"
+    m, _, stream = _darknet("yolov4-tiny-aider-416", 256, half)
+    assert stream.size == int(det_golden[f"{key}/stream_n"])
+    frames = det_golden[f"{key}/frames"]
+    x = torch.from_numpy(frames).to(dev)
+    io, _ = m(x)
+    _check_io(io.cpu().numpy(), det_golden[f"{key}/io"], half)
+    # the NCHW fp32 drop-in input gives the same io
+    xn = (torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0).to(dev)
+    io2, _ = m(xn)
+    _check_io(io2.cpu().numpy(), det_golden[f"{key}/io"], half)
+    del synth_frames
+
+
+@pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416", "yolov3-spp-aider@608",
+                                  "yolov3-tiny-aider-416@416"])
+@pytest.mark.parametrize("half", [False, True])
+def test_detector_golden_full(dev, det_golden, case, half):
+    from rtdm.synth import BASE_SEED, synth_frames
+    cfg, size = case.split("@")
+    size = int(size)
+    m, _, stream = _darknet(cfg, size, half)
+    frames = synth_frames(1, size, size, seed=BASE_SEED + 700)
+    io, _ = m(torch.from_numpy(frames).to(dev))
+    io = io.cpu().numpy()
+    assert list(io.shape) == list(det_golden[f"{case}/io_shape"])
+    _check_io(io[:, ::53], det_golden[f"{case}/io_rows"], half)
+    cs = io.astype(np.float64).sum(1)
+    ref = det_golden[f"{case}/io_colsum"]
+    assert np.allclose(cs, ref, rtol=(2e-3 if half else 1e-5), atol=1e-2), (cs, ref)
+
+
+@pytest.mark.parametrize("half", [False, True])
+def test_detector_layers_vs_oracle(dev, half):
+    """Every materialised layer output of yolov3-aider (shortcuts, routes, upsample) vs the oracle."""
+    from oracle.darknet import DarknetRef
+    from rtdm.synth import synth_frames
+    m, text, stream = _darknet("yolov3-aider-416", 160, half)
+    frames = synth_frames(2, 160, 160, seed=3)
+    m(torch.from_numpy(frames).to(dev))
+    ref_io, outs = DarknetRef(text, stream).forward(
+        torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0, keep_layers=True)
+    checked = 0
+    for i, o in enumerate(outs):
+        if not isinstance(o, torch.Tensor):
+            continue
+        try:
+            got = m.layer_output(i, 2).cpu()
+        except RuntimeError:
+            continue  # fused away
+        scale = o.abs().max().item() + 1e-6
+        err = (got - o).abs().max().item()
+        assert err <= (2e-2 if half else 1e-4) * scale + (2e-2 if half else 1e-4), (i, err, scale)
+        checked += 1
+    assert checked >= 20
+
+
+# -------------------------------------------------------------------- NMS --
+def _nms_compare(io, conf, iou, multi_label=True, agnostic=False, classes=None):
+    from oracle import nms as ON
+    from rtdm.nms import nms_batched
+    n, a, no = io.shape
+    max_det = a * (no - 5)
+    det, idx, count = nms_batched(torch.from_numpy(io).cuda(), conf, iou, multi_label, classes, agnostic, max_det)
+    det, idx, count = det.cpu().numpy(), idx.cpu().numpy(), count.cpu().numpy()
+    ref, ref_idx = ON.non_max_suppression(io, conf, iou, multi_label, classes, agnostic, return_index=True)
+    for b in range(n):
+        r = np.zeros((0, 6), np.float32) if ref[b] is None else ref[b]
+        assert count[b] == len(r), (b, count[b], len(r))
+        assert np.array_equal(det[b, :count[b]], r)
+        ri = np.zeros((0, 2)) if ref_idx[b] is None else ref_idx[b]
+        assert np.array_equal(idx[b, :count[b]], ri)
+    return count
+
+
+def test_nms_golden_io(dev, det_golden):
+    """NMS kernel fed the reference io: bit-exact survivors vs the reference non_max_suppression."""
+    key = "yolov4-tiny-aider-416@256"
+    io = det_golden[f"{key}/io"]
+    from rtdm.nms import non_max_suppression
+    for conf, iou in ((0.3, 0.4), (0.01, 0.6)):
+        got = non_max_suppression(torch.from_numpy(io).cuda(), conf, iou)
+        for b in range(io.shape[0]):
+            ref = det_golden[f"{key}/nms{conf}_{iou}/{b}"]
+            g = np.zeros((0, 6), np.float32) if got[b] is None else got[b].cpu().numpy()
+            assert g.shape == ref.shape, (conf, b, g.shape, ref.shape)
+            assert np.array_equal(g, ref)
+        _nms_compare(io, conf, iou)
+
+
+def test_nms_modes_and_edges(dev):
+    rng = np.random.default_rng(0)
+    n, a, nc = 3, 3000, 3
+    io = np.zeros((n, a, 5 + nc), np.float32)
+    io[..., 0:2] = rng.uniform(0, 400, (n, a, 2))
+    io[..., 2:4] = rng.uniform(1, 80, (n, a, 2))
+    io[..., 4:] = rng.uniform(0, 1, (n, a, 1 + nc))
+    io[0, 5, 2] = np.inf  # filtered by w < 4096
+    io[1, 7, 0] = np.nan  # nan box -> filtered (finite check / comparisons)
+    io[2] = 0  # nothing passes -> None
+    for conf, iou in ((0.3, 0.4), (0.05, 0.5), (0.7, 0.9)):
+        _nms_compare(io, conf, iou)
+        _nms_compare(io, conf, iou, multi_label=False)
+        _nms_compare(io, conf, iou, agnostic=True)
+        _nms_compare(io, conf, iou, classes=[0, 2])
+
+
+def test_nms_large_candidate_set(dev):
+    """> 4096 candidates per image exercises the global-memory path."""
+    rng = np.random.default_rng(1)
+    io = np.zeros((2, 20000, 7), np.float32)
+    io[..., 0:2] = rng.uniform(0, 600, (2, 20000, 2))
+    io[..., 2:4] = rng.uniform(3, 60, (2, 20000, 2))
+    io[..., 4:] = rng.uniform(0.2, 1, (2, 20000, 3))
+    c = _nms_compare(io, 0.05, 0.5)
+    assert c.min() > 100
+
+
+# ---------------------------------------------------------------- pipeline --
+def test_two_stage_pipeline(dev, cls_weights):
+    from oracle import classifier as OC
+    from oracle import preprocess as P
+    from oracle.darknet import DarknetRef
+    from oracle import nms as ON
+    from rtdm.classifier import build_model
+    from rtdm.pipeline import TwoStagePipeline
+    from rtdm.synth import synth_frames
+    cls = build_model("squeeze-ernet")
+    cls.load_state_dict(cls_weights["squeeze-ernet"])
+    det, text, stream = _darknet("yolov4-tiny-aider-416", 320)
+    pipe = TwoStagePipeline(cls, det, 0.3, 0.4, max_det=300)
+    frames = synth_frames(4, 320, 320, seed=42)
+    out = pipe(torch.from_numpy(frames).to(dev))
+    torch.cuda.synchronize()
+    x = torch.from_numpy(np.stack([P.cli_transform(f, 140) for f in frames]))
+    ref_logits, _, _ = OC.forward("squeeze-ernet", cls_weights["squeeze-ernet"], x)
+    assert torch.equal(out["logits"].cpu().argmax(1), ref_logits.argmax(1))
+    io_ref = DarknetRef(text, stream).forward(torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0)
+    _check_io(out["io"].cpu().numpy(), io_ref.numpy(), False)
+    # NMS on the device io is bit-exact with the oracle NMS on the same io
+    ref = ON.non_max_suppression(out["io"].cpu().numpy(), 0.3, 0.4)
+    cnt = out["count"].cpu().numpy()
+    for b in range(4):
+        r = np.zeros((0, 6), np.float32) if ref[b] is None else ref[b]
+        assert cnt[b] == len(r)
+        assert np.array_equal(out["det"][b, :min(cnt[b], 300)].cpu().numpy(), r[:300])
