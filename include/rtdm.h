@@ -138,6 +138,16 @@ rtdm_status rtdm_detector_get_info(rtdm_detector h, rtdm_detector_info* info);
 /* Human-readable execution plan (kernels, fusions, buffers); returns bytes
  * needed including the NUL when buf is too small.                               */
 int64_t rtdm_detector_describe(rtdm_detector h, char* buf, int64_t buf_len);
+/* Execution steps (kernel launches) of the plan, with the kernel symbol, the
+ * algorithmic FLOPs (2*MAC) and compulsory HBM bytes per image of each step. */
+int rtdm_detector_num_steps(rtdm_detector h);
+rtdm_status rtdm_detector_step_info(rtdm_detector h, int step, char* name, int name_len, int* layer,
+                                    double* flop_per_image, double* bytes_per_image);
+/* Per-step device timing (roofline measurement): hipEvents are recorded on the
+ * launch stream between steps of the next max_calls rtdm_detect calls (0 = off).
+ * read_timing synchronises those events and returns the summed ms per step.    */
+rtdm_status rtdm_detector_enable_timing(rtdm_detector h, int max_calls);
+rtdm_status rtdm_detector_read_timing(rtdm_detector h, double* ms_per_step, int* calls);
 /* io: [n, n_anchors_total, no] fp32, exactly the reference's torch.cat(io, 1). */
 rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float* io, void* stream);
 /* Debug/parity: copy cfg layer `layer`'s output of the LAST rtdm_detect call as

@@ -141,6 +141,8 @@ struct ConvArgs {
 
 // Launchers (conv.hip).  dtype = RTDM_F16 / RTDM_F32 (activation + weight type).
 void launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
+// Kernel symbol (template instantiation) launch_conv will pick for a / dtype.
+const char* conv_kernel_name(const ConvArgs& a, int dtype);
 // Row geometry helpers shared by host planners.
 inline void conv_set_rows(ConvArgs& a) {
   if (a.quad) {

@@ -357,6 +357,16 @@ static bool mfma_ok(const ConvArgs& a) {
   return a.in_kind == IN_NHWC && a.cin % 8 == 0 && a.in_cs % 8 == 0 && a.in_co % 8 == 0;
 }
 
+const char* conv_kernel_name(const ConvArgs& a, int dtype) {
+  if (dtype == RTDM_F16 && !a.w_f32) {
+    if (a.cout_pad >= 128) return "conv_mfma_f16<128,128,64,2,2>";
+    if (a.cout_pad == 64) return "conv_mfma_f16<128,64,64,2,2>";
+    if (a.cout_pad == 32) return "conv_mfma_f16<128,32,64,4,1>";
+    return "conv_mfma_f16<128,16,64,4,1>";
+  }
+  return dtype == RTDM_F16 ? "conv_valu<_Float16>" : "conv_valu<float>";
+}
+
 void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
   if (a.M <= 0) return;
   RTDM_REQUIRE(!a.quad || (a.oh >= 2 && a.ow >= 2), RTDM_E_INVALID, "conv: quad ordering needs >= 2x2 output");

@@ -139,6 +139,13 @@ struct rtdm_detector_s {
   rtdm::DevBlob blob;
   rtdm::DevBuf arena;
   int last_n = 0;
+  // optional per-step timing: events[call][step+1] recorded on the launch stream
+  bool timing = false;
+  int timing_cap = 0, timing_calls = 0;
+  std::vector<hipEvent_t> events;
+  ~rtdm_detector_s() {
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
+  }
 };
 
 namespace rtdm {
@@ -298,6 +305,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
                        RTDM_E_UNSUPPORTED, "cfg: shortcut with channel/shape mismatch unsupported");
           s.res_t = st;
           fused[i + 1] = true;
+          h.layer_tensor[i] = -1;        // the pre-add conv output is never materialised
           h.layer_tensor[i + 1] = full;  // conv output with the residual added
           need_full = !consumers[i + 1].empty();
         } else if (nx.type == "yolo" && only_next) {
@@ -509,6 +517,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     st.w_beta = st.w_gamma = st.w_mean = st.w_var = st.w_bias = st.w_W = nullptr;
   }
   if (weights) {
+    RTDM_HIP(hipGetDevice(&h.dev));
     h.blob.upload(blob);
     h.arena.alloc(h.per_image * esize_of(h.dtype) * h.max_batch);
   }
@@ -543,7 +552,14 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
     in_kind = IN_NCHW_F16;
   else
     throw Error{RTDM_E_INVALID, "detect: unknown input kind"};
-  for (const Step& st : h.steps) {
+  hipEvent_t* ev = nullptr;
+  if (h.timing && h.timing_calls < h.timing_cap) {
+    ev = &h.events[(size_t)h.timing_calls * (h.steps.size() + 1)];
+    ++h.timing_calls;
+    RTDM_HIP(hipEventRecord(ev[0], s));
+  }
+  for (size_t si = 0; si < h.steps.size(); ++si) {
+    const Step& st = h.steps[si];
     if (st.kind == ST_CONV) {
       ConvArgs a;
       if (st.in_t < 0) {
@@ -601,8 +617,37 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       o.co += st.k;
       launch_copy_slice(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, o, h.dtype, s);
     }
+    if (ev) RTDM_HIP(hipEventRecord(ev[si + 1], s));
   }
   h.last_n = n;
+}
+
+// Kernel symbol, FLOPs and compulsory HBM bytes per image of one step.
+static void step_info(const rtdm_detector_s& h, const Step& st, std::string& name, double& flop, double& bytes) {
+  const double es = (double)esize_of(h.dtype);
+  if (st.kind == ST_CONV) {
+    ConvArgs a;
+    a.in_kind = st.in_t < 0 ? IN_FRAME_U8 : IN_NHWC;
+    a.cout_pad = st.pc.cout_pad;
+    a.w_f32 = st.pc.mfma ? 0 : 1;
+    name = conv_kernel_name(a, h.dtype);
+    flop = 2.0 * st.oh * st.ow * (double)st.cout * st.cin * st.ks * st.ks;
+    double out = 0;
+    if (st.full_t >= 0) out += (double)st.oh * st.ow * st.cout;
+    if (st.pool_t >= 0) out += (double)(st.oh / 2) * (st.ow / 2) * st.cout;
+    if (st.up_t >= 0) out += 4.0 * st.oh * st.ow * st.cout;
+    if (st.res_t >= 0) out += (double)st.oh * st.ow * st.cout;
+    const double in = (double)st.ih * st.iw * st.cin * (st.in_t < 0 ? 1.0 / es : 1.0);
+    bytes = (in + out) * es + (st.yolo >= 0 ? (double)st.oh * st.ow * st.cout * 4.0 : 0.0);
+  } else if (st.kind == ST_MAXPOOL) {
+    name = "maxpool_kernel";
+    flop = 0;
+    bytes = ((double)st.ih * st.iw + (double)st.oh * st.ow) * st.cin * es;
+  } else {
+    name = "upsample_kernel";
+    flop = 0;
+    bytes = ((double)st.ih * st.iw + (double)st.oh * st.ow) * st.cin * es;
+  }
 }
 
 static std::string describe(const rtdm_detector_s& h) {
@@ -660,7 +705,6 @@ rtdm_status rtdm_detector_create(const char* cfg_text, int img_h, int img_w, int
     h->dtype = dtype;
     h->max_batch = max_batch;
     h->planning_only = weights == nullptr;
-    if (!h->planning_only) RTDM_HIP(hipGetDevice(&h->dev));
     std::vector<CfgBlock> defs = parse_cfg(cfg_text);
     const CfgBlock& net = defs[0];
     RTDM_REQUIRE(net.i("channels", 3) == 3, RTDM_E_UNSUPPORTED, "cfg: only 3-channel input supported");
@@ -696,6 +740,57 @@ int64_t rtdm_detector_describe(rtdm_detector h, char* buf, int64_t buf_len) {
   const int64_t need = (int64_t)s.size() + 1;
   if (buf && buf_len >= need) std::memcpy(buf, s.c_str(), need);
   return need;
+}
+
+int rtdm_detector_num_steps(rtdm_detector h) { return h ? (int)h->steps.size() : 0; }
+
+rtdm_status rtdm_detector_step_info(rtdm_detector h, int step, char* name, int name_len, int* layer,
+                                    double* flop_per_image, double* bytes_per_image) {
+  return guard([&] {
+    RTDM_REQUIRE(h && step >= 0 && step < (int)h->steps.size(), RTDM_E_INVALID, "step_info: bad step");
+    std::string nm;
+    double f = 0, b = 0;
+    step_info(*h, h->steps[step], nm, f, b);
+    if (name && name_len > 0) {
+      std::strncpy(name, nm.c_str(), name_len - 1);
+      name[name_len - 1] = 0;
+    }
+    if (layer) *layer = h->steps[step].layer;
+    if (flop_per_image) *flop_per_image = f;
+    if (bytes_per_image) *bytes_per_image = b;
+  });
+}
+
+rtdm_status rtdm_detector_enable_timing(rtdm_detector h, int max_calls) {
+  return guard([&] {
+    RTDM_REQUIRE(h && !h->planning_only, RTDM_E_INVALID, "enable_timing: bad handle");
+    for (hipEvent_t e : h->events) (void)hipEventDestroy(e);
+    h->events.clear();
+    h->timing = max_calls > 0;
+    h->timing_cap = max_calls > 0 ? max_calls : 0;
+    h->timing_calls = 0;
+    const size_t ne = (size_t)h->timing_cap * (h->steps.size() + 1);
+    h->events.resize(ne);
+    for (size_t i = 0; i < ne; ++i) RTDM_HIP(hipEventCreate(&h->events[i]));
+  });
+}
+
+rtdm_status rtdm_detector_read_timing(rtdm_detector h, double* ms_per_step, int* calls) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "read_timing: NULL handle");
+    const size_t ns = h->steps.size();
+    for (size_t i = 0; i < ns; ++i) ms_per_step[i] = 0.0;
+    for (int c = 0; c < h->timing_calls; ++c) {
+      hipEvent_t* ev = &h->events[(size_t)c * (ns + 1)];
+      RTDM_HIP(hipEventSynchronize(ev[ns]));
+      for (size_t i = 0; i < ns; ++i) {
+        float ms = 0.f;
+        RTDM_HIP(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+        ms_per_step[i] += ms;
+      }
+    }
+    if (calls) *calls = h->timing_calls;
+  });
 }
 
 rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float* io, void* stream) {

@@ -63,6 +63,11 @@ SIGNATURES = {
     "rtdm_detector_destroy": (c_int, [c_void_p]),
     "rtdm_detector_get_info": (c_int, [c_void_p, POINTER(rtdm_detector_info)]),
     "rtdm_detector_describe": (c_int64, [c_void_p, c_char_p, c_int64]),
+    "rtdm_detector_num_steps": (c_int, [c_void_p]),
+    "rtdm_detector_step_info": (c_int, [c_void_p, c_int, c_char_p, c_int, POINTER(c_int), POINTER(c_double),
+                                        POINTER(c_double)]),
+    "rtdm_detector_enable_timing": (c_int, [c_void_p, c_int]),
+    "rtdm_detector_read_timing": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int)]),
     "rtdm_detect": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "rtdm_detector_layer_output": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int64, POINTER(c_int),
                                            POINTER(c_int), POINTER(c_int), c_void_p]),

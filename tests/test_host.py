@@ -1,0 +1,128 @@
+"""CPU: host-side logic — weight formats, synthetic data determinism, frame
+sharding and the multi-process (gloo, world_size 2) weight broadcast / result gather."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import cfg_text
+
+
+def test_synth_frames_deterministic_and_shardable():
+    from rtdm.synth import synth_frames
+    a = synth_frames(4, 64, 80)
+    b = np.concatenate([synth_frames(2, 64, 80, first=0), synth_frames(2, 64, 80, first=2)])
+    assert a.dtype == np.uint8 and a.shape == (4, 64, 80, 3)
+    assert np.array_equal(a, b)
+    assert a.std() > 10
+
+
+def test_darknet_weight_file_roundtrip(tmp_path):
+    from rtdm.synth import read_darknet_weights, synth_darknet_weights, write_darknet_weights
+    s = synth_darknet_weights(cfg_text("yolov3-tiny-aider-416"))
+    p = tmp_path / "x.weights"
+    write_darknet_weights(str(p), s)
+    assert os.path.getsize(p) == 20 + 4 * s.size
+    assert np.array_equal(read_darknet_weights(str(p)), s)
+
+
+def test_state_dict_to_stream_order():
+    """{'model': state_dict} checkpoints map onto the darknet stream order (save_weights)."""
+    from oracle.darknet import DarknetRef
+    from rtdm.darknet import state_dict_to_stream
+    from rtdm.synth import synth_darknet_weights
+    text = cfg_text("yolov4-tiny-aider-416")
+    s = synth_darknet_weights(text)
+    ref = DarknetRef(text, s)
+    sd = {}
+    for i, p in ref.params.items():
+        if "gamma" in p:
+            sd[f"module_list.{i}.BatchNorm2d.bias"] = p["beta"]
+            sd[f"module_list.{i}.BatchNorm2d.weight"] = p["gamma"]
+            sd[f"module_list.{i}.BatchNorm2d.running_mean"] = p["mean"]
+            sd[f"module_list.{i}.BatchNorm2d.running_var"] = p["var"]
+        else:
+            sd[f"module_list.{i}.Conv2d.bias"] = p["bias"]
+        sd[f"module_list.{i}.Conv2d.weight"] = p["w"]
+    assert np.array_equal(state_dict_to_stream(text, sd), s)
+
+
+def test_classifier_state_dict_validation(cls_weights):
+    from rtdm.classifier import build_model, load_model
+    m = build_model("squeeze-ernet")
+    m.load_state_dict(cls_weights["squeeze-ernet"])
+    bad = dict(cls_weights["squeeze-ernet"])
+    bad.pop("fc.bias")
+    with pytest.raises(RuntimeError):
+        build_model("squeeze-ernet").load_state_dict(bad)
+    with pytest.raises(RuntimeError):
+        build_model("ernet").load_state_dict(cls_weights["squeeze-ernet"])
+    with pytest.raises(ValueError):
+        build_model("resnet")
+    with pytest.raises(FileNotFoundError):
+        load_model("ernet", "/nonexistent.pt", "cpu")
+
+
+def test_cpu_tensor_input_fails_loudly(cls_weights):
+    from rtdm.classifier import build_model
+    m = build_model("squeeze-ernet")
+    m.load_state_dict(cls_weights["squeeze-ernet"])
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 3, 140, 140))
+
+
+def test_shard_range_partitions():
+    from rtdm.distributed import shard_range
+    for gb in (1, 7, 64, 128):
+        for world in (1, 2, 3, 8):
+            covered = []
+            for r in range(world):
+                s, c = shard_range(gb, world, r)
+                covered += list(range(s, s + c))
+            assert covered == list(range(gb))
+
+
+def _dist_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rtdm.distributed import broadcast_state_dict, gather_results, shard_range
+        from rtdm.synth import classifier_param_shapes, synth_classifier_state_dict, synth_frames
+        shapes = classifier_param_shapes("ernet")
+        sd = synth_classifier_state_dict("ernet") if rank == 0 else None
+        got = broadcast_state_dict(sd, shapes, device="cpu")
+        ref = synth_classifier_state_dict("ernet")
+        ok = all(np.array_equal(got[k], ref[k]) for k in shapes)
+        s, c = shard_range(8, world, rank)
+        frames = synth_frames(c, 32, 32, first=s)
+        rec = {"sum": torch.tensor([float(frames.sum())]), "rank": torch.tensor([rank])}
+        out = gather_results(rec)
+        if rank == 0:
+            total = sum(float(t.item()) for t in out["sum"])
+            q.put((ok, total, [int(t.item()) for t in out["rank"]]))
+        else:
+            q.put((ok, None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_broadcast_and_gather():
+    import torch.multiprocessing as mp
+    from rtdm.synth import synth_frames
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[0] for r in res)
+    total = [r for r in res if r[1] is not None][0]
+    assert total[1] == float(synth_frames(8, 32, 32).sum())
+    assert total[2] == [0, 1]
