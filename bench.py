@@ -138,7 +138,7 @@ def cpu_baseline(args, text, stream, sd):
     from oracle import preprocess as OP
     from oracle.darknet import DarknetRef
     from rtdm.synth import synth_frames
-    cores = len(os.sched_getaffinity(0))
+    cores = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
     torch.set_num_threads(cores)
     ref = DarknetRef(text, stream)
     s = 240 if args.classifier == "ernet" else 140

@@ -45,18 +45,20 @@ def _coeffs(in_size: int, out_size: int):
 
 
 def _pass(img: np.ndarray, axis: int, out_size: int) -> np.ndarray:
-    """One Pillow resample pass along `axis` (1 = horizontal, 0 = vertical) of HxWx3 uint8."""
+    """One Pillow resample pass along `axis` (1 = horizontal, 0 = vertical) of HxWx3 uint8.
+    The integer multiply-accumulate is evaluated as a dense float64 matmul: every
+    partial sum is an integer below 2^31, so float64 is exact."""
     in_size = img.shape[axis]
     if in_size == out_size:
         return img
     bounds, k = _coeffs(in_size, out_size)
-    src = np.moveaxis(img.astype(np.int64), axis, 0)  # [in, other, 3]
-    out = np.empty((out_size,) + src.shape[1:], np.uint8)
+    dense = np.zeros((out_size, in_size), np.float64)
     for o in range(out_size):
         xmin, xmax = bounds[o]
-        acc = np.full(src.shape[1:], 1 << (PRECISION_BITS - 1), np.int64)
-        acc += np.tensordot(k[o, :xmax], src[xmin:xmin + xmax], axes=(0, 0))
-        out[o] = np.clip(acc >> PRECISION_BITS, 0, 255).astype(np.uint8)
+        dense[o, xmin:xmin + xmax] = k[o, :xmax]
+    src = np.moveaxis(img, axis, 0).astype(np.float64)  # [in, other, 3]
+    acc = (dense @ src.reshape(in_size, -1)).astype(np.int64) + (1 << (PRECISION_BITS - 1))
+    out = np.clip(acc >> PRECISION_BITS, 0, 255).astype(np.uint8).reshape((out_size,) + src.shape[1:])
     return np.moveaxis(out, 0, axis)
 
 

@@ -121,7 +121,7 @@ struct Epilogue {
   float* io = nullptr;
   int io_rows = 0, io_off = 0, na = 0, no = 0;
   float ystride = 0.f;
-  float anchor_vec[16];  // (w,h) pairs, anchors / stride, fp32 like models.py:431
+  const float* anchor_vec = nullptr;  // device [na][2]: anchors / stride, fp32 like models.py:431
 };
 
 struct ConvArgs {
@@ -136,6 +136,8 @@ struct ConvArgs {
   const void* w = nullptr;  // packed weights [cout_pad][kpad], k = (kh*ks+kw)*cin + c
   int kpad = 0, cout_pad = 0;
   int w_f32 = 0;            // weights packed fp32 for the VALU body (else fp16 MFMA layout)
+  const void* w_stem = nullptr;  // MFMA stem (Cin=3, 3x3): fp16 [cout_pad][32], k = (kh*3+kw)*3+c
+  const void* w_u8 = nullptr;    // the same divided by 255 (uint8 frame input)
   Epilogue e;
 };
 

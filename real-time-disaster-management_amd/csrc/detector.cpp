@@ -120,6 +120,7 @@ struct YoloHead {
   int layer = 0, na = 0, no = 0, ny = 0, nx = 0, io_off = 0;
   float ystride = 0.f;
   std::vector<float> anchor_vec;
+  size_t anchor_off = 0;  // device copy in the weight blob
 };
 
 }  // namespace rtdm
@@ -506,6 +507,10 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       }
       st.pc = pack_conv(blob, st.w_W, filters, st.cin, size, st.bn ? sc.data() : nullptr, use_mfma);
       st.pc.b_off = blob.add_f32(b);
+      if (f16 && st.in_t < 0 && st.cin == 3 && size == 3 && st.stride == 1 && st.pad == 1) {
+        st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr, 1.0);
+        st.pc.stem_u8_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr, 255.0);
+      }
     } else {
       st.pc.cout = filters;
       st.pc.cin = st.cin;
@@ -516,6 +521,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     }
     st.w_beta = st.w_gamma = st.w_mean = st.w_var = st.w_bias = st.w_W = nullptr;
   }
+  for (YoloHead& y : h.heads) y.anchor_off = blob.add_f32(y.anchor_vec);
   if (weights) {
     RTDM_HIP(hipGetDevice(&h.dev));
     h.blob.upload(blob);
@@ -602,10 +608,12 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
         a.e.na = y.na;
         a.e.no = y.no;
         a.e.ystride = y.ystride;
-        for (size_t q = 0; q < y.anchor_vec.size(); ++q) a.e.anchor_vec[q] = y.anchor_vec[q];
+        a.e.anchor_vec = h.blob.at<float>(y.anchor_off);
       }
       // the mfma/valu choice was fixed when the weights were packed
       a.w_f32 = st.pc.mfma ? 0 : 1;
+      a.w_stem = h.blob.at<void>(st.pc.stem_off);
+      a.w_u8 = h.blob.at<void>(st.pc.stem_u8_off);
       launch_conv(a, h.dtype, s);
     } else if (st.kind == ST_MAXPOOL) {
       launch_maxpool(nullptr, tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, st.k, st.s, st.p, st.zero_rb,
@@ -630,6 +638,17 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     a.in_kind = st.in_t < 0 ? IN_FRAME_U8 : IN_NHWC;
     a.cout_pad = st.pc.cout_pad;
     a.w_f32 = st.pc.mfma ? 0 : 1;
+    a.cin = st.cin;
+    a.ks = st.ks;
+    a.stride = st.stride;
+    a.pad = st.pad;
+    a.ih = st.ih;
+    a.iw = st.iw;
+    a.oh = st.oh;
+    a.ow = st.ow;
+    a.quad = st.quad ? 1 : 0;
+    a.w_stem = st.pc.stem_off != SIZE_MAX ? (const void*)1 : nullptr;
+    a.w_u8 = a.w_stem;
     name = conv_kernel_name(a, h.dtype);
     flop = 2.0 * st.oh * st.ow * (double)st.cout * st.cin * st.ks * st.ks;
     double out = 0;
