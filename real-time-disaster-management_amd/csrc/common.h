@@ -137,7 +137,6 @@ struct ConvArgs {
   int kpad = 0, cout_pad = 0;
   int w_f32 = 0;            // weights packed fp32 for the VALU body (else fp16 MFMA layout)
   const void* w_stem = nullptr;  // MFMA stem (Cin=3, 3x3): fp16 [cout_pad][32], k = (kh*3+kw)*3+c
-  const void* w_u8 = nullptr;    // the same divided by 255 (uint8 frame input)
   Epilogue e;
 };
 

@@ -424,22 +424,44 @@ __global__ __launch_bounds__(256) void conv_stem_mfma(ConvArgs a) {
   const int TW = W + 2;
   // ---- stage input rows y0-1 .. y0+R into LDS (zero border) ----
   const int nrow = R + 2;
-  for (int idx = tid; idx < nrow * TW * 3; idx += 256) {
-    const int c = idx % 3;
-    const int t = idx / 3;
-    const int x = t % TW - 1;
-    const int y = t / TW + y0 - 1;
-    float v = 0.f;
-    if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
-      if (a.in_kind == IN_FRAME_U8)
-        v = (float)((const uint8_t*)a.in)[((size_t)(n * H + y) * W + x) * 3 + c];
-      else if (a.in_kind == IN_NCHW_F32)
-        v = ((const float*)a.in)[(((size_t)n * 3 + c) * H + y) * W + x];
-      else
-        v = (float)((const _Float16*)a.in)[(((size_t)n * 3 + c) * H + y) * W + x];
+  if (a.in_kind == IN_FRAME_U8 && (W * 3) % 16 == 0) {
+    // 16-byte loads of whole frame rows (uint8 is exact in fp16)
+    const int vpr = W * 3 / 16;
+    for (int idx = tid; idx < nrow * vpr; idx += 256) {
+      const int rr = idx / vpr, v = idx - (idx / vpr) * vpr;
+      const int y = y0 - 1 + rr;
+      u32x4 d = {0u, 0u, 0u, 0u};
+      if ((unsigned)y < (unsigned)H) d = *(const u32x4*)((const uint8_t*)a.in + ((size_t)(n * H + y) * W) * 3 + v * 16);
+      _Float16* dst = tile + (rr * TW + 1) * 3 + v * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) dst[q * 4 + b] = (_Float16)(float)((d[q] >> (8 * b)) & 0xffu);
     }
-    tile[idx] = (_Float16)v;
+    for (int idx = tid; idx < nrow * 6; idx += 256) {  // left / right zero border
+      const int rr = idx / 6, e = idx - (idx / 6) * 6;
+      tile[(rr * TW + (e < 3 ? 0 : W + 1)) * 3 + (e % 3)] = (_Float16)0.f;
+    }
+  } else {
+    for (int idx = tid; idx < nrow * TW * 3; idx += 256) {
+      const int c = idx % 3;
+      const int t = idx / 3;
+      const int x = t % TW - 1;
+      const int y = t / TW + y0 - 1;
+      float v = 0.f;
+      if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
+        if (a.in_kind == IN_FRAME_U8)
+          v = (float)((const uint8_t*)a.in)[((size_t)(n * H + y) * W + x) * 3 + c];
+        else if (a.in_kind == IN_NCHW_F32)
+          v = ((const float*)a.in)[(((size_t)n * 3 + c) * H + y) * W + x];
+        else
+          v = (float)((const _Float16*)a.in)[(((size_t)n * 3 + c) * H + y) * W + x];
+      }
+      tile[idx] = (_Float16)v;
+    }
   }
+  // uint8 frames enter as 0..255: apply the /255 of detect.py:82 to the fp32 accumulator
+  const float in_scale = a.in_kind == IN_FRAME_U8 ? 1.f / 255.f : 1.f;
   // ---- per-lane K slice: 8 LDS offsets relative to the pixel's window ----
   const int kg = (lane >> 4) * 8;
   int koff[8];
@@ -452,7 +474,7 @@ __global__ __launch_bounds__(256) void conv_stem_mfma(ConvArgs a) {
     const int kh = tap / 3, kw = tap - (tap / 3) * 3;
     koff[j] = kval[j] ? (kh * TW + kw) * 3 + c : 0;
   }
-  const _Float16* wsrc = (const _Float16*)(a.in_kind == IN_FRAME_U8 ? a.w_u8 : a.w_stem);
+  const _Float16* wsrc = (const _Float16*)a.w_stem;
   const int ntn = a.cout_pad / 16;
   __syncthreads();
   const int r = lane & 15;
@@ -489,7 +511,7 @@ __global__ __launch_bounds__(256) void conv_stem_mfma(ConvArgs a) {
     }
     for (int tn = 0; tn < ntn; ++tn) {
       const h8 bf = *(const h8*)(wsrc + (size_t)(tn * 16 + r) * 32 + kg);
-      f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0) * in_scale;
       const int c = tn * 16 + r;
       if (c < a.cout && nvalid == 4) epi4<_Float16>(a, m0, c, acc);
       else if (c < a.cout && nvalid > 0) {
@@ -610,7 +632,7 @@ static bool mfma_ok(const ConvArgs& a) {
 }
 
 static bool stem_ok(const ConvArgs& a) {
-  return a.w_u8 && a.w_stem && a.in_kind != IN_NHWC && a.cin == 3 && a.ks == 3 && a.stride == 1 && a.pad == 1 &&
+  return a.w_stem && a.in_kind != IN_NHWC && a.cin == 3 && a.ks == 3 && a.stride == 1 && a.pad == 1 &&
          a.iw <= kStemMaxW && a.oh == a.ih && a.ow == a.iw && a.cout_pad % 16 == 0 &&
          (a.quad ? (a.oh % 2 == 0 && a.ow % 2 == 0) : true);
 }

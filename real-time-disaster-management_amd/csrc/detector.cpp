@@ -508,8 +508,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       st.pc = pack_conv(blob, st.w_W, filters, st.cin, size, st.bn ? sc.data() : nullptr, use_mfma);
       st.pc.b_off = blob.add_f32(b);
       if (f16 && st.in_t < 0 && st.cin == 3 && size == 3 && st.stride == 1 && st.pad == 1) {
-        st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr, 1.0);
-        st.pc.stem_u8_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr, 255.0);
+        st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr);
       }
     } else {
       st.pc.cout = filters;
@@ -613,7 +612,6 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       // the mfma/valu choice was fixed when the weights were packed
       a.w_f32 = st.pc.mfma ? 0 : 1;
       a.w_stem = h.blob.at<void>(st.pc.stem_off);
-      a.w_u8 = h.blob.at<void>(st.pc.stem_u8_off);
       launch_conv(a, h.dtype, s);
     } else if (st.kind == ST_MAXPOOL) {
       launch_maxpool(nullptr, tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, st.k, st.s, st.p, st.zero_rb,
@@ -648,7 +646,6 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     a.ow = st.ow;
     a.quad = st.quad ? 1 : 0;
     a.w_stem = st.pc.stem_off != SIZE_MAX ? (const void*)1 : nullptr;
-    a.w_u8 = a.w_stem;
     name = conv_kernel_name(a, h.dtype);
     flop = 2.0 * st.oh * st.ow * (double)st.cout * st.cin * st.ks * st.ks;
     double out = 0;

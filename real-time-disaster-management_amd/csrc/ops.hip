@@ -65,10 +65,72 @@ static inline int grid_for(int64_t total, int block) {
   return (int)g;
 }
 
+// Vector form: one thread per (output pixel, 8 fp16 / 4 fp32 channels): 27
+// 16-byte loads (3 branches x 9 taps) instead of 27 scalar loads per channel.
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void dw3_acff_vec_kernel(const T* __restrict__ in, int in_cs, int in_co, int n,
+                                                           int h, int w, int c, int lim_h, int lim_w,
+                                                           const float* __restrict__ wts,
+                                                           const float* __restrict__ bias, T* __restrict__ out) {
+  typedef T tv __attribute__((ext_vector_type(VEC)));
+  const int oh = h - 2, ow = w - 2;
+  const int cg = c / VEC;
+  const int64_t total = (int64_t)n * lim_h * lim_w * cg;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(idx % cg);
+    int64_t p = idx / cg;
+    const int ox = (int)(p % lim_w);
+    p /= lim_w;
+    const int oy = (int)(p % lim_h);
+    const int b = (int)(p / lim_h);
+    const int ch0 = g * VEC;
+    const T* src = in + (size_t)b * h * w * in_cs + in_co + ch0;
+    T* dst = out + (((size_t)b * oh + oy) * ow + ox) * (3 * c) + ch0;
+#pragma unroll
+    for (int br = 0; br < 3; ++br) {
+      const int d = br + 1;
+      float acc[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] = bias[br * c + ch0 + j];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int iy = oy + 1 + (kh - 1) * d;
+        if ((unsigned)iy >= (unsigned)h) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int ix = ox + 1 + (kw - 1) * d;
+          if ((unsigned)ix >= (unsigned)w) continue;
+          const tv x = *(const tv*)(src + ((size_t)iy * w + ix) * in_cs);
+#pragma unroll
+          for (int j = 0; j < VEC; ++j)
+            acc[j] = fmaf(wts[((size_t)br * c + ch0 + j) * 9 + kh * 3 + kw], (float)x[j], acc[j]);
+        }
+      }
+      tv o;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = (T)acc[j];
+      *(tv*)(dst + br * c) = o;
+    }
+  }
+}
+
 void launch_dw3_acff(const void* in, int in_cs, int in_co, int n, int h, int w, int c, int lim_h, int lim_w,
                      const float* wts, const float* bias, void* out, int dtype, hipStream_t s) {
   const int64_t total = (int64_t)n * lim_h * lim_w * c;
   if (total <= 0) return;
+  const int vec = dtype == RTDM_F16 ? 8 : 4;
+  if (c % vec == 0 && in_cs % vec == 0 && in_co % vec == 0) {
+    const int gv = grid_for(total / vec, 256);
+    if (dtype == RTDM_F16)
+      hipLaunchKernelGGL((dw3_acff_vec_kernel<_Float16, 8>), dim3(gv), dim3(256), 0, s, (const _Float16*)in, in_cs,
+                         in_co, n, h, w, c, lim_h, lim_w, wts, bias, (_Float16*)out);
+    else
+      hipLaunchKernelGGL((dw3_acff_vec_kernel<float, 4>), dim3(gv), dim3(256), 0, s, (const float*)in, in_cs, in_co,
+                         n, h, w, c, lim_h, lim_w, wts, bias, (float*)out);
+    RTDM_HIP(hipGetLastError());
+    return;
+  }
   const int g = grid_for(total, 256);
   if (dtype == RTDM_F16)
     hipLaunchKernelGGL(dw3_acff_kernel<_Float16>, dim3(g), dim3(256), 0, s, (const _Float16*)in, in_cs, in_co, n, h,
@@ -116,11 +178,64 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ in, 
   }
 }
 
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void maxpool_vec_kernel(const T* __restrict__ in, int in_cs, int in_co, int n,
+                                                          int h, int w, int c, int k, int stride, int pad,
+                                                          int zero_rb, T* __restrict__ out, int out_cs, int out_co,
+                                                          int oh, int ow) {
+  typedef T tv __attribute__((ext_vector_type(VEC)));
+  const int cg = c / VEC;
+  const int64_t total = (int64_t)n * oh * ow * cg;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(idx % cg);
+    int64_t p = idx / cg;
+    const int ox = (int)(p % ow);
+    p /= ow;
+    const int oy = (int)(p % oh);
+    const int b = (int)(p / oh);
+    float m[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) m[j] = -INFINITY;
+    const int y0 = oy * stride - pad, x0 = ox * stride - pad;
+    for (int dy = 0; dy < k; ++dy) {
+      const int iy = y0 + dy;
+      for (int dx = 0; dx < k; ++dx) {
+        const int ix = x0 + dx;
+        if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w) {
+          const tv v = *(const tv*)(in + (((size_t)b * h + iy) * w + ix) * in_cs + in_co + g * VEC);
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+        } else if (zero_rb) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) m[j] = fmaxf(m[j], 0.f);
+        }
+      }
+    }
+    tv o;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = (T)m[j];
+    *(tv*)(out + (((size_t)b * oh + oy) * ow + ox) * out_cs + out_co + g * VEC) = o;
+  }
+}
+
 void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, int stride, int pad, int zero_rb,
                     View ov, int oh, int ow, int dtype, hipStream_t s) {
   (void)in;
   const int64_t total = (int64_t)n * oh * ow * c;
   if (total <= 0) return;
+  const int vec = dtype == RTDM_F16 ? 8 : 4;
+  if (c % vec == 0 && ((iv.cs | iv.co | ov.cs | ov.co) % vec) == 0) {
+    const int gv = grid_for(total / vec, 256);
+    if (dtype == RTDM_F16)
+      hipLaunchKernelGGL((maxpool_vec_kernel<_Float16, 8>), dim3(gv), dim3(256), 0, s, (const _Float16*)iv.ptr, iv.cs,
+                         iv.co, n, h, w, c, k, stride, pad, zero_rb, (_Float16*)ov.ptr, ov.cs, ov.co, oh, ow);
+    else
+      hipLaunchKernelGGL((maxpool_vec_kernel<float, 4>), dim3(gv), dim3(256), 0, s, (const float*)iv.ptr, iv.cs, iv.co,
+                         n, h, w, c, k, stride, pad, zero_rb, (float*)ov.ptr, ov.cs, ov.co, oh, ow);
+    RTDM_HIP(hipGetLastError());
+    return;
+  }
   const int g = grid_for(total, 256);
   if (dtype == RTDM_F16)
     hipLaunchKernelGGL(maxpool_kernel<_Float16>, dim3(g), dim3(256), 0, s, (const _Float16*)iv.ptr, iv.cs, iv.co, n,

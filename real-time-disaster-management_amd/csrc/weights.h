@@ -36,12 +36,12 @@ struct PackedConv {
   bool mfma = false;      // fp16 MFMA layout (else fp32 for the VALU kernel)
   size_t w_off = 0;       // [cout_pad][kpad]
   size_t b_off = SIZE_MAX, s_off = SIZE_MAX, t_off = SIZE_MAX;  // bias / post scale / post shift
-  size_t stem_off = SIZE_MAX, stem_u8_off = SIZE_MAX;            // MFMA stem copies (Cin=3, 3x3)
+  size_t stem_off = SIZE_MAX;  // MFMA stem copy (Cin=3, 3x3)
 };
 
 // Cin=3 3x3 stem weights for conv_stem_mfma: fp16 [cout_pad16][32], K = (kh*3+kw)*3 + c
-// (27 used), optionally divided by 255 (uint8 frames feed raw 0..255 values).
-inline size_t pack_stem(Blob& blob, const float* w, int cout, const double* oscale, double div) {
+// (27 used).
+inline size_t pack_stem(Blob& blob, const float* w, int cout, const double* oscale) {
   const int cp = (int)round_up(cout, 16);
   std::vector<_Float16> h((size_t)cp * 32, (_Float16)0.f);
   for (int o = 0; o < cout; ++o)
@@ -50,7 +50,7 @@ inline size_t pack_stem(Blob& blob, const float* w, int cout, const double* osca
         for (int kw = 0; kw < 3; ++kw) {
           double v = w[(((size_t)o * 3 + c) * 3 + kh) * 3 + kw];
           if (oscale) v *= oscale[o];
-          h[(size_t)o * 32 + (kh * 3 + kw) * 3 + c] = (_Float16)(float)(v / div);
+          h[(size_t)o * 32 + (kh * 3 + kw) * 3 + c] = (_Float16)(float)v;
         }
   return blob.add(h.data(), h.size() * sizeof(_Float16));
 }
