@@ -124,6 +124,29 @@ struct Epilogue {
   const float* anchor_vec = nullptr;  // device [na][2]: anchors / stride, fp32 like models.py:431
 };
 
+// Branch-free unsigned division by a runtime-invariant divisor (round-up
+// multiplier, Hacker's Delight 10-8 / libdivide u32 "add" variant): valid for
+// 0 <= n < 2^31.  Built on the host, 4-5 VALU ops on the device.
+struct FastDiv {
+  uint32_t m = 0;
+  int l = 0;  // ceil(log2 d)
+  int d = 1;
+};
+inline FastDiv make_fastdiv(int d) {
+  FastDiv f;
+  f.d = d < 1 ? 1 : d;
+  int l = 0;
+  while ((1ll << l) < f.d) ++l;
+  f.l = l;
+  f.m = l == 0 ? 0u : (uint32_t)(((((uint64_t)1 << 32) * (((uint64_t)1 << l) - (uint64_t)f.d)) / (uint64_t)f.d) + 1);
+  return f;
+}
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  if (f.l == 0) return n;
+  const uint32_t t = __umulhi((uint32_t)n, f.m);
+  return (int)((t + (((uint32_t)n - t) >> 1)) >> (f.l - 1));
+}
+
 struct ConvArgs {
   const void* in = nullptr;
   int in_cs = 0, in_co = 0, in_kind = IN_NHWC;
@@ -133,6 +156,7 @@ struct ConvArgs {
   int quad = 0;  // M ordering: 1 => groups of 4 rows are 2x2 pixel quads
   int qh = 0, qw = 0;
   int M = 0;     // rows of the implicit GEMM
+  FastDiv fd_ow, fd_oh, fd_qw, fd_qh;  // set by conv_set_rows
   const void* w = nullptr;  // packed weights [cout_pad][kpad], k = (kh*ks+kw)*cin + c
   int kpad = 0, cout_pad = 0;
   int w_f32 = 0;            // weights packed fp32 for the VALU body (else fp16 MFMA layout)
@@ -153,6 +177,10 @@ inline void conv_set_rows(ConvArgs& a) {
   } else {
     a.M = a.n * a.oh * a.ow;
   }
+  a.fd_ow = make_fastdiv(a.ow);
+  a.fd_oh = make_fastdiv(a.oh);
+  a.fd_qw = make_fastdiv(a.qw);
+  a.fd_qh = make_fastdiv(a.qh);
 }
 
 // ----------------------------------------------------------- other ops ----

@@ -38,43 +38,58 @@ __device__ __forceinline__ void stf(T* p, float v) {
 __device__ __forceinline__ void row_to_pix(const ConvArgs& a, int m, int& n, int& oy, int& ox) {
   if (a.quad) {
     const int q = m >> 2, d = m & 3;
-    const int qx = q % a.qw;
-    const int t = q / a.qw;
-    const int qy = t % a.qh;
-    n = t / a.qh;
+    const int t = fdiv(q, a.fd_qw);
+    const int qx = q - t * a.qw;
+    n = fdiv(t, a.fd_qh);
+    const int qy = t - n * a.qh;
     oy = 2 * qy + (d >> 1);
     ox = 2 * qx + (d & 1);
   } else {
-    ox = m % a.ow;
-    const int t = m / a.ow;
-    oy = t % a.oh;
-    n = t / a.oh;
+    const int t = fdiv(m, a.fd_ow);
+    ox = m - t * a.ow;
+    n = fdiv(t, a.fd_oh);
+    oy = t - n * a.oh;
   }
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
+
+// Pixel of row m0 + r given the pixel (n, oy0, ox0) of row m0 (m0 % 4 == 0):
+// quad order -> the 2x2 quad; linear order -> the next pixels of the same image
+// row when they exist (row_to_pix otherwise).
+__device__ __forceinline__ void row_pix4(const ConvArgs& a, int m0, int r, int n0, int oy0, int ox0, int& n, int& oy,
+                                         int& ox) {
+  if (a.quad) {
+    n = n0;
+    oy = oy0 + (r >> 1);
+    ox = ox0 + (r & 1);
+  } else if (ox0 + r < a.ow) {
+    n = n0;
+    oy = oy0;
+    ox = ox0 + r;
+  } else {
+    row_to_pix(a, m0 + r, n, oy, ox);
+  }
+}
 
 // Epilogue for the 4 accumulator values of rows m0..m0+3 (m0 % 4 == 0) in
 // output channel c.  In quad mode the 4 rows are one 2x2 pixel quad.
 template <typename T>
 __device__ __forceinline__ void epi4(const ConvArgs& a, int m0, int c, f4 v) {
   const Epilogue& e = a.e;
+  if (m0 >= a.M) return;
   const float bias = e.bias ? e.bias[c] : 0.f;
   const float sc = e.scale ? e.scale[c] : 1.f;
   const float sh = e.scale ? e.shift[c] : 0.f;
   float pmax = -INFINITY;
-  int pn = 0, poy = 0, pox = 0;
+  int n0, oy0, ox0;
+  row_to_pix(a, m0, n0, oy0, ox0);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int m = m0 + r;
     if (m < a.M) {
       int n, oy, ox;
-      row_to_pix(a, m, n, oy, ox);
-      if (r == 0) {
-        pn = n;
-        poy = oy;
-        pox = ox;
-      }
+      row_pix4(a, m0, r, n0, oy0, ox0, n, oy, ox);
       float x = v[r] + bias;
       if (e.act == ACT_LEAKY) {
         x = x > 0.f ? x : x * e.slope;
@@ -111,8 +126,8 @@ __device__ __forceinline__ void epi4(const ConvArgs& a, int m0, int c, f4 v) {
       }
     }
   }
-  if (e.pool.ptr && a.quad && m0 < a.M) {
-    const size_t pp = ((size_t)pn * a.qh + (poy >> 1)) * a.qw + (pox >> 1);
+  if (e.pool.ptr && a.quad) {
+    const size_t pp = ((size_t)n0 * a.qh + (oy0 >> 1)) * a.qw + (ox0 >> 1);
     stf((T*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c, pmax);
   }
 }
@@ -138,18 +153,14 @@ __device__ __forceinline__ void epi_vec8(const ConvArgs& a, int m0, int c0, cons
   float pmax[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) pmax[j] = -INFINITY;
-  int pn = 0, poy = 0, pox = 0;
+  int pn, poy, pox;
+  row_to_pix(a, m0, pn, poy, pox);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int m = m0 + r;
     if (m >= a.M) continue;
     int n, oy, ox;
-    row_to_pix(a, m, n, oy, ox);
-    if (r == 0) {
-      pn = n;
-      poy = oy;
-      pox = ox;
-    }
+    row_pix4(a, m0, r, pn, poy, pox, n, oy, ox);
     const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
     float x[8];
 #pragma unroll
