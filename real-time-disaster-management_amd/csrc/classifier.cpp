@@ -110,10 +110,12 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
         wf[o * 27 + q] = (float)acc;
       }
     h.stem = pack_conv(blob, wf.data(), 8, 3, 3, nullptr, false);
+    if (f16) h.stem.stem_off = pack_stem(blob, wf.data(), 8, nullptr);
     h.stem.b_off = blob.add(br, 8 * sizeof(float));
     h.stem_cout = 8;
   } else {
     h.stem = pack_conv(blob, w1, 16, 3, 3, nullptr, false);
+    if (f16) h.stem.stem_off = pack_stem(blob, w1, 16, nullptr);
     h.stem_cout = 16;
   }
 
@@ -301,6 +303,7 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
   a.kpad = h.stem.kpad;
   a.cout_pad = h.stem.cout_pad;
   a.w_f32 = h.stem.mfma ? 0 : 1;
+  a.w_stem = h.blob.at<void>(h.stem.stem_off);
   a.e.bias = h.blob.at<float>(h.stem.b_off);
   a.e.full = View{buf(h.stem_buf), h.stem_cout, 0};
   launch_conv(a, h.dtype, s);

@@ -414,127 +414,209 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_f16(ConvArgs a) {
 }
 
 // --------------------------------------------------------------------------
-// fp16 MFMA stem: Cin = 3, 3x3, stride 1, pad 1 (the Darknet first conv, fed by
-// uint8 frames or NCHW model inputs).  One block = one output row (linear M
-// order) or one 2-row quad band (quad order, fused 2x2 maxpool).  The input
-// rows the band needs are staged into LDS as fp16 (uint8 is exact in fp16; the
-// /255 is folded into the uint8 weight copy), then every lane gathers its
-// 8-element K slice (k = (kh*3 + kw)*3 + c, 27 padded to 32) for one
-// v_mfma_f32_16x16x32_f16 per 16 output pixels per 16 output channels.
+// fp16 MFMA stem: Cin = 3, 3x3, stride 1|2, pad 0|1 — the Darknet first conv
+// (uint8 frames or NCHW model inputs, detect.py:80-82 /255 applied to the fp32
+// accumulator) and the ACFF classifiers' conv1 (squeeze_ernet.py:11, ernet.py:10;
+// fp16 NHWC output of the fused CLI transform or NCHW model inputs).
+//
+// Output-channel-major GEMM, D[cout][pixel] = W[cout][k] x X[k][pixel], on
+// v_mfma_f32_16x16x32_f16: the weight fragments (A) are loaded once per block
+// and stay in registers; each lane's B fragment is 8 contiguous fp16 of the LDS
+// input image, so one MFMA tile costs 2 x (2 ds_read_b64) per lane.
+//   LDS image: the block's input rows, every pixel padded to 4 channels
+//              (c0,c1,c2,0) = 8 bytes, zero columns/rows for the padding.
+//   K (64 = 2 MFMA k-steps): group G = 0..5 -> (kh = G>>1, pixel pair
+//              kw in {0,1} | {2,3}), 8 values = 2 pixels x 4 channels; G = 6,7
+//              are zero.  Weights for kw = 3 and c = 3 are zero.
+//   D layout:  lane = pixel (lane & 15), 4 consecutive channels per lane
+//              ((lane >> 4) * 4 + j) -> 8-byte NHWC stores; in quad order the
+//              16 pixels are 4 2x2 quads on lane groups of 4, so the fused 2x2
+//              maxpool is two DPP quad_perm max steps.
+// One block = kStemRows output rows of one image, 4 waves stride over the
+// 16-pixel tiles of those rows.
 // --------------------------------------------------------------------------
-constexpr int kStemMaxW = 1024;
-__global__ __launch_bounds__(256) void conv_stem_mfma(ConvArgs a) {
-  __shared__ _Float16 tile[4 * (kStemMaxW + 2) * 3];
+constexpr int kStemRows = 4;
+
+__device__ __forceinline__ uint32_t pack_h2(float a, float b) {
+  const _Float16 ha = (_Float16)a, hb = (_Float16)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+}
+
+template <bool POOL, int NTN>
+__global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint2 stem_lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int R = a.quad ? 2 : 1;                 // output rows per block
-  const int rows_per_img = a.quad ? a.qh : a.oh;
-  const int n = blockIdx.x / rows_per_img;
-  const int yb = blockIdx.x - n * rows_per_img;  // quad row or output row
-  const int y0 = yb * R;
-  const int W = a.iw, H = a.ih;
-  const int TW = W + 2;
-  // ---- stage input rows y0-1 .. y0+R into LDS (zero border) ----
-  const int nrow = R + 2;
-  if (a.in_kind == IN_FRAME_U8 && (W * 3) % 16 == 0) {
-    // 16-byte loads of whole frame rows (uint8 is exact in fp16)
-    const int vpr = W * 3 / 16;
-    for (int idx = tid; idx < nrow * vpr; idx += 256) {
-      const int rr = idx / vpr, v = idx - (idx / vpr) * vpr;
-      const int y = y0 - 1 + rr;
-      u32x4 d = {0u, 0u, 0u, 0u};
-      if ((unsigned)y < (unsigned)H) d = *(const u32x4*)((const uint8_t*)a.in + ((size_t)(n * H + y) * W) * 3 + v * 16);
-      _Float16* dst = tile + (rr * TW + 1) * 3 + v * 16;
+  const int s = a.stride, pad = a.pad;
+  const int bpi = (a.oh + kStemRows - 1) / kStemRows;
+  const int n = blockIdx.x / bpi;
+  const int oy0 = (blockIdx.x - n * bpi) * kStemRows;
+  const int nrows = (kStemRows - 1) * s + 3;
+  const int cols = (a.ow - 1) * s - pad + 5;  // LDS column = x + 1, x in [-1, (ow-1)*s - pad + 3]
+  const int iy0 = oy0 * s - pad;
+  const int H = a.ih, W = a.iw;
+
+  // ---- stage the input rows iy0 .. iy0+nrows-1 (fp16, 4 channels / pixel) ----
+  if (a.in_kind == IN_FRAME_U8 && (W & 3) == 0 && cols >= W + 1) {
+    const int gpr = W >> 2;  // 4-pixel groups per row (12 bytes)
+    for (int idx = tid; idx < nrows * gpr; idx += 256) {
+      const int r = idx / gpr, g = idx - r * gpr;
+      const int y = iy0 + r;
+      uint32_t d0 = 0, d1 = 0, d2 = 0;
+      if ((unsigned)y < (unsigned)H) {
+        const uint32_t* src = (const uint32_t*)((const uint8_t*)a.in + ((size_t)(n * H + y) * W + 4 * g) * 3);
+        d0 = src[0];
+        d1 = src[1];
+        d2 = src[2];
+      }
+      const uint32_t b[12] = {d0 & 255u, (d0 >> 8) & 255u, (d0 >> 16) & 255u, d0 >> 24,
+                              d1 & 255u, (d1 >> 8) & 255u, (d1 >> 16) & 255u, d1 >> 24,
+                              d2 & 255u, (d2 >> 8) & 255u, (d2 >> 16) & 255u, d2 >> 24};
+      uint2* dst = stem_lds + r * cols + 4 * g + 1;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) dst[q * 4 + b] = (_Float16)(float)((d[q] >> (8 * b)) & 0xffu);
+      for (int p = 0; p < 4; ++p)
+        dst[p] = make_uint2(pack_h2((float)b[3 * p], (float)b[3 * p + 1]), pack_h2((float)b[3 * p + 2], 0.f));
     }
-    for (int idx = tid; idx < nrow * 6; idx += 256) {  // left / right zero border
-      const int rr = idx / 6, e = idx - (idx / 6) * 6;
-      tile[(rr * TW + (e < 3 ? 0 : W + 1)) * 3 + (e % 3)] = (_Float16)0.f;
+    for (int idx = tid; idx < nrows * cols; idx += 256) {  // padding columns
+      const int r = idx / cols, lc = idx - r * cols;
+      if (lc == 0 || lc > W) stem_lds[r * cols + lc] = make_uint2(0u, 0u);
     }
   } else {
-    for (int idx = tid; idx < nrow * TW * 3; idx += 256) {
-      const int c = idx % 3;
-      const int t = idx / 3;
-      const int x = t % TW - 1;
-      const int y = t / TW + y0 - 1;
-      float v = 0.f;
+    for (int idx = tid; idx < nrows * cols; idx += 256) {
+      const int r = idx / cols, lc = idx - r * cols;
+      const int y = iy0 + r, x = lc - 1;
+      float v[3] = {0.f, 0.f, 0.f};
       if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
-        if (a.in_kind == IN_FRAME_U8)
-          v = (float)((const uint8_t*)a.in)[((size_t)(n * H + y) * W + x) * 3 + c];
-        else if (a.in_kind == IN_NCHW_F32)
-          v = ((const float*)a.in)[(((size_t)n * 3 + c) * H + y) * W + x];
-        else
-          v = (float)((const _Float16*)a.in)[(((size_t)n * 3 + c) * H + y) * W + x];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          if (a.in_kind == IN_FRAME_U8)
+            v[c] = (float)((const uint8_t*)a.in)[((size_t)(n * H + y) * W + x) * 3 + c];
+          else if (a.in_kind == IN_NCHW_F32)
+            v[c] = ((const float*)a.in)[(((size_t)n * 3 + c) * H + y) * W + x];
+          else if (a.in_kind == IN_NCHW_F16)
+            v[c] = (float)((const _Float16*)a.in)[(((size_t)n * 3 + c) * H + y) * W + x];
+          else
+            v[c] = (float)((const _Float16*)a.in)[((size_t)(n * H + y) * W + x) * a.in_cs + a.in_co + c];
+        }
       }
-      tile[idx] = (_Float16)v;
+      stem_lds[idx] = make_uint2(pack_h2(v[0], v[1]), pack_h2(v[2], 0.f));
     }
   }
-  // uint8 frames enter as 0..255: apply the /255 of detect.py:82 to the fp32 accumulator
+
+  // ---- per-lane constants: weight fragments and epilogue vectors ----
+  // POOL (pixel-major, D[pixel][cout]): lane = channel (lane & 15), 4 pixels per
+  //   lane = one 2x2 quad -> the maxpool is in-lane; 2-byte stores.
+  // !POOL (channel-major, D[cout][pixel]): lane = pixel, 4 channels per lane ->
+  //   8-byte stores.
+  const int p = lane & 15, g = lane >> 4;
+  const Epilogue& e = a.e;
+  h8 wa[NTN][2];
+  constexpr int NE = POOL ? 1 : 4;  // epilogue channels per lane per cout tile
+  float bias[NTN][NE], sc[NTN][NE], sh[NTN][NE];
+#pragma unroll
+  for (int t = 0; t < NTN; ++t) {
+    const _Float16* wp = (const _Float16*)a.w_stem + (size_t)(16 * t + p) * 64 + 8 * g;
+    wa[t][0] = *(const h8*)wp;
+    wa[t][1] = *(const h8*)(wp + 32);
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int c = POOL ? 16 * t + p : 16 * t + 4 * g + j;
+      const bool cv = c < a.cout;
+      bias[t][j] = (e.bias && cv) ? e.bias[c] : 0.f;
+      sc[t][j] = (e.scale && cv) ? e.scale[c] : 1.f;
+      sh[t][j] = (e.scale && cv) ? e.shift[c] : 0.f;
+    }
+  }
   const float in_scale = a.in_kind == IN_FRAME_U8 ? 1.f / 255.f : 1.f;
-  // ---- per-lane K slice: 8 LDS offsets relative to the pixel's window ----
-  const int kg = (lane >> 4) * 8;
-  int koff[8];
-  bool kval[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = kg + j;
-    kval[j] = k < 27;
-    const int tap = k / 3, c = k - (k / 3) * 3;
-    const int kh = tap / 3, kw = tap - (tap / 3) * 3;
-    koff[j] = kval[j] ? (kh * TW + kw) * 3 + c : 0;
-  }
-  const _Float16* wsrc = (const _Float16*)a.w_stem;
-  const int ntn = a.cout_pad / 16;
+  const int act = e.act;
+  const float slope = e.slope;
   __syncthreads();
-  const int r = lane & 15;
-  int groups;  // 16-pixel MFMA row groups in this block
-  if (a.quad)
-    groups = (a.qw + 3) / 4;
-  else
-    groups = (a.ow + 15) / 16;
-  for (int g = wid; g < groups; g += 4) {
-    int py, px;  // pixel of this lane's A row, relative to the band
-    if (a.quad) {
-      const int qx = g * 4 + (r >> 2), d = r & 3;
-      py = d >> 1;
-      px = 2 * qx + (d & 1);
-    } else {
-      py = 0;
-      px = g * 16 + r;
-    }
-    const bool pv = px < a.ow;
-    const int base = (py * TW + (pv ? px : 0)) * 3;
-    h8 af;
+
+  auto epi = [&](float x, int t, int j) {
+    x = x * in_scale + bias[t][j];
+    if (act == ACT_LEAKY)
+      x = x > 0.f ? x : x * slope;
+    else if (act == ACT_SWISH)
+      x = x * sigmoidf_(x);
+    return x * sc[t][j] + sh[t][j];
+  };
+  const int kh0 = g >> 1, pr0 = g & 1;
+  if (POOL) {
+    // waves 0,1 -> quad row 0, waves 2,3 -> quad row 1 (kStemRows == 4); a wave's
+    // tiles are 4 consecutive quads, striding by 2 tiles.
+    const int qw = a.ow >> 1, qh = a.oh >> 1;
+    const int tr = wid >> 1;
+    const int py = (oy0 >> 1) + tr;
+    if (py >= qh) return;
+    const int d = p & 3;
+    const int ly = 2 * tr + (d >> 1);  // LDS row of kh = 0 (stride 1 / 2 scaled below)
+    const uint2* rowk0 = stem_lds + (ly * s + kh0) * cols;
+    const uint2* rowk2 = stem_lds + (ly * s + 2) * cols;
+    _Float16* pool_row = (_Float16*)e.pool.ptr + ((size_t)n * qh + py) * qw * e.pool.cs + e.pool.co;
+    for (int tx = wid & 1; tx * 4 < qw; tx += 2) {
+      const int qx = tx * 4 + (p >> 2);
+      const int ox = 2 * (qx < qw ? qx : qw - 1) + (d & 1);
+      const int lx = ox * s - pad + 1;
+      const uint2 b00 = rowk0[lx + 2 * pr0], b01 = rowk0[lx + 2 * pr0 + 1];
+      uint2 b10 = rowk2[lx + 2 * (g & 1)], b11 = rowk2[lx + 2 * (g & 1) + 1];
+      if (g >= 2) b10 = b11 = make_uint2(0u, 0u);
+      const h8 bf0 = __builtin_bit_cast(h8, (u32x4{b00.x, b00.y, b01.x, b01.y}));
+      const h8 bf1 = __builtin_bit_cast(h8, (u32x4{b10.x, b10.y, b11.x, b11.y}));
+      const int oq = tx * 4 + g;  // pooled x of this lane's output quad
 #pragma unroll
-    for (int j = 0; j < 8; ++j) af[j] = kval[j] ? tile[base + koff[j]] : (_Float16)0.f;
-    // epilogue rows of this lane: 4 consecutive M rows
-    int m0, nvalid;
-    if (a.quad) {
-      const int qx = g * 4 + (lane >> 4);
-      m0 = ((n * a.qh + yb) * a.qw + qx) * 4;
-      nvalid = qx < a.qw ? 4 : 0;
-    } else {
-      const int ox = g * 16 + (lane >> 4) * 4;
-      m0 = (n * a.oh + y0) * a.ow + ox;
-      nvalid = a.ow - ox < 4 ? (a.ow - ox > 0 ? a.ow - ox : 0) : 4;
+      for (int t = 0; t < NTN; ++t) {
+        f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf0, wa[t][0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1, wa[t][1], acc, 0, 0, 0);
+        const float m = fmaxf(fmaxf(epi(acc[0], t, 0), epi(acc[1], t, 0)), fmaxf(epi(acc[2], t, 0), epi(acc[3], t, 0)));
+        const int c = 16 * t + p;
+        if (oq < qw && c < a.cout) pool_row[(size_t)oq * e.pool.cs + c] = (_Float16)m;
+      }
     }
-    for (int tn = 0; tn < ntn; ++tn) {
-      const h8 bf = *(const h8*)(wsrc + (size_t)(tn * 16 + r) * 32 + kg);
-      f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0) * in_scale;
-      const int c = tn * 16 + r;
-      if (c < a.cout && nvalid == 4) epi4<_Float16>(a, m0, c, acc);
-      else if (c < a.cout && nvalid > 0) {
-        f4 t = acc;
-        ConvArgs b = a;
-        b.M = m0 + nvalid;  // mask rows beyond the image row
-        epi4<_Float16>(b, m0, c, t);
+  } else {
+    const int tiles_x = (a.ow + 15) >> 4;
+    const int ntiles = tiles_x * kStemRows;
+    for (int t = wid; t < ntiles; t += 4) {
+      const int tr = t / tiles_x, tx = t - tr * tiles_x;
+      const int oy = oy0 + tr;
+      if (oy >= a.oh) break;
+      const int ox = tx * 16 + p;
+      const bool valid = ox < a.ow;
+      const int lx = (valid ? ox : a.ow - 1) * s - pad + 1;
+      const uint2* rowk0 = stem_lds + (tr * s + kh0) * cols;
+      const uint2* rowk2 = stem_lds + (tr * s + 2) * cols;
+      const uint2 b00 = rowk0[lx + 2 * pr0], b01 = rowk0[lx + 2 * pr0 + 1];
+      uint2 b10 = rowk2[lx + 2 * (g & 1)], b11 = rowk2[lx + 2 * (g & 1) + 1];
+      if (g >= 2) b10 = b11 = make_uint2(0u, 0u);
+      const h8 bf0 = __builtin_bit_cast(h8, (u32x4{b00.x, b00.y, b01.x, b01.y}));
+      const h8 bf1 = __builtin_bit_cast(h8, (u32x4{b10.x, b10.y, b11.x, b11.y}));
+      const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
+#pragma unroll
+      for (int tt = 0; tt < NTN; ++tt) {
+        f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[tt][0], bf0, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[tt][1], bf1, acc, 0, 0, 0);
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = epi(acc[j], tt, j);
+        const int c0 = 16 * tt + 4 * g;
+        if (valid && e.full.ptr) {
+          _Float16* fp = (_Float16*)e.full.ptr + pix * e.full.cs + e.full.co + c0;
+          if (c0 + 4 <= a.cout) {
+            *(uint2*)fp = make_uint2(pack_h2(v[0], v[1]), pack_h2(v[2], v[3]));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (c0 + j < a.cout) fp[j] = (_Float16)v[j];
+          }
+        }
       }
     }
   }
 }
 
+static size_t stem3_lds_bytes(const ConvArgs& a) {
+  const int nrows = (kStemRows - 1) * a.stride + 3;
+  const int cols = (a.ow - 1) * a.stride - a.pad + 5;
+  return (size_t)nrows * cols * sizeof(uint2);
+}
 // --------------------------------------------------------------------------
 // VALU fp32 implicit GEMM: 64x64 block tile, 16-deep K-blocks, 4x4 per thread.
 // Handles every input kind (NHWC activations, uint8 frames, NCHW tensors) and
@@ -643,13 +725,23 @@ static bool mfma_ok(const ConvArgs& a) {
 }
 
 static bool stem_ok(const ConvArgs& a) {
-  return a.w_stem && a.in_kind != IN_NHWC && a.cin == 3 && a.ks == 3 && a.stride == 1 && a.pad == 1 &&
-         a.iw <= kStemMaxW && a.oh == a.ih && a.ow == a.iw && a.cout_pad % 16 == 0 &&
-         (a.quad ? (a.oh % 2 == 0 && a.ow % 2 == 0) : true);
+  if (!a.w_stem || a.cin != 3 || a.ks != 3 || (a.stride != 1 && a.stride != 2) || a.pad < 0 || a.pad > 1) return false;
+  if (a.in_kind == IN_NHWC && (a.in_cs < 3)) return false;
+  if (a.cout_pad % 16 != 0 || (a.cout_pad != 16 && a.cout_pad != 32 && a.cout_pad != 64)) return false;
+  if (a.e.res.ptr || a.e.up.ptr || a.e.io) return false;
+  if (a.e.full.ptr && ((a.e.full.cs | a.e.full.co) & 3)) return false;
+  // pooled variant: output only the 2x2-pooled view (quad order); plain variant: full view only
+  if (a.quad ? (!a.e.pool.ptr || a.e.full.ptr || (a.oh | a.ow) & 1) : (!a.e.full.ptr || a.e.pool.ptr)) return false;
+  return stem3_lds_bytes(a) <= 64 * 1024;
 }
 
 const char* conv_kernel_name(const ConvArgs& a, int dtype) {
-  if (dtype == RTDM_F16 && stem_ok(a)) return "conv_stem_mfma";
+  if (dtype == RTDM_F16 && stem_ok(a)) {
+    static const char* names[2][3] = {{"conv_stem3<false,1>", "conv_stem3<false,2>", "conv_stem3<false,4>"},
+                                      {"conv_stem3<true,1>", "conv_stem3<true,2>", "conv_stem3<true,4>"}};
+    const int ntn = a.cout_pad / 16;
+    return names[a.quad ? 1 : 0][ntn == 1 ? 0 : ntn == 2 ? 1 : 2];
+  }
   if (dtype == RTDM_F16 && !a.w_f32) {
     if (a.cout_pad >= 128) return "conv_mfma_f16<128,128,64,2,2>";
     if (a.cout_pad == 64) return "conv_mfma_f16<128,64,64,2,2>";
@@ -664,8 +756,18 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
   RTDM_REQUIRE(!a.quad || (a.oh >= 2 && a.ow >= 2), RTDM_E_INVALID, "conv: quad ordering needs >= 2x2 output");
   RTDM_REQUIRE(!a.e.pool.ptr || a.quad, RTDM_E_INVALID, "conv: pooled output needs quad ordering");
   if (dtype == RTDM_F16 && stem_ok(a)) {
-    const int blocks = a.n * (a.quad ? a.qh : a.oh);
-    hipLaunchKernelGGL(conv_stem_mfma, dim3(blocks), dim3(256), 0, s, a);
+    const int blocks = a.n * ((a.oh + kStemRows - 1) / kStemRows);
+    const size_t lds = stem3_lds_bytes(a);
+    const int ntn = a.cout_pad / 16;
+    if (a.quad) {
+      if (ntn == 1) hipLaunchKernelGGL((conv_stem3<true, 1>), dim3(blocks), dim3(256), lds, s, a);
+      else if (ntn == 2) hipLaunchKernelGGL((conv_stem3<true, 2>), dim3(blocks), dim3(256), lds, s, a);
+      else hipLaunchKernelGGL((conv_stem3<true, 4>), dim3(blocks), dim3(256), lds, s, a);
+    } else {
+      if (ntn == 1) hipLaunchKernelGGL((conv_stem3<false, 1>), dim3(blocks), dim3(256), lds, s, a);
+      else if (ntn == 2) hipLaunchKernelGGL((conv_stem3<false, 2>), dim3(blocks), dim3(256), lds, s, a);
+      else hipLaunchKernelGGL((conv_stem3<false, 4>), dim3(blocks), dim3(256), lds, s, a);
+    }
   } else if (dtype == RTDM_F16 && !a.w_f32) {
     RTDM_REQUIRE(mfma_ok(a), RTDM_E_INVALID, "conv: fp16 MFMA weights but input view not 16-byte aligned NHWC");
     if (a.cout_pad >= 128)

@@ -507,7 +507,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       }
       st.pc = pack_conv(blob, st.w_W, filters, st.cin, size, st.bn ? sc.data() : nullptr, use_mfma);
       st.pc.b_off = blob.add_f32(b);
-      if (f16 && st.in_t < 0 && st.cin == 3 && size == 3 && st.stride == 1 && st.pad == 1) {
+      if (f16 && st.in_t < 0 && st.cin == 3 && size == 3 && (st.stride == 1 || st.stride == 2) && st.pad <= 1) {
         st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr);
       }
     } else {

@@ -39,19 +39,22 @@ struct PackedConv {
   size_t stem_off = SIZE_MAX;  // MFMA stem copy (Cin=3, 3x3)
 };
 
-// Cin=3 3x3 stem weights for conv_stem_mfma: fp16 [cout_pad16][32], K = (kh*3+kw)*3 + c
-// (27 used).
+// Cin=3 3x3 stem weights for conv_stem3: fp16 [cout_pad16][64].  K index
+// k = 8*G + j: G < 6 -> kh = G >> 1, kw = 2*(G & 1) + (j >> 2), c = j & 3 (zero
+// when kw == 3 or c == 3); G = 6, 7 zero.  Matches the kernel's LDS image of
+// 4-channel pixels read as 2-pixel x 4-channel groups.
 inline size_t pack_stem(Blob& blob, const float* w, int cout, const double* oscale) {
   const int cp = (int)round_up(cout, 16);
-  std::vector<_Float16> h((size_t)cp * 32, (_Float16)0.f);
+  std::vector<_Float16> h((size_t)cp * 64, (_Float16)0.f);
   for (int o = 0; o < cout; ++o)
-    for (int c = 0; c < 3; ++c)
-      for (int kh = 0; kh < 3; ++kh)
-        for (int kw = 0; kw < 3; ++kw) {
-          double v = w[(((size_t)o * 3 + c) * 3 + kh) * 3 + kw];
-          if (oscale) v *= oscale[o];
-          h[(size_t)o * 32 + (kh * 3 + kw) * 3 + c] = (_Float16)(float)v;
-        }
+    for (int G = 0; G < 6; ++G)
+      for (int j = 0; j < 8; ++j) {
+        const int kh = G >> 1, kw = 2 * (G & 1) + (j >> 2), c = j & 3;
+        if (kw >= 3 || c >= 3) continue;
+        double v = w[(((size_t)o * 3 + c) * 3 + kh) * 3 + kw];
+        if (oscale) v *= oscale[o];
+        h[(size_t)o * 64 + 8 * G + j] = (_Float16)(float)v;
+      }
   return blob.add(h.data(), h.size() * sizeof(_Float16));
 }
 
