@@ -19,6 +19,8 @@ struct AcffStage {
   bool pool = false;                    // 2x2 floor maxpool after the block
   bool affine = true;                   // BN as post-activation affine in epilogue
   size_t dw_w = 0, dw_b = 0;            // [3][cin][9], [3][cin]
+  size_t dw_wt = 0;                     // [3][9][cin] (tap-major copy for the fused kernel)
+  bool fused = false;                   // fp16 fused ACFF kernel (acff.hip)
   PackedConv pw;                        // fused 1x1 conv
   size_t d_buf = 0, out_buf = 0;        // arena offsets (elements) per image
   int oh = 0, ow = 0;                   // dw/1x1 output geometry
@@ -172,6 +174,11 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
     }
     st.dw_w = blob.add_f32(dww);
     st.dw_b = blob.add_f32(dwb);
+    std::vector<float> dwt(dww.size());
+    for (int br = 0; br < 3; ++br)
+      for (int t = 0; t < 9; ++t)
+        for (int c = 0; c < sp.cin; ++c) dwt[((size_t)br * 9 + t) * sp.cin + c] = dww[((size_t)br * sp.cin + c) * 9 + t];
+    st.dw_wt = blob.add_f32(dwt);
     // fused 1x1 conv + BN (acff.py:31-34)
     const float* fw = pm.get(p + ".fused_conv.weight", (int64_t)sp.cout * 3 * sp.cin);
     const float* fb = pm.get(p + ".fused_conv.bias", sp.cout);
@@ -181,6 +188,7 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
               1e-5, bs, bt);
     st.pw = pack_conv(blob, fw, sp.cout, 3 * sp.cin, 1, nullptr, f16);
     st.pw.b_off = blob.add(fb, sizeof(float) * sp.cout);
+    st.fused = f16 && acff_fused_ok(sp.cin, st.pw.cout_pad, st.pw.kpad);
     st.d_buf = take((size_t)st.oh * st.ow * 3 * sp.cin);
     if (sp.red && sp.red_before_pool) {
       // acff2 -> conv_red2 -> pool2: BN affine folded into conv_red2
@@ -311,6 +319,59 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
   View cur{buf(h.stem_buf), h.stem_cout, 0};
   for (const AcffStage& st : h.stages) {
     const int lim = st.pool || st.red_pool ? (st.oh / 2) * 2 : st.oh;
+    if (st.fused) {
+      const float* sc = st.affine ? h.blob.at<float>(st.pw.s_off) : nullptr;
+      const float* sh = st.affine ? h.blob.at<float>(st.pw.t_off) : nullptr;
+      const bool pool_here = st.pool && !st.red_pool;
+      void* dst = st.red && st.red_pool ? buf(st.mid_buf) : buf(st.out_buf);
+      launch_acff_fused(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_wt),
+                        h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pw.w_off), st.pw.kpad, st.cout, st.pw.cout_pad,
+                        h.blob.at<float>(st.pw.b_off), sc, sh, 0.01f, dst, st.cout, pool_here ? 1 : 0, s);
+      if (st.red && st.red_pool) {
+        ConvArgs r;
+        r.in = buf(st.mid_buf);
+        r.in_cs = st.cout;
+        r.n = n;
+        r.ih = r.iw = st.oh;
+        r.cin = st.cout;
+        r.ks = 1;
+        r.oh = r.ow = st.oh;
+        r.cout = st.redw.cout;
+        r.quad = 1;
+        conv_set_rows(r);
+        r.w = h.blob.at<void>(st.redw.w_off);
+        r.kpad = st.redw.kpad;
+        r.cout_pad = st.redw.cout_pad;
+        r.w_f32 = st.redw.mfma ? 0 : 1;
+        r.e.bias = h.blob.at<float>(st.redw.b_off);
+        r.e.pool = View{buf(st.red_buf), st.redw.cout, 0};
+        launch_conv(r, h.dtype, s);
+        cur = View{buf(st.red_buf), st.redw.cout, 0};
+        continue;
+      }
+      cur = View{buf(st.out_buf), st.cout, 0};
+      if (st.red) {  // conv_red3 on the pooled output
+        ConvArgs r;
+        r.in = cur.ptr;
+        r.in_cs = st.cout;
+        r.n = n;
+        r.ih = r.iw = st.out_h;
+        r.cin = st.cout;
+        r.ks = 1;
+        r.oh = r.ow = st.out_h;
+        r.cout = st.redw.cout;
+        conv_set_rows(r);
+        r.w = h.blob.at<void>(st.redw.w_off);
+        r.kpad = st.redw.kpad;
+        r.cout_pad = st.redw.cout_pad;
+        r.w_f32 = st.redw.mfma ? 0 : 1;
+        r.e.bias = h.blob.at<float>(st.redw.b_off);
+        r.e.full = View{buf(st.red_buf), st.redw.cout, 0};
+        launch_conv(r, h.dtype, s);
+        cur = View{buf(st.red_buf), st.redw.cout, 0};
+      }
+      continue;
+    }
     launch_dw3_acff(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_w),
                     h.blob.at<float>(st.dw_b), buf(st.d_buf), h.dtype, s);
     ConvArgs g;

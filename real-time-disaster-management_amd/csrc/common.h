@@ -188,6 +188,12 @@ inline void conv_set_rows(ConvArgs& a) {
 void launch_dw3_acff(const void* in, int in_cs, int in_co, int n, int h, int w, int c, int lim_h, int lim_w,
                      const float* wts /*[3][c][9]*/, const float* bias /*[3][c]*/, void* out /*[n,h-2,w-2,3c]*/,
                      int dtype, hipStream_t s);
+// acff.hip: fused ACFF block (dw3 -> concat -> 1x1 -> LeakyReLU -> BN affine -> opt. 2x2 pool), fp16
+bool acff_fused_ok(int cin, int cout_pad, int kpad);
+void launch_acff_fused(const void* in, int in_cs, int in_co, int n, int h, int w, int cin, int lim_h, int lim_w,
+                       const float* dw_wt /*[3][9][cin]*/, const float* dw_b /*[3][cin]*/, const void* pw, int kpad,
+                       int cout, int cout_pad, const float* bias, const float* scale, const float* shift, float slope,
+                       void* out, int out_cs, int pool, hipStream_t s);
 void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, int stride, int pad, int zero_pad_rb,
                     View ov, int oh, int ow, int dtype, hipStream_t s);
 void launch_upsample(View iv, int n, int h, int w, int c, int f, View ov, int dtype, hipStream_t s);
