@@ -711,6 +711,216 @@ __global__ __launch_bounds__(256) void conv_valu(ConvArgs a) {
 }
 
 // --------------------------------------------------------------------------
+// Direct 3x3 / stride 1 / pad 1 convolution on MFMA with an LDS-resident input
+// tile (the early, small-Cin Darknet layers, where im2col re-reads dominate).
+//
+// A block owns an 8 x 16 output tile x BN output channels.  Per Cin chunk of CC
+// channels (a power of two <= 64) it stages the 10 x 18 input halo tile into
+// LDS once (pixel stride CC+8 halfs: consecutive pixels land 4 banks apart, so
+// the 16 lanes of a fragment read conflict-free), then runs the chunk's 9*CC/32
+// k-steps: K = (tap, channel) in the packed-weight order of pack_conv
+// (k = tap*Cin + c), each lane's 8 k-values = 8 channels of one tap.
+// Channel-major product D[cout][pixel] = W x X: the weight fragment (A) comes
+// from global (L2-resident) one k-step ahead, the pixel fragment (B) from LDS
+// at a per-lane tap offset.  Each lane ends with 4 consecutive channels of one
+// pixel per fragment -> 8-byte NHWC stores; the 2x2 maxpool combines two
+// fragments in-lane and lane pairs through DPP.
+// Waves 2 x 2: wave (wp, wc) = tile rows 4wp..4wp+3 x channels wc*BN/2.
+// --------------------------------------------------------------------------
+constexpr int kDirTH = 8, kDirTW = 16, kDirHW = kDirTW + 2;
+
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, 0));
+}
+
+template <int BN>
+__global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
+  constexpr int TC = BN / 32;  // 16-channel tiles per wave
+  extern __shared__ __attribute__((aligned(16))) _Float16 dir_lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cc = 1 << cc_log2, PS = cc + 8;
+  const int tiles_x = (a.ow + kDirTW - 1) / kDirTW, tiles_y = (a.oh + kDirTH - 1) / kDirTH;
+  const int nbn = a.cout_pad / BN;
+  int bid = blockIdx.x;
+  {
+    const int nblk = gridDim.x, xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int nb = bid % nbn;
+  int t = bid / nbn;
+  const int tx = t % tiles_x;
+  t /= tiles_x;
+  const int ty = t % tiles_y;
+  const int n = t / tiles_y;
+  const int oy0 = ty * kDirTH, ox0 = tx * kDirTW;
+  const int wp = wid >> 1, wc = wid & 1;
+  const int p = lane & 15, g = lane >> 4;
+  const int co_base = nb * BN + wc * (BN / 2);
+
+  const _Float16* __restrict__ in = (const _Float16*)a.in + a.in_co;
+  const _Float16* __restrict__ wt = (const _Float16*)a.w + (size_t)(co_base + p) * a.kpad;
+  f4 acc[TC][4];
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int cgl = cc_log2 - 3;  // log2(8-channel groups per tap)
+  for (int c0 = 0; c0 < a.cin; c0 += cc) {
+    if (c0) __syncthreads();
+    const int cv = cc >> 3;
+    for (int i = tid; i < (kDirTH + 2) * kDirHW * cv; i += 256) {
+      const int pix = i >> cgl, v = i & (cv - 1);
+      const int r = pix / kDirHW, c = pix - r * kDirHW;
+      const int y = oy0 - 1 + r, x = ox0 - 1 + c;
+      u32x4 d = {0u, 0u, 0u, 0u};
+      if ((unsigned)y < (unsigned)a.ih && (unsigned)x < (unsigned)a.iw)
+        d = *(const u32x4*)(in + ((size_t)(n * a.ih + y) * a.iw + x) * a.in_cs + c0 + v * 8);
+      *(u32x4*)(dir_lds + pix * PS + v * 8) = d;
+    }
+    __syncthreads();
+    const int nq = 9 << cgl;         // 8-channel groups in this chunk's K
+    const int nks = (nq + 3) >> 2;   // 32-deep k-steps
+    auto wload = [&](int s, h8 (&w)[TC]) {
+      const int q0 = 4 * s + g;
+      const bool kv = q0 < nq;
+      const int q = kv ? q0 : 0;  // no out-of-range address even if the load is speculated
+      const int tap = q >> cgl, cg = q & ((1 << cgl) - 1);
+      const size_t k = (size_t)tap * a.cin + c0 + cg * 8;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const h8 z = {};
+        w[i] = kv ? *(const h8*)(wt + (size_t)i * 16 * a.kpad + k) : z;
+      }
+    };
+    h8 wcur[TC], wnext[TC];
+    wload(0, wcur);
+    for (int s = 0; s < nks; ++s) {
+      if (s + 1 < nks) wload(s + 1, wnext);
+      const int q = 4 * s + g;
+      const bool kv = q < nq;
+      const int tap = kv ? q >> cgl : 0, cg = q & ((1 << cgl) - 1);
+      const int kh = tap / 3, kw = tap - (tap / 3) * 3;
+      const _Float16* bp = dir_lds + ((4 * wp + kh) * kDirHW + p + kw) * PS + cg * 8;
+      h8 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const h8 z = {};
+        const h8 v = *(const h8*)(bp + j * kDirHW * PS);
+        b[j] = kv ? v : z;
+      }
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wcur[i], b[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TC; ++i) wcur[i] = wnext[i];
+    }
+  }
+
+  // ---- epilogue: lane = pixel (oy0 + 4wp + j, ox0 + p), 4 channels per fragment ----
+  const Epilogue& e = a.e;
+  const int ox = ox0 + p;
+#pragma unroll
+  for (int i = 0; i < TC; ++i) {
+    const int c0 = co_base + i * 16 + 4 * g;
+    const bool cval = c0 < a.cout;
+    float bias[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[r] = (e.bias && cval) ? e.bias[c0 + r] : 0.f;
+    float v[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oy = oy0 + 4 * wp + j;
+      const bool pv = cval && oy < a.oh && ox < a.ow;
+      const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
+      float x[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t2 = acc[i][j][r] + bias[r];
+        if (e.act == ACT_LEAKY)
+          t2 = t2 > 0.f ? t2 : t2 * e.slope;
+        else if (e.act == ACT_SWISH)
+          t2 = t2 * sigmoidf_(t2);
+        x[r] = t2;
+      }
+      if (e.res.ptr && pv) {
+        const uint2 rv = *(const uint2*)((const _Float16*)e.res.ptr + pix * e.res.cs + e.res.co + c0);
+        const _Float16* rh = (const _Float16*)&rv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] += (float)rh[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j][r] = x[r];
+      const uint2 hv = make_uint2(pack_h2(x[0], x[1]), pack_h2(x[2], x[3]));
+      if (e.full.ptr && pv) *(uint2*)((_Float16*)e.full.ptr + pix * e.full.cs + e.full.co + c0) = hv;
+      if (e.up.ptr && pv) {
+        const int uw = a.ow * 2;
+        const size_t u0 = ((size_t)n * a.oh * 2 + 2 * oy) * uw + 2 * ox;
+        _Float16* up = (_Float16*)e.up.ptr + e.up.co + c0;
+        *(uint2*)(up + u0 * e.up.cs) = hv;
+        *(uint2*)(up + (u0 + 1) * e.up.cs) = hv;
+        *(uint2*)(up + (u0 + uw) * e.up.cs) = hv;
+        *(uint2*)(up + (u0 + uw + 1) * e.up.cs) = hv;
+      }
+    }
+    if (e.pool.ptr) {
+      const int qh = a.oh >> 1, qw = a.ow >> 1;
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        float m[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t2 = fmaxf(v[j][r], v[j + 1][r]);
+          m[r] = fmaxf(t2, dpp_xor1(t2));
+        }
+        const int py = (oy0 + 4 * wp + j) >> 1, px = ox >> 1;
+        if (cval && (p & 1) == 0 && py < qh && px < qw) {
+          const size_t pp = ((size_t)n * qh + py) * qw + px;
+          *(uint2*)((_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0) =
+              make_uint2(pack_h2(m[0], m[1]), pack_h2(m[2], m[3]));
+        }
+      }
+    }
+  }
+}
+
+static int direct_cc_log2(int cin) {
+  for (int l = 6; l >= 3; --l)
+    if (cin % (1 << l) == 0) return l;
+  return -1;
+}
+
+static size_t direct_lds_bytes(int cc_log2) {
+  return (size_t)(kDirTH + 2) * kDirHW * ((1 << cc_log2) + 8) * 2;
+}
+
+static bool direct_ok(const ConvArgs& a) {
+  if (a.in_kind != IN_NHWC || a.ks != 3 || a.stride != 1 || a.pad != 1 || a.w_f32) return false;
+  if (a.cin % 16 || a.cin > 32 || (a.in_cs | a.in_co) & 7 || a.cout % 4 || a.e.io || a.e.scale) return false;
+  if (a.cout_pad != 32 && a.cout_pad != 64 && a.cout_pad % 128) return false;
+  if (a.oh != a.ih || a.ow != a.iw || a.ow < 64) return false;
+  const View* vs[4] = {&a.e.full, &a.e.pool, &a.e.up, &a.e.res};
+  for (const View* v : vs)
+    if (v->ptr && ((v->cs | v->co) & 3)) return false;
+  if (a.e.pool.ptr && ((a.oh | a.ow) & 1)) return false;
+  return direct_cc_log2(a.cin) >= 4;
+}
+
+static void launch_direct(const ConvArgs& a, hipStream_t s) {
+  const int l = direct_cc_log2(a.cin);
+  const int bn = a.cout_pad >= 128 ? 128 : a.cout_pad;
+  const int64_t blocks = (int64_t)a.n * ((a.oh + kDirTH - 1) / kDirTH) * ((a.ow + kDirTW - 1) / kDirTW) * (a.cout_pad / bn);
+  const size_t lds = direct_lds_bytes(l);
+  if (bn == 128)
+    hipLaunchKernelGGL(conv3_direct<128>, dim3((unsigned)blocks), dim3(256), lds, s, a, l);
+  else if (bn == 64)
+    hipLaunchKernelGGL(conv3_direct<64>, dim3((unsigned)blocks), dim3(256), lds, s, a, l);
+  else
+    hipLaunchKernelGGL(conv3_direct<32>, dim3((unsigned)blocks), dim3(256), lds, s, a, l);
+}
+
+// --------------------------------------------------------------------------
 template <int BM, int BN, int BK, int WM, int WN>
 static void launch_mfma(const ConvArgs& a, hipStream_t s) {
   RTDM_REQUIRE(a.cout_pad % BN == 0, RTDM_E_INVALID, "conv: cout_pad not a multiple of BN");
@@ -742,6 +952,10 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     const int ntn = a.cout_pad / 16;
     return names[a.quad ? 1 : 0][ntn == 1 ? 0 : ntn == 2 ? 1 : 2];
   }
+  if (dtype == RTDM_F16 && direct_ok(a)) {
+    const int bn = a.cout_pad >= 128 ? 128 : a.cout_pad;
+    return bn == 128 ? "conv3_direct<128>" : bn == 64 ? "conv3_direct<64>" : "conv3_direct<32>";
+  }
   if (dtype == RTDM_F16 && !a.w_f32) {
     if (a.cout_pad >= 128) return "conv_mfma_f16<128,128,64,2,2>";
     if (a.cout_pad == 64) return "conv_mfma_f16<128,64,64,2,2>";
@@ -768,6 +982,8 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
       else if (ntn == 2) hipLaunchKernelGGL((conv_stem3<false, 2>), dim3(blocks), dim3(256), lds, s, a);
       else hipLaunchKernelGGL((conv_stem3<false, 4>), dim3(blocks), dim3(256), lds, s, a);
     }
+  } else if (dtype == RTDM_F16 && direct_ok(a)) {
+    launch_direct(a, s);
   } else if (dtype == RTDM_F16 && !a.w_f32) {
     RTDM_REQUIRE(mfma_ok(a), RTDM_E_INVALID, "conv: fp16 MFMA weights but input view not 16-byte aligned NHWC");
     if (a.cout_pad >= 128)

@@ -494,6 +494,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       use_mfma = cs % 8 == 0 && co % 8 == 0;
     }
     const int filters = st.cout, size = st.ks;
+    const bool stem = f16 && st.in_t < 0 && st.cin == 3 && size == 3 && (st.stride == 1 || st.stride == 2) && st.pad <= 1;
     if (weights) {
       std::vector<double> sc(filters, 1.0);
       std::vector<float> b(filters);
@@ -507,9 +508,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       }
       st.pc = pack_conv(blob, st.w_W, filters, st.cin, size, st.bn ? sc.data() : nullptr, use_mfma);
       st.pc.b_off = blob.add_f32(b);
-      if (f16 && st.in_t < 0 && st.cin == 3 && size == 3 && (st.stride == 1 || st.stride == 2) && st.pad <= 1) {
-        st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr);
-      }
+      if (stem) st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr);
     } else {
       st.pc.cout = filters;
       st.pc.cin = st.cin;
@@ -517,6 +516,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       st.pc.mfma = use_mfma;
       st.pc.kpad = (int)round_up((int64_t)size * size * st.cin, 64);
       st.pc.cout_pad = cout_pad_for(filters);
+      if (stem) st.pc.stem_off = 0;  // planning only: marks the stem kernel for step_info
     }
     st.w_beta = st.w_gamma = st.w_mean = st.w_var = st.w_bias = st.w_W = nullptr;
   }
@@ -628,6 +628,14 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
   h.last_n = n;
 }
 
+// Geometry of tensor t's view (pointer is a non-null placeholder) for kernel selection.
+static View view_geom(const rtdm_detector_s& h, int t) {
+  if (t < 0 || !h.tensors[t].materialised) return View{};
+  const Tensor& x = h.tensors[t];
+  if (x.home >= 0) return View{(void*)64, h.tensors[x.home].c, x.home_co};
+  return View{(void*)64, x.c, 0};
+}
+
 // Kernel symbol, FLOPs and compulsory HBM bytes per image of one step.
 static void step_info(const rtdm_detector_s& h, const Step& st, std::string& name, double& flop, double& bytes) {
   const double es = (double)esize_of(h.dtype);
@@ -646,6 +654,17 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     a.ow = st.ow;
     a.quad = st.quad ? 1 : 0;
     a.w_stem = st.pc.stem_off != SIZE_MAX ? (const void*)1 : nullptr;
+    a.cout = st.cout;
+    if (st.in_t >= 0) {
+      const View iv = view_geom(h, st.in_t);
+      a.in_cs = iv.cs;
+      a.in_co = iv.co;
+    }
+    a.e.full = view_geom(h, st.full_t);
+    a.e.pool = view_geom(h, st.pool_t);
+    a.e.up = view_geom(h, st.up_t);
+    a.e.res = view_geom(h, st.res_t);
+    if (st.yolo >= 0) a.e.io = (float*)64;
     name = conv_kernel_name(a, h.dtype);
     flop = 2.0 * st.oh * st.ow * (double)st.cout * st.cin * st.ks * st.ks;
     double out = 0;
@@ -787,7 +806,7 @@ rtdm_status rtdm_detector_enable_timing(rtdm_detector h, int max_calls) {
     h->timing_calls = 0;
     const size_t ne = (size_t)h->timing_cap * (h->steps.size() + 1);
     h->events.resize(ne);
-    for (size_t i = 0; i < ne; ++i) RTDM_HIP(hipEventCreate(&h->events[i]));
+    for (size_t i = 0; i < ne; ++i) RTDM_HIP(hipEventCreateWithFlags(&h->events[i], hipEventDisableSystemFence));
   });
 }
 
