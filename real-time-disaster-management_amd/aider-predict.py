@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Drop-in for disaster_detection/aider-predict.py on the MI355X HIP runtime.
+
+Same flags (--model --image --weights --no-cuda --trt --quant, aider-predict.py:124-138)
+and the same printed result: class name + confidence = softmax(model output)[cls]·100
+(the reference's double softmax, :77-80).  The image transform
+(Resize(int(1.14·S)) → CenterCrop(S) → ToTensor → Normalize, dataloaders/aider.py:412-431)
+runs on the GPU, Pillow-exact.  ``--trt`` has no TensorRT behind it: it adds a second
+prediction on the fp16 path (``--quant fp16``) or the fp32 path, which is what the
+reference's TRT engines were for.  Plotting (cv2/matplotlib) is replaced by ``--save``.
+"""
+import argparse
+import logging
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+
+from rtdm.classifier import load_model  # noqa: E402
+from rtdm.cli import predict_frames, read_image_rgb, select_device  # noqa: E402
+
+logger = logging.getLogger(__name__)
+
+
+def predict(model, image_path, device):
+    """aider-predict.py:47-86 counterpart -> (class name, confidence %)."""
+    img = read_image_rgb(image_path)
+    frames = torch.from_numpy(img[None]).to(device)
+    _, names, conf = predict_frames(model, frames)
+    return names[0], conf[0]
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser(description='Predict disaster types from aerial images')
+    parser.add_argument('--model', type=str, default='ernet', choices=['ernet', 'squeeze-ernet', 'squeeze-redconv'],
+                        help='model architecture')
+    parser.add_argument('--image', type=str, required=True, help='path to input image')
+    parser.add_argument('--weights', type=str, default=None, help='path to model weights')
+    parser.add_argument('--no-cuda', action='store_true', help='disable CUDA (not supported: GPU-only runtime)')
+    parser.add_argument('--trt', action='store_true', help='also run the reduced-precision path (TensorRT stand-in)')
+    parser.add_argument('--quant', type=str, default='fp16', choices=['fp16', 'fp32'],
+                        help='precision of the --trt path')
+    parser.add_argument('--save', type=str, default=None, help='write the annotated image here (replaces plt.show)')
+    args = parser.parse_args(argv)
+
+    device = select_device(args.no_cuda)
+    logger.info(f"Using device: {device}")
+    if args.weights is None:
+        args.weights = f'weights/{args.model}.pt'
+        if not os.path.exists(args.weights):
+            raise FileNotFoundError(f"No weights found at {args.weights}")
+
+    model = load_model(args.model, args.weights, device)
+    prediction, confidence = predict(model, args.image, device)
+    logger.info(f"Prediction: {prediction} ({confidence:.1f}%)")
+    result = {"prediction": prediction, "confidence": confidence}
+    if args.trt:
+        trt_model = load_model(args.model, args.weights, device, half=args.quant == 'fp16')
+        trt_prediction, trt_confidence = predict(trt_model, args.image, device)
+        logger.info(f"TensorRT Prediction: {trt_prediction} ({trt_confidence:.1f}%)")
+        result.update({"trt_prediction": trt_prediction, "trt_confidence": trt_confidence})
+    if args.save:
+        from PIL import Image, ImageDraw
+        im = Image.open(args.image).convert("RGB")
+        d = ImageDraw.Draw(im)
+        d.text((10, 10), f"{prediction} ({confidence:.1f}%)", fill=(255, 255, 255))
+        if args.trt:
+            d.text((10, 30), f"TRT: {result['trt_prediction']} ({result['trt_confidence']:.1f}%)", fill=(255, 255, 255))
+        im.save(args.save)
+    return result
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Drop-in for victim_localization/yolov3/detect.py on the HIP runtime.
+
+Same flags (:159-174) and outputs: per image "%gx%g <counts per class> Done. (time)",
+``--save-txt`` rows "x1 y1 x2 y2 cls conf" (:118-121), annotated images in --output.
+Darknet(cfg, img_size) + load_darknet_weights / torch.load(...)['model'] (:21-28) →
+model(img)[0] (:87) → non_max_suppression(conf, iou, classes, agnostic) (:91) →
+scale_coords back to the source image (:108).  Frames are letterboxed on the host like
+LoadImages → letterbox (utils/datasets.py:599-631, auto=True: longer side → img_size,
+the shorter padded to a multiple of 32 with (128,128,128)); cv2.INTER_AREA is replaced
+by Pillow's BOX filter (shrinking) / BILINEAR (growing).  Each distinct letterboxed
+shape gets its own planned detector handle (the reference rebuilds grids per shape,
+models.py:228-230).
+"""
+import argparse
+import os
+import shutil
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rtdm.cli import list_images, read_image_rgb, select_device  # noqa: E402
+from rtdm.darknet import Darknet, load_darknet_weights  # noqa: E402
+from rtdm.nms import non_max_suppression  # noqa: E402
+
+
+def letterbox(img: np.ndarray, new_shape: int, color=(128, 128, 128), auto: bool = True):
+    """datasets.py:599-631: r = new/max(h, w); pad the resized image to new_shape (auto=False)
+    or only to the next multiple of 32 (auto=True, the LoadImages default).
+    Returns (img, ratio, (dw, dh))."""
+    from PIL import Image
+    h0, w0 = img.shape[:2]
+    r = new_shape / max(h0, w0)
+    new_unpad = (int(round(w0 * r)), int(round(h0 * r)))
+    dw, dh = new_shape - new_unpad[0], new_shape - new_unpad[1]
+    if auto:
+        dw, dh = dw % 32, dh % 32
+    dw, dh = dw / 2, dh / 2
+    if (w0, h0) != new_unpad:
+        img = np.asarray(Image.fromarray(img).resize(new_unpad, Image.BOX if r < 1 else Image.BILINEAR), np.uint8)
+    top, bottom = int(round(dh - 0.1)), int(round(dh + 0.1))
+    left, right = int(round(dw - 0.1)), int(round(dw + 0.1))
+    out = np.empty((new_unpad[1] + top + bottom, new_unpad[0] + left + right, 3), np.uint8)
+    out[...] = np.asarray(color, np.uint8)
+    out[top:top + new_unpad[1], left:left + new_unpad[0]] = img
+    return out, r, (dw, dh)
+
+
+def scale_coords(img1_shape, coords, img0_shape):
+    """utils.py:123-136 (+ clip_coords :139-142): boxes from the letterboxed frame back to the source."""
+    gain = max(img1_shape) / max(img0_shape)
+    pad = (img1_shape[1] - img0_shape[1] * gain) / 2, (img1_shape[0] - img0_shape[0] * gain) / 2
+    coords[:, [0, 2]] -= pad[0]
+    coords[:, [1, 3]] -= pad[1]
+    coords[:, :4] /= gain
+    coords[:, 0].clamp_(0, img0_shape[1])
+    coords[:, 1].clamp_(0, img0_shape[0])
+    coords[:, 2].clamp_(0, img0_shape[1])
+    coords[:, 3].clamp_(0, img0_shape[0])
+    return coords
+
+
+def load_names(path):
+    if path and os.path.exists(path):
+        with open(path) as f:
+            return [x.strip() for x in f if x.strip()]
+    return None
+
+
+def detect(opt):
+    device = select_device(opt.device == 'cpu')
+    out = opt.output
+    if os.path.exists(out):
+        shutil.rmtree(out)
+    os.makedirs(out)
+    model = Darknet(opt.cfg, opt.img_size)
+    if opt.weights.endswith('.pt'):
+        model.load_state_dict(torch.load(opt.weights, map_location='cpu', weights_only=True)['model'])
+    else:
+        load_darknet_weights(model, opt.weights)
+    if opt.half:
+        model.half()
+    models = {model.img_size: model}
+
+    def model_for(shape):
+        if shape not in models:
+            m = Darknet(model.cfg_text, shape)
+            m.load_weight_stream(model._stream)
+            if opt.half:
+                m.half()
+            models[shape] = m
+        return models[shape]
+
+    names = load_names(opt.names) or [str(i) for i in range(model.no - 5)]
+    t0 = time.time()
+    results = {}
+    for path in list_images(opt.source):
+        im0 = read_image_rgb(path)
+        img, _, _ = letterbox(im0, opt.img_size)
+        x = torch.from_numpy(img[None]).to(device)  # uint8 NHWC; the /255 is fused on device
+        torch.cuda.synchronize()
+        t1 = time.time()
+        pred, _ = model_for(tuple(img.shape[:2]))(x)
+        det = non_max_suppression(pred, opt.conf_thres, opt.iou_thres, classes=opt.classes,
+                                  agnostic=opt.agnostic_nms)[0]
+        torch.cuda.synchronize()
+        t2 = time.time()
+        s = '%gx%g ' % img.shape[:2]
+        save_path = os.path.join(out, os.path.basename(path))
+        rows = []
+        if det is not None and len(det):
+            det = det.cpu()
+            det[:, :4] = scale_coords(img.shape[:2], det[:, :4], im0.shape).round()
+            for c in det[:, -1].unique():
+                n = int((det[:, -1] == c).sum())
+                s += '%g %ss, ' % (n, names[int(c)])
+            for *xyxy, conf, cls in det.tolist():
+                rows.append((*xyxy, cls, conf))
+                if opt.save_txt:
+                    with open(save_path + '.txt', 'a') as f:
+                        f.write(('%g ' * 6 + '\n') % (*xyxy, cls, conf))
+            if not opt.no_save_img:
+                from PIL import Image, ImageDraw
+                im = Image.fromarray(im0)
+                d = ImageDraw.Draw(im)
+                for x1, y1, x2, y2, cls, conf in rows:
+                    d.rectangle([x1, y1, x2, y2], outline=(255, 0, 0), width=2)
+                    d.text((x1, max(0, y1 - 12)), '%s %.2f' % (names[int(cls)], conf), fill=(255, 0, 0))
+                im.save(save_path)
+        results[path] = rows
+        print('%sDone. (%.3fs)' % (s, t2 - t1))
+    print('Done. (%.3fs)' % (time.time() - t0))
+    return results
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser()
+    parser.add_argument('--cfg', type=str, default='cfg/yolov3-spp.cfg', help='*.cfg path')
+    parser.add_argument('--names', type=str, default='data/aider.names', help='*.names path')
+    parser.add_argument('--weights', type=str, default='weights/best.pt', help='weights path')
+    parser.add_argument('--source', type=str, default='data/custom/test/images', help='image file or folder')
+    parser.add_argument('--output', type=str, default='output', help='output folder')
+    parser.add_argument('--img-size', type=int, default=416, help='inference size (pixels)')
+    parser.add_argument('--conf-thres', type=float, default=0.3, help='object confidence threshold')
+    parser.add_argument('--iou-thres', type=float, default=0.4, help='IOU threshold for NMS')
+    parser.add_argument('--half', action='store_true', help='half precision FP16 inference')
+    parser.add_argument('--device', default='', help='device id (cpu is refused: GPU-only runtime)')
+    parser.add_argument('--save-txt', action='store_true', help='save results to *.txt')
+    parser.add_argument('--no-save-img', action='store_true', help='do not write annotated images')
+    parser.add_argument('--classes', nargs='+', type=int, help='filter by class')
+    parser.add_argument('--agnostic-nms', action='store_true', help='class-agnostic NMS')
+    opt = parser.parse_args(argv)
+    print(opt)
+    with torch.no_grad():
+        return detect(opt)
+
+
+if __name__ == '__main__':
+    main()
