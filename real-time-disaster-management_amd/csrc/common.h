@@ -160,7 +160,9 @@ struct ConvArgs {
   const void* w = nullptr;  // packed weights [cout_pad][kpad], k = (kh*ks+kw)*cin + c
   int kpad = 0, cout_pad = 0;
   int w_f32 = 0;            // weights packed fp32 for the VALU body (else fp16 MFMA layout)
-  const void* w_stem = nullptr;  // MFMA stem (Cin=3, 3x3): fp16 [cout_pad][32], k = (kh*3+kw)*3+c
+  const void* w_stem = nullptr;  // MFMA stem (Cin=3, 3x3): fp16 [cout_pad][64] (pack_stem)
+  const void* zero = nullptr;    // >= 16 zero bytes in device memory (glds padding source)
+  FastDiv fd_cin;                // set by conv_set_rows
   Epilogue e;
 };
 
@@ -178,6 +180,7 @@ inline void conv_set_rows(ConvArgs& a) {
     a.M = a.n * a.oh * a.ow;
   }
   a.fd_ow = make_fastdiv(a.ow);
+  a.fd_cin = make_fastdiv(a.cin);
   a.fd_oh = make_fastdiv(a.oh);
   a.fd_qw = make_fastdiv(a.qw);
   a.fd_qh = make_fastdiv(a.qh);

@@ -711,6 +711,151 @@ __global__ __launch_bounds__(256) void conv_valu(ConvArgs a) {
 }
 
 // --------------------------------------------------------------------------
+// fp16 implicit GEMM with direct global->LDS staging (global_load_lds_dwordx4).
+// 128 x 128 block tile, BK = 64, 4 waves (2 x 2, 64 x 64 each), two LDS
+// buffers: the loads of K-block kb+1 are issued before the MFMAs of kb and
+// retired by the one __syncthreads() (vmcnt(0) + barrier) per K-block.
+// glds writes each wave-instruction's 64 x 16 bytes lane-linearly (8 rows of
+// 128 B), so the bank-conflict swizzle lives in the per-lane SOURCE address:
+// LDS slot s of row r holds k-vector s ^ ((r >> 1) & 7), and a fragment read
+// of k-vector v in row r reads slot v ^ ((r >> 1) & 7) — the 16 rows a
+// ds_read_b128 lane group touches then cover all 64 banks.  Out-of-image taps,
+// K padding and rows past M read a 16-byte zero block (a.zero) instead.
+// --------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+__global__ __launch_bounds__(256, 2) void conv_glds_f16(ConvArgs a) {
+  constexpr int BM = 128, BN = 128, BK = 64;
+  constexpr int BUF = (BM + BN) * BK;  // halfs per stage buffer
+  constexpr int CSTR = BN + 4;
+  constexpr int SMEM = (2 * BUF * 2 > BM * CSTR * 4) ? 2 * BUF * 2 : BM * CSTR * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SMEM];
+  _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nblk = gridDim.x;
+  const int ntn = a.cout_pad / BN;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int m_base = (bid / ntn) * BM;
+  const int n_base = (bid - (bid / ntn) * ntn) * BN;
+
+  // ---- per-lane staging rows: instr j covers rows 32*wid + 8*j + lane/8, slot lane%8 ----
+  const int slot = lane & 7;
+  const _Float16* __restrict__ in = (const _Float16*)a.in + a.in_co;
+  const _Float16* __restrict__ zero = (const _Float16*)a.zero;
+  int a_pix[4], a_iy[4], a_ix[4], kofs[4];
+  const _Float16* b_src[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = 32 * wid + 8 * j + (lane >> 3);
+    kofs[j] = 8 * (slot ^ ((r >> 1) & 7));
+    const int m = m_base + r;
+    int n = 0, oy = 0, ox = 0;
+    if (m < a.M) row_to_pix(a, m, n, oy, ox);
+    a_pix[j] = n * a.ih * a.iw;
+    a_iy[j] = m < a.M ? oy * a.stride - a.pad : -(1 << 28);
+    a_ix[j] = ox * a.stride - a.pad;
+    b_src[j] = (const _Float16*)a.w + (size_t)(n_base + r) * a.kpad + kofs[j];
+  }
+  const int K = a.ks * a.ks * a.cin;
+  const int nk = a.kpad / BK;
+  const FastDiv fd_cin = a.fd_cin;
+
+  auto stage = [&](int buf, int kb) {
+    _Float16* As = smem + buf * BUF;
+    _Float16* Bs = As + BM * BK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kg = kb * BK + kofs[j];
+      const int tap = fdiv(kg, fd_cin);
+      const int c = kg - tap * a.cin;
+      const int kh = a.ks == 3 ? (tap * 11) >> 5 : 0;
+      const int kw = tap - kh * a.ks;
+      const int iy = a_iy[j] + kh, ix = a_ix[j] + kw;
+      const bool v = kg < K && (unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw;
+      const _Float16* src = v ? in + (size_t)(a_pix[j] + iy * a.iw + ix) * a.in_cs + c : zero;
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(As + (32 * wid + 8 * j) * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(b_src[j] + kb * BK), (lds_ptr_t)(Bs + (32 * wid + 8 * j) * BK), 16,
+                                       0, 0);
+  };
+
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, g = lane >> 4;
+  const int rsw = (fr >> 1) & 7;  // swizzle key of this lane's fragment rows
+  const int s0 = 8 * ((0 + g) ^ rsw), s1 = 8 * ((4 + g) ^ rsw);
+
+  stage(0, 0);
+  __syncthreads();
+  for (int kb = 0; kb < nk; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nk) stage(cur ^ 1, kb + 1);
+    const _Float16* As = smem + cur * BUF + (wm * 64 + fr) * BK;
+    const _Float16* Bs = smem + cur * BUF + BM * BK + (wn * 64 + fr) * BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int so = kk ? s1 : s0;
+      h8 af[4], bf[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) af[t] = *(const h8*)(As + t * 16 * BK + so);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bf[t] = *(const h8*)(Bs + t * 16 * BK + so);
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[tm], bf[tn], acc[tm][tn], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: accumulators -> LDS C tile -> 4 rows x 8 channels per thread ----
+  float* Cs = reinterpret_cast<float*>(smem_raw);
+  const int rq = g * 4;
+#pragma unroll
+  for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+      const int row = wm * 64 + tm * 16 + rq;
+      const int col = wn * 64 + tn * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Cs[(row + j) * CSTR + col] = acc[tm][tn][j];
+    }
+  __syncthreads();
+  constexpr int CG = BN / 8;
+  constexpr int UNITS = (BM / 4) * CG;
+  for (int u = tid; u < UNITS; u += 256) {
+    const int q = u / CG, gg = u - (u / CG) * CG;
+    const int m0 = m_base + q * 4, c0 = n_base + gg * 8;
+    if (m0 >= a.M || c0 >= a.cout) continue;
+    float v[4][8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[r][j] = Cs[(q * 4 + r) * CSTR + gg * 8 + j];
+    epi_vec8(a, m0, c0, v);
+  }
+}
+
+static bool glds_ok(const ConvArgs& a) {
+  return a.zero && a.in_kind == IN_NHWC && !a.w_f32 && a.cin % 8 == 0 && (a.in_cs | a.in_co) % 8 == 0 &&
+         a.cout_pad % 128 == 0 && a.kpad % 64 == 0 && (a.ks == 1 || a.ks == 3);
+}
+
+// --------------------------------------------------------------------------
 // Direct 3x3 / stride 1 / pad 1 convolution on MFMA with an LDS-resident input
 // tile (the early, small-Cin Darknet layers, where im2col re-reads dominate).
 //
@@ -956,6 +1101,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     const int bn = a.cout_pad >= 128 ? 128 : a.cout_pad;
     return bn == 128 ? "conv3_direct<128>" : bn == 64 ? "conv3_direct<64>" : "conv3_direct<32>";
   }
+  if (dtype == RTDM_F16 && glds_ok(a)) return "conv_glds_f16";
   if (dtype == RTDM_F16 && !a.w_f32) {
     if (a.cout_pad >= 128) return "conv_mfma_f16<128,128,64,2,2>";
     if (a.cout_pad == 64) return "conv_mfma_f16<128,64,64,2,2>";
@@ -984,6 +1130,10 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     }
   } else if (dtype == RTDM_F16 && direct_ok(a)) {
     launch_direct(a, s);
+  } else if (dtype == RTDM_F16 && glds_ok(a)) {
+    const int64_t nblk = (int64_t)((a.M + 127) / 128) * (a.cout_pad / 128);
+    RTDM_REQUIRE(nblk < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
+    hipLaunchKernelGGL(conv_glds_f16, dim3((unsigned)nblk), dim3(256), 0, s, a);
   } else if (dtype == RTDM_F16 && !a.w_f32) {
     RTDM_REQUIRE(mfma_ok(a), RTDM_E_INVALID, "conv: fp16 MFMA weights but input view not 16-byte aligned NHWC");
     if (a.cout_pad >= 128)

@@ -139,6 +139,7 @@ struct rtdm_detector_s {
   size_t per_image = 0;  // arena elements per image
   rtdm::DevBlob blob;
   rtdm::DevBuf arena;
+  rtdm::DevBuf zero;  // 256 zero bytes: padding source of the glds conv kernel
   int last_n = 0;
   // optional per-step timing: events[call][step+1] recorded on the launch stream
   bool timing = false;
@@ -525,6 +526,8 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     RTDM_HIP(hipGetDevice(&h.dev));
     h.blob.upload(blob);
     h.arena.alloc(h.per_image * esize_of(h.dtype) * h.max_batch);
+    h.zero.alloc(256);
+    RTDM_HIP(hipMemset(h.zero.p, 0, 256));
   }
 }
 
@@ -612,6 +615,7 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       // the mfma/valu choice was fixed when the weights were packed
       a.w_f32 = st.pc.mfma ? 0 : 1;
       a.w_stem = h.blob.at<void>(st.pc.stem_off);
+      a.zero = h.zero.p;
       launch_conv(a, h.dtype, s);
     } else if (st.kind == ST_MAXPOOL) {
       launch_maxpool(nullptr, tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, st.k, st.s, st.p, st.zero_rb,
@@ -654,6 +658,8 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     a.ow = st.ow;
     a.quad = st.quad ? 1 : 0;
     a.w_stem = st.pc.stem_off != SIZE_MAX ? (const void*)1 : nullptr;
+    a.zero = (const void*)64;
+    a.kpad = st.pc.kpad;
     a.cout = st.cout;
     if (st.in_t >= 0) {
       const View iv = view_geom(h, st.in_t);

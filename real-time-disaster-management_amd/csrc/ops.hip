@@ -640,6 +640,7 @@ void launch_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, c
 // row-major order of the reference's multi-label expansion (utils.py:524).
 static constexpr int kNmsThreads = 1024;
 static constexpr int kNmsLdsCap = 4096;
+static constexpr int kNmsMaskCap = 512;  // LDS IoU-bitmask path: n * ceil(n/64) * 8 B <= 32 KiB
 
 struct NmsWs {  // per-image slice of the workspace
   uint64_t* keys;
@@ -683,6 +684,7 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
   __shared__ float4 s_box[kNmsLdsCap];
   __shared__ float s_area[kNmsLdsCap];
   __shared__ uint32_t s_supp[kNmsLdsCap / 32];
+  __shared__ uint64_t s_mask[kNmsMaskCap * (kNmsMaskCap / 64)];
   __shared__ int s_n;
   const int img = blockIdx.x;
   const int tid = threadIdx.x;
@@ -778,29 +780,77 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
   for (int i = tid; i < (n + 31) / 32; i += kNmsThreads) S[i] = 0u;
   __syncthreads();
 
-  // 4. greedy suppression
+  // 4. greedy suppression.
+  // n <= kNmsMaskCap: the torchvision-CUDA formulation — every (i, 64-column
+  // word) IoU bitmask in parallel into LDS, then one wave scans candidates in
+  // score order, OR-ing the masks of kept boxes (no workgroup barrier per
+  // candidate).  Same IoU arithmetic and the same keep set as the greedy loop.
   int nkeep = 0;
-  for (int i = 0; i < n; ++i) {
-    if ((S[i >> 5] >> (i & 31)) & 1u) continue;
-    if (tid == 0) g.keep[nkeep] = i;
-    ++nkeep;
-    const float4 bi = B[i];
-    const float ai = A[i];
-    for (int j = i + 1 + tid; j < n; j += kNmsThreads) {
-      if ((S[j >> 5] >> (j & 31)) & 1u) continue;
-      const float4 bj = B[j];
-      const float xx1 = fmaxf(bi.x, bj.x);
-      const float yy1 = fmaxf(bi.y, bj.y);
-      const float xx2 = fminf(bi.z, bj.z);
-      const float yy2 = fminf(bi.w, bj.w);
-      const float w = fmaxf(0.f, xx2 - xx1);
-      const float h = fmaxf(0.f, yy2 - yy1);
-      const float inter = w * h;
-      const float ovr = inter / ((ai + A[j]) - inter);
-      if ((double)ovr > iou_thr) atomicOr(&S[j >> 5], 1u << (j & 31));
+  if (n <= kNmsMaskCap) {
+    const int W = (n + 63) >> 6;
+    for (int p = tid; p < n * W; p += kNmsThreads) {
+      const int i = p / W, w = p - (p / W) * W;
+      const float4 bi = B[i];
+      const float ai = A[i];
+      uint64_t bits = 0;
+      const int j0 = w * 64;
+      const int j1 = j0 + 64 < n ? j0 + 64 : n;
+      for (int j = j0 > i + 1 ? j0 : i + 1; j < j1; ++j) {
+        const float4 bj = B[j];
+        const float xx1 = fmaxf(bi.x, bj.x);
+        const float yy1 = fmaxf(bi.y, bj.y);
+        const float xx2 = fminf(bi.z, bj.z);
+        const float yy2 = fminf(bi.w, bj.w);
+        const float w2 = fmaxf(0.f, xx2 - xx1);
+        const float h2 = fmaxf(0.f, yy2 - yy1);
+        const float inter = w2 * h2;
+        const float ovr = inter / ((ai + A[j]) - inter);
+        if ((double)ovr > iou_thr) bits |= 1ull << (j - j0);
+      }
+      s_mask[p] = bits;
     }
     __syncthreads();
+    if (tid < 64) {
+      uint64_t removed = 0;  // lane l < W holds word l
+      int nk = 0;
+      for (int i = 0; i < n; ++i) {
+        const int wi = i >> 6;
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)removed, wi);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(removed >> 32), wi);
+        const uint64_t word = ((uint64_t)hi << 32) | lo;
+        if ((word >> (i & 63)) & 1ull) continue;
+        if (tid == 0) g.keep[nk] = i;
+        ++nk;
+        if (tid < W) removed |= s_mask[i * W + tid];
+      }
+      if (tid == 0) s_n = nk;
+    }
+    __syncthreads();
+    nkeep = s_n;
+  } else {
+    for (int i = 0; i < n; ++i) {
+      if ((S[i >> 5] >> (i & 31)) & 1u) continue;
+      if (tid == 0) g.keep[nkeep] = i;
+      ++nkeep;
+      const float4 bi = B[i];
+      const float ai = A[i];
+      for (int j = i + 1 + tid; j < n; j += kNmsThreads) {
+        if ((S[j >> 5] >> (j & 31)) & 1u) continue;
+        const float4 bj = B[j];
+        const float xx1 = fmaxf(bi.x, bj.x);
+        const float yy1 = fmaxf(bi.y, bj.y);
+        const float xx2 = fminf(bi.z, bj.z);
+        const float yy2 = fminf(bi.w, bj.w);
+        const float w = fmaxf(0.f, xx2 - xx1);
+        const float h = fmaxf(0.f, yy2 - yy1);
+        const float inter = w * h;
+        const float ovr = inter / ((ai + A[j]) - inter);
+        if ((double)ovr > iou_thr) atomicOr(&S[j >> 5], 1u << (j & 31));
+      }
+      __syncthreads();
+    }
   }
+  __syncthreads();  // g.keep written by wave 0 / thread 0 -> read by all below
 
   // 5. rows [x1,y1,x2,y2,conf,cls] in kept (descending score) order
   const int nout = nkeep < max_det ? nkeep : max_det;

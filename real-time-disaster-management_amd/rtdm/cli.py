@@ -38,7 +38,7 @@ def read_image_rgb(path: str) -> np.ndarray:
     if not os.path.exists(path):
         raise ValueError(f"Could not load image at {path}")
     with Image.open(path) as im:
-        return np.ascontiguousarray(np.asarray(im.convert("RGB"), dtype=np.uint8))
+        return np.array(im.convert("RGB"), dtype=np.uint8)
 
 
 def list_images(source: str):
