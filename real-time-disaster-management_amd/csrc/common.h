@@ -163,6 +163,7 @@ struct ConvArgs {
   const void* w_stem = nullptr;  // MFMA stem (Cin=3, 3x3): fp16 [cout_pad][64] (pack_stem)
   const void* zero = nullptr;    // >= 16 zero bytes in device memory (glds padding source)
   FastDiv fd_cin;                // set by conv_set_rows
+  int glds_uni = 0;              // conv_glds_f16: uniform-tap staging (set by launch_conv)
   Epilogue e;
 };
 
@@ -211,6 +212,7 @@ struct ResizePlan {  // Pillow 8bpc antialiased bilinear, restricted to a center
   int crop_top = 0, crop_left = 0;
   int ksize_h = 0, ksize_v = 0;
   int row_first = 0, rows = 0;  // input rows needed by the vertical pass
+  int band_rows = 0;            // max input rows of one 16-output-row band (fused kernel)
   DevBuf bounds_h, coef_h, bounds_v, coef_v;  // int32 device arrays
 };
 void build_resize_plan(ResizePlan& p, int in_h, int in_w, int out_size, bool upload);

@@ -566,7 +566,11 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
       for (int t = 0; t < NTN; ++t) {
         f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf0, wa[t][0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1, wa[t][1], acc, 0, 0, 0);
-        const float m = fmaxf(fmaxf(epi(acc[0], t, 0), epi(acc[1], t, 0)), fmaxf(epi(acc[2], t, 0), epi(acc[3], t, 0)));
+        // bias, LeakyReLU/linear and the positive 1/255 scale are monotone non-decreasing
+        // (and so is their fp32 rounding): pool first, then one epilogue per quad
+        const float m = e.scale || act == ACT_SWISH
+                            ? fmaxf(fmaxf(epi(acc[0], t, 0), epi(acc[1], t, 0)), fmaxf(epi(acc[2], t, 0), epi(acc[3], t, 0)))
+                            : epi(fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])), t, 0);
         const int c = 16 * t + p;
         if (oq < qw && c < a.cout) pool_row[(size_t)oq * e.pool.cs + c] = (_Float16)m;
       }
@@ -766,21 +770,50 @@ __global__ __launch_bounds__(256, 2) void conv_glds_f16(ConvArgs a) {
   const int K = a.ks * a.ks * a.cin;
   const int nk = a.kpad / BK;
   const FastDiv fd_cin = a.fd_cin;
+  // Uniform path (Cin % 64 == 0, tensor < 2^30 elements): a K-block never straddles a
+  // tap, so (kh, kw, c0) are wave-uniform scalars advanced once per K-block and each
+  // row needs only two bounds checks and a 32-bit offset from the uniform base.
+  const bool uni = a.glds_uni;
+  int rowoff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rowoff[j] = (a_pix[j] + a_iy[j] * a.iw + a_ix[j]) * a.in_cs + kofs[j];
+  const int cpt = a.cin / BK;  // K-blocks per tap (uniform path)
+  int st_kh = 0, st_kw = 0, st_c = 0;  // uniform-path cursor: the next K-block to stage
 
   auto stage = [&](int buf, int kb) {
     _Float16* As = smem + buf * BUF;
     _Float16* Bs = As + BM * BK;
+    if (uni) {
+      const int tapoff = (st_kh * a.iw + st_kw) * a.in_cs + st_c * BK;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kg = kb * BK + kofs[j];
-      const int tap = fdiv(kg, fd_cin);
-      const int c = kg - tap * a.cin;
-      const int kh = a.ks == 3 ? (tap * 11) >> 5 : 0;
-      const int kw = tap - kh * a.ks;
-      const int iy = a_iy[j] + kh, ix = a_ix[j] + kw;
-      const bool v = kg < K && (unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw;
-      const _Float16* src = v ? in + (size_t)(a_pix[j] + iy * a.iw + ix) * a.in_cs + c : zero;
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(As + (32 * wid + 8 * j) * BK), 16, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        const int iy = a_iy[j] + st_kh, ix = a_ix[j] + st_kw;
+        _Float16* dst = As + (32 * wid + 8 * j) * BK;
+        if ((unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw)
+          __builtin_amdgcn_global_load_lds((gbl_ptr_t)(in + (uint32_t)(rowoff[j] + tapoff)), (lds_ptr_t)dst, 16, 0, 0);
+        else
+          *(u32x4*)(dst + lane * 8) = u32x4{0u, 0u, 0u, 0u};
+      }
+      if (++st_c == cpt) {
+        st_c = 0;
+        if (++st_kw == a.ks) {
+          st_kw = 0;
+          ++st_kh;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kg = kb * BK + kofs[j];
+        const int tap = fdiv(kg, fd_cin);
+        const int c = kg - tap * a.cin;
+        const int kh = a.ks == 3 ? (tap * 11) >> 5 : 0;
+        const int kw = tap - kh * a.ks;
+        const int iy = a_iy[j] + kh, ix = a_ix[j] + kw;
+        const bool v = kg < K && (unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw;
+        const _Float16* src = v ? in + (size_t)(a_pix[j] + iy * a.iw + ix) * a.in_cs + c : zero;
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(As + (32 * wid + 8 * j) * BK), 16, 0, 0);
+      }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -855,11 +888,18 @@ static bool glds_ok(const ConvArgs& a) {
          a.cout_pad % 128 == 0 && a.kpad % 64 == 0 && (a.ks == 1 || a.ks == 3);
 }
 
+// Uniform-tap staging applies when every K-block lies inside one tap and the
+// input view's element offsets fit in 30 bits.
+static int glds_uniform(const ConvArgs& a) {
+  const int64_t elems = (int64_t)a.n * a.ih * a.iw * a.in_cs;
+  return a.cin % 64 == 0 && a.kpad == a.ks * a.ks * a.cin && elems < (1ll << 30);
+}
+
 // --------------------------------------------------------------------------
 // Direct 3x3 / stride 1 / pad 1 convolution on MFMA with an LDS-resident input
 // tile (the early, small-Cin Darknet layers, where im2col re-reads dominate).
 //
-// A block owns an 8 x 16 output tile x BN output channels.  Per Cin chunk of CC
+// A block owns a TH x 16 output tile x BN output channels.  Per Cin chunk of CC
 // channels (a power of two <= 64) it stages the 10 x 18 input halo tile into
 // LDS once (pixel stride CC+8 halfs: consecutive pixels land 4 banks apart, so
 // the 16 lanes of a fragment read conflict-free), then runs the chunk's 9*CC/32
@@ -870,17 +910,21 @@ static bool glds_ok(const ConvArgs& a) {
 // at a per-lane tap offset.  Each lane ends with 4 consecutive channels of one
 // pixel per fragment -> 8-byte NHWC stores; the 2x2 maxpool combines two
 // fragments in-lane and lane pairs through DPP.
-// Waves 2 x 2: wave (wp, wc) = tile rows 4wp..4wp+3 x channels wc*BN/2.
+// Waves WPX (pixels) x 4/WPX (channels): wave (wp, wc) = tile rows 4wp..4wp+3
+// x TC 16-channel tiles; TH = 4*WPX, BN = 16*TC*(4/WPX).  Small Cout uses
+// WPX = 4 (every wave owns all BN channels of its 64 pixels).
 // --------------------------------------------------------------------------
-constexpr int kDirTH = 8, kDirTW = 16, kDirHW = kDirTW + 2;
+constexpr int kDirTW = 16, kDirHW = kDirTW + 2;
 
 __device__ __forceinline__ float dpp_xor1(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, 0));
 }
 
-template <int BN>
+template <int TC, int WPX>
 __global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
-  constexpr int TC = BN / 32;  // 16-channel tiles per wave
+  constexpr int WCH = 4 / WPX;           // waves along channels
+  constexpr int BN = 16 * TC * WCH;      // channels per block
+  constexpr int kDirTH = 4 * WPX;        // tile rows
   extern __shared__ __attribute__((aligned(16))) _Float16 dir_lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int cc = 1 << cc_log2, PS = cc + 8;
@@ -898,9 +942,9 @@ __global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
   const int ty = t % tiles_y;
   const int n = t / tiles_y;
   const int oy0 = ty * kDirTH, ox0 = tx * kDirTW;
-  const int wp = wid >> 1, wc = wid & 1;
+  const int wp = wid / WCH, wc = wid - (wid / WCH) * WCH;
   const int p = lane & 15, g = lane >> 4;
-  const int co_base = nb * BN + wc * (BN / 2);
+  const int co_base = nb * BN + wc * (16 * TC);
 
   const _Float16* __restrict__ in = (const _Float16*)a.in + a.in_co;
   const _Float16* __restrict__ wt = (const _Float16*)a.w + (size_t)(co_base + p) * a.kpad;
@@ -966,6 +1010,38 @@ __global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
   // ---- epilogue: lane = pixel (oy0 + 4wp + j, ox0 + p), 4 channels per fragment ----
   const Epilogue& e = a.e;
   const int ox = ox0 + p;
+  if (e.pool.ptr && !e.full.ptr && !e.up.ptr && !e.res.ptr && e.act != ACT_SWISH) {
+    // pooled output only: bias + LeakyReLU are monotone, so max-pool the raw
+    // accumulators (2 fragments in-lane, lane pairs by DPP) and run the epilogue
+    // once per pooled pixel — bit-identical to pooling the activated values.
+    const int qh = a.oh >> 1, qw = a.ow >> 1;
+#pragma unroll
+    for (int i = 0; i < TC; ++i) {
+      const int c0 = co_base + i * 16 + 4 * g;
+      const bool cval = c0 < a.cout;
+      float bias[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[r] = (e.bias && cval) ? e.bias[c0 + r] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        float m[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t2 = fmaxf(acc[i][j][r], acc[i][j + 1][r]);
+          float x = fmaxf(t2, dpp_xor1(t2)) + bias[r];
+          if (e.act == ACT_LEAKY) x = x > 0.f ? x : x * e.slope;
+          m[r] = x;
+        }
+        const int py = (oy0 + 4 * wp + j) >> 1, px = ox >> 1;
+        if (cval && (p & 1) == 0 && py < qh && px < qw) {
+          const size_t pp = ((size_t)n * qh + py) * qw + px;
+          *(uint2*)((_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0) =
+              make_uint2(pack_h2(m[0], m[1]), pack_h2(m[2], m[3]));
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TC; ++i) {
     const int c0 = co_base + i * 16 + 4 * g;
@@ -1036,8 +1112,18 @@ static int direct_cc_log2(int cin) {
   return -1;
 }
 
-static size_t direct_lds_bytes(int cc_log2) {
-  return (size_t)(kDirTH + 2) * kDirHW * ((1 << cc_log2) + 8) * 2;
+// Direct-conv configuration for cout_pad: (TC, WPX) and channels per block.
+struct DirCfg {
+  int tc, wpx, bn, th;
+};
+static DirCfg direct_cfg(int cout_pad) {
+  if (cout_pad == 32) return {2, 4, 32, 16};
+  if (cout_pad == 64) return {4, 4, 64, 16};
+  return {4, 2, 128, 8};
+}
+
+static size_t direct_lds_bytes(int cc_log2, int th) {
+  return (size_t)(th + 2) * kDirHW * ((1 << cc_log2) + 8) * 2;
 }
 
 static bool direct_ok(const ConvArgs& a) {
@@ -1054,15 +1140,15 @@ static bool direct_ok(const ConvArgs& a) {
 
 static void launch_direct(const ConvArgs& a, hipStream_t s) {
   const int l = direct_cc_log2(a.cin);
-  const int bn = a.cout_pad >= 128 ? 128 : a.cout_pad;
-  const int64_t blocks = (int64_t)a.n * ((a.oh + kDirTH - 1) / kDirTH) * ((a.ow + kDirTW - 1) / kDirTW) * (a.cout_pad / bn);
-  const size_t lds = direct_lds_bytes(l);
-  if (bn == 128)
-    hipLaunchKernelGGL(conv3_direct<128>, dim3((unsigned)blocks), dim3(256), lds, s, a, l);
-  else if (bn == 64)
-    hipLaunchKernelGGL(conv3_direct<64>, dim3((unsigned)blocks), dim3(256), lds, s, a, l);
+  const DirCfg c = direct_cfg(a.cout_pad);
+  const int64_t blocks = (int64_t)a.n * ((a.oh + c.th - 1) / c.th) * ((a.ow + kDirTW - 1) / kDirTW) * (a.cout_pad / c.bn);
+  const size_t lds = direct_lds_bytes(l, c.th);
+  if (c.bn == 128)
+    hipLaunchKernelGGL((conv3_direct<4, 2>), dim3((unsigned)blocks), dim3(256), lds, s, a, l);
+  else if (c.bn == 64)
+    hipLaunchKernelGGL((conv3_direct<4, 4>), dim3((unsigned)blocks), dim3(256), lds, s, a, l);
   else
-    hipLaunchKernelGGL(conv3_direct<32>, dim3((unsigned)blocks), dim3(256), lds, s, a, l);
+    hipLaunchKernelGGL((conv3_direct<2, 4>), dim3((unsigned)blocks), dim3(256), lds, s, a, l);
 }
 
 // --------------------------------------------------------------------------
@@ -1098,8 +1184,8 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     return names[a.quad ? 1 : 0][ntn == 1 ? 0 : ntn == 2 ? 1 : 2];
   }
   if (dtype == RTDM_F16 && direct_ok(a)) {
-    const int bn = a.cout_pad >= 128 ? 128 : a.cout_pad;
-    return bn == 128 ? "conv3_direct<128>" : bn == 64 ? "conv3_direct<64>" : "conv3_direct<32>";
+    const int bn = direct_cfg(a.cout_pad).bn;
+    return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
   }
   if (dtype == RTDM_F16 && glds_ok(a)) return "conv_glds_f16";
   if (dtype == RTDM_F16 && !a.w_f32) {
@@ -1133,7 +1219,9 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
   } else if (dtype == RTDM_F16 && glds_ok(a)) {
     const int64_t nblk = (int64_t)((a.M + 127) / 128) * (a.cout_pad / 128);
     RTDM_REQUIRE(nblk < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
-    hipLaunchKernelGGL(conv_glds_f16, dim3((unsigned)nblk), dim3(256), 0, s, a);
+    ConvArgs b = a;
+    b.glds_uni = glds_uniform(a);
+    hipLaunchKernelGGL(conv_glds_f16, dim3((unsigned)nblk), dim3(256), 0, s, b);
   } else if (dtype == RTDM_F16 && !a.w_f32) {
     RTDM_REQUIRE(mfma_ok(a), RTDM_E_INVALID, "conv: fp16 MFMA weights but input view not 16-byte aligned NHWC");
     if (a.cout_pad >= 128)

@@ -498,6 +498,11 @@ void build_resize_plan(ResizePlan& p, int in_h, int in_w, int out_size, bool upl
   p.row_first = rmin;
   p.rows = rmax - rmin;
   for (int i = 0; i < out_size; ++i) cv[2 * i] -= rmin;
+  p.band_rows = 0;
+  for (int y0 = 0; y0 < out_size; y0 += 16) {  // kResizeBand
+    const int y1 = std::min(out_size, y0 + 16) - 1;
+    p.band_rows = std::max(p.band_rows, cv[2 * y1] + cv[2 * y1 + 1] - cv[2 * y0]);
+  }
   if (!upload) return;
   auto up = [](DevBuf& d, const std::vector<int>& v) {
     d.alloc(v.size() * sizeof(int));
@@ -575,9 +580,98 @@ __global__ __launch_bounds__(256) void resize_v_kernel(const uint8_t* __restrict
   }
 }
 
+// Fused form: one block per (image, band of kResizeBand output rows).  The
+// band's input rows get the horizontal pass straight from the frame into an
+// LDS row buffer (uint8 after clip8, like Pillow's intermediate image), then
+// the vertical pass + ToTensor + Normalize reads only LDS.  Same integer
+// arithmetic as the two-kernel path (bit-exact with Pillow).
+constexpr int kResizeBand = 16;
+
+template <typename T>
+__global__ __launch_bounds__(256) void resize_fused_kernel(const uint8_t* __restrict__ frames, int in_h, int in_w,
+                                                           int row_first, int out, int kh_size, int kv_size,
+                                                           const int* __restrict__ bh, const int* __restrict__ ch,
+                                                           const int* __restrict__ bv, const int* __restrict__ cv,
+                                                           T* __restrict__ dst, int nchw) {
+  extern __shared__ __attribute__((aligned(16))) int rs_lds[];
+  int* kcoef = rs_lds;                       // [out][kh_size]
+  int* kb = kcoef + out * kh_size;           // [out][2]
+  uint8_t* tmp = (uint8_t*)(kb + 2 * out);   // [band rows][out][3]
+  const int bands = (out + kResizeBand - 1) / kResizeBand;
+  const int b = blockIdx.x / bands;
+  const int yy0 = (blockIdx.x - b * bands) * kResizeBand;
+  const int yy1 = yy0 + kResizeBand < out ? yy0 + kResizeBand : out;
+  const int r0 = bv[2 * yy0];
+  const int r1 = bv[2 * (yy1 - 1)] + bv[2 * (yy1 - 1) + 1];
+  for (int i = threadIdx.x; i < out * kh_size; i += 256) kcoef[i] = ch[i];
+  for (int i = threadIdx.x; i < 2 * out; i += 256) kb[i] = bh[i];
+  __syncthreads();
+  // horizontal pass for input rows row_first + [r0, r1)
+  const int nrow = r1 - r0;
+  for (int i = threadIdx.x; i < nrow * out; i += 256) {
+    const int r = i / out, xx = i - r * out;
+    const int xmin = kb[2 * xx], xmax = kb[2 * xx + 1];
+    const int* k = kcoef + xx * kh_size;
+    const uint8_t* src = frames + (((size_t)b * in_h + row_first + r0 + r) * in_w + xmin) * 3;
+    int s0 = 1 << (kPrecisionBits - 1), s1 = s0, s2 = s0;
+    for (int x = 0; x < xmax; ++x) {
+      const int kx = k[x];
+      s0 += src[x * 3 + 0] * kx;
+      s1 += src[x * 3 + 1] * kx;
+      s2 += src[x * 3 + 2] * kx;
+    }
+    uint8_t* d = tmp + (size_t)i * 3;
+    d[0] = (uint8_t)clip8(s0);
+    d[1] = (uint8_t)clip8(s1);
+    d[2] = (uint8_t)clip8(s2);
+  }
+  __syncthreads();
+  const float mean[3] = {0.485f, 0.456f, 0.406f};
+  const float stdv[3] = {0.229f, 0.224f, 0.225f};
+  for (int i = threadIdx.x; i < (yy1 - yy0) * out; i += 256) {
+    const int yr = i / out, xx = i - yr * out;
+    const int yy = yy0 + yr;
+    const int ymin = bv[2 * yy] - r0, ymax = bv[2 * yy + 1];
+    const int* k = cv + (size_t)yy * kv_size;
+    int acc[3] = {1 << (kPrecisionBits - 1), 1 << (kPrecisionBits - 1), 1 << (kPrecisionBits - 1)};
+    for (int y = 0; y < ymax; ++y) {
+      const uint8_t* t = tmp + ((size_t)(ymin + y) * out + xx) * 3;
+      const int ky = k[y];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) acc[c] += t[c] * ky;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = ((float)clip8(acc[c]) / 255.f - mean[c]) / stdv[c];
+      if (nchw)
+        dst[(((size_t)b * 3 + c) * out + yy) * out + xx] = (T)v;
+      else
+        dst[(((size_t)b * out + yy) * out + xx) * 3 + c] = (T)v;
+    }
+  }
+}
+
+static size_t resize_fused_lds(const ResizePlan& p) {
+  return (size_t)p.out * p.ksize_h * 4 + (size_t)p.out * 2 * 4 + (size_t)p.band_rows * p.out * 3;
+}
+
 void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_t* tmp, void* out, int out_layout,
                        int dtype, hipStream_t s) {
   if (n <= 0) return;
+  const size_t lds = resize_fused_lds(p);
+  if (lds <= 64 * 1024) {
+    const int blocks = n * ((p.out + kResizeBand - 1) / kResizeBand);
+    if (out_layout == 1 || dtype == RTDM_F32)
+      hipLaunchKernelGGL(resize_fused_kernel<float>, dim3(blocks), dim3(256), lds, s, frames, p.in_h, p.in_w,
+                         p.row_first, p.out, p.ksize_h, p.ksize_v, p.bounds_h.as<int>(), p.coef_h.as<int>(),
+                         p.bounds_v.as<int>(), p.coef_v.as<int>(), (float*)out, out_layout == 1 ? 1 : 0);
+    else
+      hipLaunchKernelGGL(resize_fused_kernel<_Float16>, dim3(blocks), dim3(256), lds, s, frames, p.in_h, p.in_w,
+                         p.row_first, p.out, p.ksize_h, p.ksize_v, p.bounds_h.as<int>(), p.coef_h.as<int>(),
+                         p.bounds_v.as<int>(), p.coef_v.as<int>(), (_Float16*)out, 0);
+    RTDM_HIP(hipGetLastError());
+    return;
+  }
   const int64_t th = (int64_t)n * p.rows * p.out;
   hipLaunchKernelGGL(resize_h_kernel, dim3(grid_for(th, 256)), dim3(256), 0, s, frames, n, p.in_h, p.in_w,
                      p.row_first, p.rows, p.out, p.ksize_h, p.bounds_h.as<int>(), p.coef_h.as<int>(), tmp);
