@@ -217,20 +217,27 @@ __device__ __forceinline__ void epi_vec8(const ConvArgs& a, int m0, int c0, cons
       }
     }
     if (e.io) {
+      // (anchor, field) of channel c0 by one division, then stepped per channel;
+      // fp16 path: hardware exp / reciprocal (well inside the fp16 tolerance)
+      int ai = c0 / e.no, k = c0 - ai * e.no;
+      const size_t pix_io = (size_t)n * e.io_rows + e.io_off + (size_t)oy * a.ow + ox;
+      const size_t plane = (size_t)a.oh * a.ow;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (j >= nc) continue;
-        const int c = c0 + j;
-        const int ai = c / e.no, k = c - ai * e.no;
-        float o;
-        if (k < 2)
-          o = (sigmoidf_(x[j]) + (float)(k == 0 ? ox : oy)) * e.ystride;
-        else if (k < 4)
-          o = (expf(x[j]) * e.anchor_vec[2 * ai + (k - 2)]) * e.ystride;
-        else
-          o = sigmoidf_(x[j]);
-        const size_t row = (size_t)e.io_off + ((size_t)ai * a.oh + oy) * a.ow + ox;
-        e.io[((size_t)n * e.io_rows + row) * e.no + k] = o;
+        if (j < nc) {
+          float o;
+          if (k < 2)
+            o = (__frcp_rn(1.f + __expf(-x[j])) + (float)(k == 0 ? ox : oy)) * e.ystride;
+          else if (k < 4)
+            o = (__expf(x[j]) * e.anchor_vec[2 * ai + (k - 2)]) * e.ystride;
+          else
+            o = __frcp_rn(1.f + __expf(-x[j]));
+          e.io[(pix_io + (size_t)ai * plane) * e.no + k] = o;
+        }
+        if (++k == e.no) {
+          k = 0;
+          ++ai;
+        }
       }
     }
   }
@@ -729,11 +736,12 @@ __global__ __launch_bounds__(256) void conv_valu(ConvArgs a) {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
-__global__ __launch_bounds__(256, 2) void conv_glds_f16(ConvArgs a) {
+template <int NS>
+__global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_glds_f16(ConvArgs a) {
   constexpr int BM = 128, BN = 128, BK = 64;
   constexpr int BUF = (BM + BN) * BK;  // halfs per stage buffer
   constexpr int CSTR = BN + 4;
-  constexpr int SMEM = (2 * BUF * 2 > BM * CSTR * 4) ? 2 * BUF * 2 : BM * CSTR * 4;
+  constexpr int SMEM = (NS * BUF * 2 > BM * CSTR * 4) ? NS * BUF * 2 : BM * CSTR * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SMEM];
   _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
 
@@ -788,11 +796,9 @@ __global__ __launch_bounds__(256, 2) void conv_glds_f16(ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int iy = a_iy[j] + st_kh, ix = a_ix[j] + st_kw;
-        _Float16* dst = As + (32 * wid + 8 * j) * BK;
-        if ((unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw)
-          __builtin_amdgcn_global_load_lds((gbl_ptr_t)(in + (uint32_t)(rowoff[j] + tapoff)), (lds_ptr_t)dst, 16, 0, 0);
-        else
-          *(u32x4*)(dst + lane * 8) = u32x4{0u, 0u, 0u, 0u};
+        const bool v = (unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw;
+        const _Float16* src = v ? in + (uint32_t)(rowoff[j] + tapoff) : zero;
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(As + (32 * wid + 8 * j) * BK), 16, 0, 0);
       }
       if (++st_c == cpt) {
         st_c = 0;
@@ -831,11 +837,25 @@ __global__ __launch_bounds__(256, 2) void conv_glds_f16(ConvArgs a) {
   const int rsw = (fr >> 1) & 7;  // swizzle key of this lane's fragment rows
   const int s0 = 8 * ((0 + g) ^ rsw), s1 = 8 * ((4 + g) ^ rsw);
 
+  // NS = 2: loads of kb+1 in flight during kb, retired by __syncthreads (vmcnt(0)).
+  // NS = 3: loads of kb+1 and kb+2 in flight; every stage is exactly 8 glds per
+  // wave, so "s_waitcnt vmcnt(8)" + raw s_barrier retires stage kb+1 while kb+2
+  // stays in flight across the barrier (no ordinary global loads in the loop).
   stage(0, 0);
-  __syncthreads();
+  if (NS == 3 && nk > 1) {
+    stage(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else {
+    __syncthreads();
+  }
   for (int kb = 0; kb < nk; ++kb) {
-    const int cur = kb & 1;
-    if (kb + 1 < nk) stage(cur ^ 1, kb + 1);
+    const int cur = NS == 2 ? (kb & 1) : kb % 3;
+    if (NS == 2) {
+      if (kb + 1 < nk) stage(cur ^ 1, kb + 1);
+    } else {
+      if (kb + 2 < nk) stage(cur == 0 ? 2 : cur - 1, kb + 2);
+    }
     const _Float16* As = smem + cur * BUF + (wm * 64 + fr) * BK;
     const _Float16* Bs = smem + cur * BUF + BM * BK + (wn * 64 + fr) * BK;
 #pragma unroll
@@ -852,8 +872,17 @@ __global__ __launch_bounds__(256, 2) void conv_glds_f16(ConvArgs a) {
         for (int tn = 0; tn < 4; ++tn)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[tm], bf[tn], acc[tm][tn], 0, 0, 0);
     }
-    __syncthreads();
+    if (NS == 2) {
+      __syncthreads();
+    } else {
+      if (kb + 2 < nk)
+        asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
   }
+  if (NS == 3) __syncthreads();
 
   // ---- epilogue: accumulators -> LDS C tile -> 4 rows x 8 channels per thread ----
   float* Cs = reinterpret_cast<float*>(smem_raw);
@@ -886,6 +915,17 @@ __global__ __launch_bounds__(256, 2) void conv_glds_f16(ConvArgs a) {
 static bool glds_ok(const ConvArgs& a) {
   return a.zero && a.in_kind == IN_NHWC && !a.w_f32 && a.cin % 8 == 0 && (a.in_cs | a.in_co) % 8 == 0 &&
          a.cout_pad % 128 == 0 && a.kpad % 64 == 0 && (a.ks == 1 || a.ks == 3);
+}
+
+// Pipeline depth of conv_glds_f16 (RTDM_GLDS_STAGES=2|3; default 2).  Measured on
+// the yolov4-tiny@608 b64 layers: the 3-stage form (96 KiB LDS -> 1 block/CU)
+// runs 1.3-1.6x slower than 2 stages at 2 blocks/CU.
+static int glds_stages() {
+  static int v = [] {
+    const char* e = getenv("RTDM_GLDS_STAGES");
+    return (e && atoi(e) == 3) ? 3 : 2;
+  }();
+  return v;
 }
 
 // Uniform-tap staging applies when every K-block lies inside one tap and the
@@ -1187,7 +1227,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     const int bn = direct_cfg(a.cout_pad).bn;
     return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
   }
-  if (dtype == RTDM_F16 && glds_ok(a)) return "conv_glds_f16";
+  if (dtype == RTDM_F16 && glds_ok(a)) return glds_stages() == 3 ? "conv_glds_f16<3>" : "conv_glds_f16<2>";
   if (dtype == RTDM_F16 && !a.w_f32) {
     if (a.cout_pad >= 128) return "conv_mfma_f16<128,128,64,2,2>";
     if (a.cout_pad == 64) return "conv_mfma_f16<128,64,64,2,2>";
@@ -1221,7 +1261,10 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     RTDM_REQUIRE(nblk < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
     ConvArgs b = a;
     b.glds_uni = glds_uniform(a);
-    hipLaunchKernelGGL(conv_glds_f16, dim3((unsigned)nblk), dim3(256), 0, s, b);
+    if (glds_stages() == 3)
+      hipLaunchKernelGGL(conv_glds_f16<3>, dim3((unsigned)nblk), dim3(256), 0, s, b);
+    else
+      hipLaunchKernelGGL(conv_glds_f16<2>, dim3((unsigned)nblk), dim3(256), 0, s, b);
   } else if (dtype == RTDM_F16 && !a.w_f32) {
     RTDM_REQUIRE(mfma_ok(a), RTDM_E_INVALID, "conv: fp16 MFMA weights but input view not 16-byte aligned NHWC");
     if (a.cout_pad >= 128)
