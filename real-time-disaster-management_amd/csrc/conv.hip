@@ -736,16 +736,21 @@ __global__ __launch_bounds__(256) void conv_valu(ConvArgs a) {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
-template <int NS>
-__global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_glds_f16(ConvArgs a) {
-  constexpr int BM = 128, BN = 128, BK = 64;
-  constexpr int BUF = (BM + BN) * BK;  // halfs per stage buffer
+template <int BM, int NS>
+__global__ __launch_bounds__(BM * 2, (BM == 128 && NS == 2) ? 2 : 1) void conv_glds_f16(ConvArgs a) {
+  constexpr int BN = 128, BK = 64;
+  constexpr int WAVES = BM / 32;         // 4 (128 x 128 tile) or 8 (256 x 128 tile)
+  constexpr int NT = 64 * WAVES;
+  constexpr int NB = BN / (8 * WAVES);   // B-tile wave-instructions per wave per stage
+  constexpr int VM = 4 + NB;             // vm ops per wave per stage (exact, for counted vmcnt)
+  constexpr int BUF = (BM + BN) * BK;    // halfs per stage buffer
   constexpr int CSTR = BN + 4;
   constexpr int SMEM = (NS * BUF * 2 > BM * CSTR * 4) ? NS * BUF * 2 : BM * CSTR * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SMEM];
   _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar LDS addresses)
   const int wm = wid >> 1, wn = wid & 1;
   const int nblk = gridDim.x;
   const int ntn = a.cout_pad / BN;
@@ -757,12 +762,14 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_glds_f16(ConvArgs a
   const int m_base = (bid / ntn) * BM;
   const int n_base = (bid - (bid / ntn) * ntn) * BN;
 
-  // ---- per-lane staging rows: instr j covers rows 32*wid + 8*j + lane/8, slot lane%8 ----
+  // ---- staging rows: A instr j covers rows 32*wid + 8*j + lane/8, B instr j rows
+  //      (8*NB)*wid + 8*j + lane/8; slot lane%8 holds k-vector slot ^ ((row >> 1) & 7) ----
   const int slot = lane & 7;
   const _Float16* __restrict__ in = (const _Float16*)a.in + a.in_co;
   const _Float16* __restrict__ zero = (const _Float16*)a.zero;
   int a_pix[4], a_iy[4], a_ix[4], kofs[4];
-  const _Float16* b_src[4];
+  int voff_a[4];
+  uint32_t vmask[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int r = 32 * wid + 8 * j + (lane >> 3);
@@ -773,58 +780,85 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_glds_f16(ConvArgs a
     a_pix[j] = n * a.ih * a.iw;
     a_iy[j] = m < a.M ? oy * a.stride - a.pad : -(1 << 28);
     a_ix[j] = ox * a.stride - a.pad;
-    b_src[j] = (const _Float16*)a.w + (size_t)(n_base + r) * a.kpad + kofs[j];
+    voff_a[j] = m < a.M ? ((a_pix[j] + a_iy[j] * a.iw + a_ix[j]) * a.in_cs + kofs[j]) * 2 : 0;
+    uint32_t msk = 0;
+    for (int t = 0; t < a.ks * a.ks; ++t) {
+      const int kh = a.ks == 3 ? (t * 11) >> 5 : 0, kw = t - kh * a.ks;
+      const int iy = a_iy[j] + kh, ix = a_ix[j] + kw;
+      if ((unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw) msk |= 1u << t;
+    }
+    vmask[j] = msk;
+  }
+  int kofs_b[NB], voff_b[NB];
+  const _Float16* b_src[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int r = 8 * NB * wid + 8 * j + (lane >> 3);
+    kofs_b[j] = 8 * (slot ^ ((r >> 1) & 7));
+    voff_b[j] = (r * a.kpad + kofs_b[j]) * 2;
+    b_src[j] = (const _Float16*)a.w + (size_t)(n_base + r) * a.kpad + kofs_b[j];
   }
   const int K = a.ks * a.ks * a.cin;
   const int nk = a.kpad / BK;
   const FastDiv fd_cin = a.fd_cin;
   // Uniform path (Cin % 64 == 0, tensor < 2^30 elements): a K-block never straddles a
-  // tap, so (kh, kw, c0) are wave-uniform scalars advanced once per K-block and each
-  // row needs only two bounds checks and a 32-bit offset from the uniform base.
+  // tap, so the tap and channel block are wave-uniform scalars advanced once per
+  // K-block.  Loads are buffer_load ... lds through one descriptor per operand: per
+  // row a 32-bit byte offset and a 9-bit tap-validity mask fixed at the start; an
+  // invalid tap / row gets an offset past num_records, which the buffer unit returns
+  // as zeros (the convolution's zero padding).  B offsets are fixed per lane, the
+  // K-block advance rides in soffset.
   const bool uni = a.glds_uni;
-  int rowoff[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) rowoff[j] = (a_pix[j] + a_iy[j] * a.iw + a_ix[j]) * a.in_cs + kofs[j];
+  __amdgpu_buffer_rsrc_t rs_in, rs_w;
+  if (uni) {
+    const int64_t in_bytes = ((int64_t)a.n * a.ih * a.iw * a.in_cs - a.in_co) * 2;
+    rs_in = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+    rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)((const _Float16*)a.w + (size_t)n_base * a.kpad), 0,
+                                             BN * a.kpad * 2, 0x00020000);
+  }
   const int cpt = a.cin / BK;  // K-blocks per tap (uniform path)
-  int st_kh = 0, st_kw = 0, st_c = 0;  // uniform-path cursor: the next K-block to stage
+  int st_tap = 0, st_c = 0;     // uniform-path cursor: the next K-block to stage
 
   auto stage = [&](int buf, int kb) {
     _Float16* As = smem + buf * BUF;
     _Float16* Bs = As + BM * BK;
     if (uni) {
-      const int tapoff = (st_kh * a.iw + st_kw) * a.in_cs + st_c * BK;
+      const int kh = a.ks == 3 ? (st_tap * 11) >> 5 : 0, kw = st_tap - kh * a.ks;
+      const int tapoff = ((kh * a.iw + kw) * a.in_cs + st_c * BK) * 2;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int iy = a_iy[j] + st_kh, ix = a_ix[j] + st_kw;
-        const bool v = (unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw;
-        const _Float16* src = v ? in + (uint32_t)(rowoff[j] + tapoff) : zero;
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(As + (32 * wid + 8 * j) * BK), 16, 0, 0);
+        const int vo = ((vmask[j] >> st_tap) & 1u) ? voff_a[j] + tapoff : (int)0x80000000;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(As + (32 * wid + 8 * j) * BK), 16, vo, 0, 0, 0);
+      }
+      const int soff = kb * BK * 2;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        _Float16* bdst = Bs + (8 * NB * wid + 8 * j) * BK;
+        const int vob = voff_b[j];
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)bdst, 16, vob, soff, 0, 0);
       }
       if (++st_c == cpt) {
         st_c = 0;
-        if (++st_kw == a.ks) {
-          st_kw = 0;
-          ++st_kh;
-        }
+        ++st_tap;
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int kg = kb * BK + kofs[j];
-        const int tap = fdiv(kg, fd_cin);
-        const int c = kg - tap * a.cin;
-        const int kh = a.ks == 3 ? (tap * 11) >> 5 : 0;
-        const int kw = tap - kh * a.ks;
-        const int iy = a_iy[j] + kh, ix = a_ix[j] + kw;
-        const bool v = kg < K && (unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw;
-        const _Float16* src = v ? in + (size_t)(a_pix[j] + iy * a.iw + ix) * a.in_cs + c : zero;
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(As + (32 * wid + 8 * j) * BK), 16, 0, 0);
-      }
+      return;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(b_src[j] + kb * BK), (lds_ptr_t)(Bs + (32 * wid + 8 * j) * BK), 16,
-                                       0, 0);
+    for (int j = 0; j < 4; ++j) {
+      const int kg = kb * BK + kofs[j];
+      const int tap = fdiv(kg, fd_cin);
+      const int c = kg - tap * a.cin;
+      const int kh = a.ks == 3 ? (tap * 11) >> 5 : 0;
+      const int kw = tap - kh * a.ks;
+      const int iy = a_iy[j] + kh, ix = a_ix[j] + kw;
+      const bool v = kg < K && (unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw;
+      const _Float16* src = v ? in + (size_t)(a_pix[j] + iy * a.iw + ix) * a.in_cs + c : zero;
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(As + (32 * wid + 8 * j) * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(b_src[j] + kb * BK), (lds_ptr_t)(Bs + (8 * NB * wid + 8 * j) * BK),
+                                       16, 0, 0);
   };
 
   f4 acc[4][4];
@@ -838,13 +872,16 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_glds_f16(ConvArgs a
   const int s0 = 8 * ((0 + g) ^ rsw), s1 = 8 * ((4 + g) ^ rsw);
 
   // NS = 2: loads of kb+1 in flight during kb, retired by __syncthreads (vmcnt(0)).
-  // NS = 3: loads of kb+1 and kb+2 in flight; every stage is exactly 8 glds per
-  // wave, so "s_waitcnt vmcnt(8)" + raw s_barrier retires stage kb+1 while kb+2
-  // stays in flight across the barrier (no ordinary global loads in the loop).
+  // NS = 3: loads of kb+1 and kb+2 in flight; every stage is exactly VM buffer/global
+  // LDS-DMA ops per wave, so "s_waitcnt vmcnt(VM)" + raw s_barrier retires stage kb+1
+  // while kb+2 stays in flight across the barrier (no other vector-memory ops in the loop).
   stage(0, 0);
   if (NS == 3 && nk > 1) {
     stage(1, 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if (VM == 8)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   } else {
     __syncthreads();
@@ -875,10 +912,14 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_glds_f16(ConvArgs a
     if (NS == 2) {
       __syncthreads();
     } else {
-      if (kb + 2 < nk)
-        asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-      else
+      if (kb + 2 < nk) {
+        if (VM == 8)
+          asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      } else {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
       __builtin_amdgcn_s_barrier();
     }
   }
@@ -899,7 +940,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_glds_f16(ConvArgs a
   __syncthreads();
   constexpr int CG = BN / 8;
   constexpr int UNITS = (BM / 4) * CG;
-  for (int u = tid; u < UNITS; u += 256) {
+  for (int u = tid; u < UNITS; u += NT) {
     const int q = u / CG, gg = u - (u / CG) * CG;
     const int m0 = m_base + q * 4, c0 = n_base + gg * 8;
     if (m0 >= a.M || c0 >= a.cout) continue;
@@ -917,13 +958,18 @@ static bool glds_ok(const ConvArgs& a) {
          a.cout_pad % 128 == 0 && a.kpad % 64 == 0 && (a.ks == 1 || a.ks == 3);
 }
 
-// Pipeline depth of conv_glds_f16 (RTDM_GLDS_STAGES=2|3; default 2).  Measured on
-// the yolov4-tiny@608 b64 layers: the 3-stage form (96 KiB LDS -> 1 block/CU)
-// runs 1.3-1.6x slower than 2 stages at 2 blocks/CU.
-static int glds_stages() {
-  static int v = [] {
-    const char* e = getenv("RTDM_GLDS_STAGES");
-    return (e && atoi(e) == 3) ? 3 : 2;
+// conv_glds_f16 variant (RTDM_GLDS=<BM>x<stages>, e.g. 128x2, 256x3).
+struct GldsCfg {
+  int bm, ns;
+};
+static GldsCfg glds_cfg() {
+  static GldsCfg v = [] {
+    GldsCfg c{128, 2};
+    if (const char* e = getenv("RTDM_GLDS")) {
+      int bm = 0, ns = 0;
+      if (sscanf(e, "%dx%d", &bm, &ns) == 2 && (bm == 128 || bm == 256) && (ns == 2 || ns == 3)) c = {bm, ns};
+    }
+    return c;
   }();
   return v;
 }
@@ -1227,7 +1273,12 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     const int bn = direct_cfg(a.cout_pad).bn;
     return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
   }
-  if (dtype == RTDM_F16 && glds_ok(a)) return glds_stages() == 3 ? "conv_glds_f16<3>" : "conv_glds_f16<2>";
+  if (dtype == RTDM_F16 && glds_ok(a)) {
+    static const char* names[2][2] = {{"conv_glds_f16<128,2>", "conv_glds_f16<128,3>"},
+                                      {"conv_glds_f16<256,2>", "conv_glds_f16<256,3>"}};
+    const GldsCfg c = glds_cfg();
+    return names[c.bm == 256][c.ns == 3];
+  }
   if (dtype == RTDM_F16 && !a.w_f32) {
     if (a.cout_pad >= 128) return "conv_mfma_f16<128,128,64,2,2>";
     if (a.cout_pad == 64) return "conv_mfma_f16<128,64,64,2,2>";
@@ -1257,14 +1308,20 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
   } else if (dtype == RTDM_F16 && direct_ok(a)) {
     launch_direct(a, s);
   } else if (dtype == RTDM_F16 && glds_ok(a)) {
-    const int64_t nblk = (int64_t)((a.M + 127) / 128) * (a.cout_pad / 128);
+    const GldsCfg c = glds_cfg();
+    const int64_t nblk = (int64_t)((a.M + c.bm - 1) / c.bm) * (a.cout_pad / 128);
     RTDM_REQUIRE(nblk < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
     ConvArgs b = a;
     b.glds_uni = glds_uniform(a);
-    if (glds_stages() == 3)
-      hipLaunchKernelGGL(conv_glds_f16<3>, dim3((unsigned)nblk), dim3(256), 0, s, b);
+    const dim3 grid((unsigned)nblk), block(2 * c.bm);
+    if (c.bm == 128 && c.ns == 2)
+      hipLaunchKernelGGL((conv_glds_f16<128, 2>), grid, block, 0, s, b);
+    else if (c.bm == 128)
+      hipLaunchKernelGGL((conv_glds_f16<128, 3>), grid, block, 0, s, b);
+    else if (c.ns == 2)
+      hipLaunchKernelGGL((conv_glds_f16<256, 2>), grid, block, 0, s, b);
     else
-      hipLaunchKernelGGL(conv_glds_f16<2>, dim3((unsigned)nblk), dim3(256), 0, s, b);
+      hipLaunchKernelGGL((conv_glds_f16<256, 3>), grid, block, 0, s, b);
   } else if (dtype == RTDM_F16 && !a.w_f32) {
     RTDM_REQUIRE(mfma_ok(a), RTDM_E_INVALID, "conv: fp16 MFMA weights but input view not 16-byte aligned NHWC");
     if (a.cout_pad >= 128)
