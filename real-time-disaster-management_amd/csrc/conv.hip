@@ -1192,6 +1192,144 @@ __global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
   }
 }
 
+// --------------------------------------------------------------------------
+// conv3_pool_small: 3x3 / s1 / p1 convolution + fused 2x2 maxpool for the
+// small-Cin early layers (Cin 16 / 32, Cout 32 / 64; the 608x608 Darknet's
+// layers 2 and 4, where the work per output is tiny and address arithmetic,
+// not MFMA, sets the speed).  Everything that does not depend on the tile is
+// hoisted out of the K loop:
+//   * each lane's weight fragments for the whole K (NKS k-steps x WCH channel
+//     tiles) are loaded once into registers;
+//   * each lane's LDS offset for every k-step (tap, 8-channel group) is
+//     computed once; per k-step the B fragment of tile row j is one
+//     ds_read_b128 at that offset + a compile-time row stride;
+//   * the 2x2 maxpool runs on the raw accumulators (bias + LeakyReLU are
+//     monotone): in-lane over tile rows j, j+1 and across the lane pair
+//     (p, p^1) by DPP, then one bias/activation/store per pooled pixel.
+// Block: TH x 16 output pixels x COUT channels; waves = (TH / WROWS) row
+// groups x (COUT / 16 / WCH) channel groups = 4.  LDS: the 18 x 18 input halo,
+// pixel stride CIN + 8 halfs (16 consecutive pixels hit distinct banks).
+// --------------------------------------------------------------------------
+template <int CIN, int COUT, int TH, int WROWS, int WCH>
+__global__ __launch_bounds__(256) void conv3_pool_small(ConvArgs a) {
+  constexpr int TW = 16, HW = TW + 2, PS = CIN + 8;
+  constexpr int CG = CIN / 8;                // 8-channel groups per tap
+  constexpr int NQ = 9 * CG;                 // 8-channel groups in K
+  constexpr int NKS = (NQ + 3) / 4;          // 32-deep k-steps
+  constexpr int RG = TH / WROWS;             // row groups of waves
+  static_assert(RG * (COUT / 16 / WCH) == 4, "wave layout must cover 4 waves");
+  __shared__ __attribute__((aligned(16))) _Float16 xs[(TH + 2) * HW * PS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int p = lane & 15, g = lane >> 4;
+  const int tiles_x = (a.ow + TW - 1) / TW, tiles_y = (a.oh + TH - 1) / TH;
+  int bid = blockIdx.x;
+  {
+    const int nblk = gridDim.x, xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int tx = bid % tiles_x;
+  const int t1 = bid / tiles_x;
+  const int ty = t1 % tiles_y;
+  const int n = t1 / tiles_y;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int wr = wid % RG, wc = wid / RG;
+  const int co0 = wc * WCH * 16;
+
+  // weights for the whole K, issued first (L2-resident, overlaps the halo staging)
+  h8 wf[NKS][WCH];
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    const int q = 4 * s + g;  // k = 8q (zero-padded weights beyond 9*CIN)
+#pragma unroll
+    for (int t = 0; t < WCH; ++t) wf[s][t] = *(const h8*)((const _Float16*)a.w + (size_t)(co0 + 16 * t + p) * a.kpad + 8 * q);
+  }
+  // input halo rows oy0-1 .. oy0+TH, cols ox0-1 .. ox0+TW
+  const _Float16* __restrict__ in = (const _Float16*)a.in + a.in_co;
+  for (int i = tid; i < (TH + 2) * HW * CG; i += 256) {
+    const int pix = i / CG, v = i - pix * CG;
+    const int r = pix / HW, c = pix - r * HW;
+    const int y = oy0 - 1 + r, x = ox0 - 1 + c;
+    u32x4 d = {0u, 0u, 0u, 0u};
+    if ((unsigned)y < (unsigned)a.ih && (unsigned)x < (unsigned)a.iw)
+      d = *(const u32x4*)(in + ((size_t)(n * a.ih + y) * a.iw + x) * a.in_cs + v * 8);
+    *(u32x4*)(xs + pix * PS + v * 8) = d;
+  }
+  // per-lane LDS offset of every k-step (tap clamped for the zero-weight tail)
+  int kofs[NKS];
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    int q = 4 * s + g;
+    q = q < NQ ? q : NQ - 1;
+    const int tap = q / CG, cg = q - tap * CG;
+    const int kh = tap / 3, kw = tap - kh * 3;
+    kofs[s] = (kh * HW + kw) * PS + cg * 8;
+  }
+  const _Float16* xb = xs + (wr * WROWS * HW + p) * PS;
+  f4 acc[WROWS][WCH];
+#pragma unroll
+  for (int j = 0; j < WROWS; ++j)
+#pragma unroll
+    for (int t = 0; t < WCH; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    const _Float16* bp = xb + kofs[s];
+#pragma unroll
+    for (int j = 0; j < WROWS; ++j) {
+      const h8 b = *(const h8*)(bp + j * HW * PS);
+#pragma unroll
+      for (int t = 0; t < WCH; ++t) acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][t], b, acc[j][t], 0, 0, 0);
+    }
+  }
+  // pooled epilogue: lane = pixel column ox0 + p, rows j; channels co0 + 16t + 4g + r
+  const Epilogue& e = a.e;
+  const int qh = a.oh >> 1, qw = a.ow >> 1;
+  const int px = (ox0 + p) >> 1;
+#pragma unroll
+  for (int t = 0; t < WCH; ++t) {
+    const int c0 = co0 + 16 * t + 4 * g;
+    float bias[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[r] = e.bias ? e.bias[c0 + r] : 0.f;
+#pragma unroll
+    for (int j = 0; j < WROWS; j += 2) {
+      float m[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t2 = fmaxf(acc[j][t][r], acc[j + 1][t][r]);
+        float x = fmaxf(t2, dpp_xor1(t2)) + bias[r];
+        if (e.act == ACT_LEAKY) x = x > 0.f ? x : x * e.slope;
+        m[r] = x;
+      }
+      const int py = (oy0 + wr * WROWS + j) >> 1;
+      if ((p & 1) == 0 && py < qh && px < qw) {
+        const size_t pp = ((size_t)n * qh + py) * qw + px;
+        *(uint2*)((_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0) =
+            make_uint2(pack_h2(m[0], m[1]), pack_h2(m[2], m[3]));
+      }
+    }
+  }
+}
+
+static bool pool_small_ok(const ConvArgs& a) {
+  if (a.in_kind != IN_NHWC || a.ks != 3 || a.stride != 1 || a.pad != 1 || a.w_f32) return false;
+  if (!((a.cin == 16 && a.cout == 32) || (a.cin == 32 && a.cout == 64))) return false;
+  if (a.cout_pad != a.cout || (a.in_cs | a.in_co) & 7 || a.oh != a.ih || a.ow != a.iw || (a.oh | a.ow) & 1) return false;
+  if (!a.e.pool.ptr || a.e.full.ptr || a.e.up.ptr || a.e.res.ptr || a.e.io || a.e.scale || a.e.act == ACT_SWISH)
+    return false;
+  if ((a.e.pool.cs | a.e.pool.co) & 3) return false;
+  return a.kpad >= 32 * ((9 * a.cin / 8 + 3) / 4);  // weights read up to k = 32 * NKS
+}
+
+static void launch_pool_small(const ConvArgs& a, hipStream_t s) {
+  const int th = a.cin == 16 ? 16 : 8;
+  const int64_t blocks = (int64_t)a.n * ((a.oh + th - 1) / th) * ((a.ow + 15) / 16);
+  if (a.cin == 16)
+    hipLaunchKernelGGL((conv3_pool_small<16, 32, 16, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+}
+
 static int direct_cc_log2(int cin) {
   for (int l = 6; l >= 3; --l)
     if (cin % (1 << l) == 0) return l;
@@ -1269,6 +1407,8 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     const int ntn = a.cout_pad / 16;
     return names[a.quad ? 1 : 0][ntn == 1 ? 0 : ntn == 2 ? 1 : 2];
   }
+  if (dtype == RTDM_F16 && pool_small_ok(a))
+    return a.cin == 16 ? "conv3_pool_small<16,32,16,4,2>" : "conv3_pool_small<32,64,8,4,2>";
   if (dtype == RTDM_F16 && direct_ok(a)) {
     const int bn = direct_cfg(a.cout_pad).bn;
     return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
@@ -1305,6 +1445,8 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
       else if (ntn == 2) hipLaunchKernelGGL((conv_stem3<false, 2>), dim3(blocks), dim3(256), lds, s, a);
       else hipLaunchKernelGGL((conv_stem3<false, 4>), dim3(blocks), dim3(256), lds, s, a);
     }
+  } else if (dtype == RTDM_F16 && pool_small_ok(a)) {
+    launch_pool_small(a, s);
   } else if (dtype == RTDM_F16 && direct_ok(a)) {
     launch_direct(a, s);
   } else if (dtype == RTDM_F16 && glds_ok(a)) {
