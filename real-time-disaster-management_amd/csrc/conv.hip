@@ -20,6 +20,8 @@
 // (disaster_detection/model/acff.py:49-53, BN applied as a post-activation affine).
 #include "common.h"
 
+#include <algorithm>
+
 namespace rtdm {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -1217,42 +1219,25 @@ __global__ __launch_bounds__(256) void conv3_pool_small(ConvArgs a) {
   constexpr int NQ = 9 * CG;                 // 8-channel groups in K
   constexpr int NKS = (NQ + 3) / 4;          // 32-deep k-steps
   constexpr int RG = TH / WROWS;             // row groups of waves
+  constexpr int HALO = (TH + 2) * HW * CG;   // 16-byte vectors per staged tile
+  constexpr int PV = (HALO + 255) / 256;     // prefetch registers per thread
+  constexpr int XS = (TH + 2) * HW * PS;     // halfs per LDS buffer
   static_assert(RG * (COUT / 16 / WCH) == 4, "wave layout must cover 4 waves");
-  __shared__ __attribute__((aligned(16))) _Float16 xs[(TH + 2) * HW * PS];
+  __shared__ __attribute__((aligned(16))) _Float16 xs[2 * XS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int p = lane & 15, g = lane >> 4;
   const int tiles_x = (a.ow + TW - 1) / TW, tiles_y = (a.oh + TH - 1) / TH;
-  int bid = blockIdx.x;
-  {
-    const int nblk = gridDim.x, xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
-  const int tx = bid % tiles_x;
-  const int t1 = bid / tiles_x;
-  const int ty = t1 % tiles_y;
-  const int n = t1 / tiles_y;
-  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int ntiles = a.n * tiles_y * tiles_x;
   const int wr = wid % RG, wc = wid / RG;
   const int co0 = wc * WCH * 16;
 
-  // weights for the whole K, issued first (L2-resident, overlaps the halo staging)
+  // weights for the whole K stay in registers across all tiles of this (persistent) block
   h8 wf[NKS][WCH];
 #pragma unroll
   for (int s = 0; s < NKS; ++s) {
     const int q = 4 * s + g;  // k = 8q (zero-padded weights beyond 9*CIN)
 #pragma unroll
     for (int t = 0; t < WCH; ++t) wf[s][t] = *(const h8*)((const _Float16*)a.w + (size_t)(co0 + 16 * t + p) * a.kpad + 8 * q);
-  }
-  // input halo rows oy0-1 .. oy0+TH, cols ox0-1 .. ox0+TW
-  const _Float16* __restrict__ in = (const _Float16*)a.in + a.in_co;
-  for (int i = tid; i < (TH + 2) * HW * CG; i += 256) {
-    const int pix = i / CG, v = i - pix * CG;
-    const int r = pix / HW, c = pix - r * HW;
-    const int y = oy0 - 1 + r, x = ox0 - 1 + c;
-    u32x4 d = {0u, 0u, 0u, 0u};
-    if ((unsigned)y < (unsigned)a.ih && (unsigned)x < (unsigned)a.iw)
-      d = *(const u32x4*)(in + ((size_t)(n * a.ih + y) * a.iw + x) * a.in_cs + v * 8);
-    *(u32x4*)(xs + pix * PS + v * 8) = d;
   }
   // per-lane LDS offset of every k-step (tap clamped for the zero-weight tail)
   int kofs[NKS];
@@ -1264,50 +1249,89 @@ __global__ __launch_bounds__(256) void conv3_pool_small(ConvArgs a) {
     const int kh = tap / 3, kw = tap - kh * 3;
     kofs[s] = (kh * HW + kw) * PS + cg * 8;
   }
-  const _Float16* xb = xs + (wr * WROWS * HW + p) * PS;
-  f4 acc[WROWS][WCH];
+  float bias[WCH][4];
 #pragma unroll
-  for (int j = 0; j < WROWS; ++j)
+  for (int t = 0; t < WCH; ++t)
 #pragma unroll
-    for (int t = 0; t < WCH; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
+    for (int r = 0; r < 4; ++r) bias[t][r] = a.e.bias ? a.e.bias[co0 + 16 * t + 4 * g + r] : 0.f;
+
+  const _Float16* __restrict__ in = (const _Float16*)a.in + a.in_co;
+  u32x4 pre[PV];
+  auto prefetch = [&](int tile) {
+    const int tx = tile % tiles_x, t1 = tile / tiles_x;
+    const int ty = t1 % tiles_y, n = t1 / tiles_y;
 #pragma unroll
-  for (int s = 0; s < NKS; ++s) {
-    const _Float16* bp = xb + kofs[s];
-#pragma unroll
-    for (int j = 0; j < WROWS; ++j) {
-      const h8 b = *(const h8*)(bp + j * HW * PS);
-#pragma unroll
-      for (int t = 0; t < WCH; ++t) acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][t], b, acc[j][t], 0, 0, 0);
+    for (int k = 0; k < PV; ++k) {
+      const int i = tid + 256 * k;
+      const int pix = i / CG, v = i - pix * CG;
+      const int r = pix / HW, c = pix - r * HW;
+      const int y = ty * TH - 1 + r, x = tx * TW - 1 + c;
+      u32x4 d = {0u, 0u, 0u, 0u};
+      if (i < HALO && (unsigned)y < (unsigned)a.ih && (unsigned)x < (unsigned)a.iw)
+        d = *(const u32x4*)(in + ((size_t)(n * a.ih + y) * a.iw + x) * a.in_cs + v * 8);
+      pre[k] = d;
     }
-  }
-  // pooled epilogue: lane = pixel column ox0 + p, rows j; channels co0 + 16t + 4g + r
+  };
   const Epilogue& e = a.e;
   const int qh = a.oh >> 1, qw = a.ow >> 1;
-  const int px = (ox0 + p) >> 1;
+  int buf = 0;
+  int tile = blockIdx.x;
+  if (tile < ntiles) prefetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    _Float16* xb_w = xs + buf * XS;
 #pragma unroll
-  for (int t = 0; t < WCH; ++t) {
-    const int c0 = co0 + 16 * t + 4 * g;
-    float bias[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bias[r] = e.bias ? e.bias[c0 + r] : 0.f;
-#pragma unroll
-    for (int j = 0; j < WROWS; j += 2) {
-      float m[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float t2 = fmaxf(acc[j][t][r], acc[j + 1][t][r]);
-        float x = fmaxf(t2, dpp_xor1(t2)) + bias[r];
-        if (e.act == ACT_LEAKY) x = x > 0.f ? x : x * e.slope;
-        m[r] = x;
-      }
-      const int py = (oy0 + wr * WROWS + j) >> 1;
-      if ((p & 1) == 0 && py < qh && px < qw) {
-        const size_t pp = ((size_t)n * qh + py) * qw + px;
-        *(uint2*)((_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0) =
-            make_uint2(pack_h2(m[0], m[1]), pack_h2(m[2], m[3]));
+    for (int k = 0; k < PV; ++k) {
+      const int i = tid + 256 * k;
+      if (i < HALO) {
+        const int pix = i / CG, v = i - pix * CG;
+        *(u32x4*)(xb_w + pix * PS + v * 8) = pre[k];
       }
     }
+    __syncthreads();
+    const int tx = tile % tiles_x, t1 = tile / tiles_x;
+    const int ty = t1 % tiles_y, n = t1 / tiles_y;
+    if (tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);  // in flight during the MFMAs
+    const _Float16* xb = xb_w + (wr * WROWS * HW + p) * PS;
+    f4 acc[WROWS][WCH];
+#pragma unroll
+    for (int j = 0; j < WROWS; ++j)
+#pragma unroll
+      for (int t = 0; t < WCH; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const _Float16* bp = xb + kofs[s];
+#pragma unroll
+      for (int j = 0; j < WROWS; ++j) {
+        const h8 b = *(const h8*)(bp + j * HW * PS);
+#pragma unroll
+        for (int t = 0; t < WCH; ++t)
+          acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][t], b, acc[j][t], 0, 0, 0);
+      }
+    }
+    // pooled epilogue: lane = pixel column ox0 + p, rows j; channels co0 + 16t + 4g + r
+    const int px = (tx * TW + p) >> 1;
+#pragma unroll
+    for (int t = 0; t < WCH; ++t) {
+      const int c0 = co0 + 16 * t + 4 * g;
+#pragma unroll
+      for (int j = 0; j < WROWS; j += 2) {
+        float m[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t2 = fmaxf(acc[j][t][r], acc[j + 1][t][r]);
+          float x = fmaxf(t2, dpp_xor1(t2)) + bias[t][r];
+          if (e.act == ACT_LEAKY) x = x > 0.f ? x : x * e.slope;
+          m[r] = x;
+        }
+        const int py = (ty * TH + wr * WROWS + j) >> 1;
+        if ((p & 1) == 0 && py < qh && px < qw) {
+          const size_t pp = ((size_t)n * qh + py) * qw + px;
+          *(uint2*)((_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0) =
+              make_uint2(pack_h2(m[0], m[1]), pack_h2(m[2], m[3]));
+        }
+      }
+    }
+    buf ^= 1;
   }
 }
 
@@ -1321,13 +1345,38 @@ static bool pool_small_ok(const ConvArgs& a) {
   return a.kpad >= 32 * ((9 * a.cin / 8 + 3) / 4);  // weights read up to k = 32 * NKS
 }
 
+// Resident blocks per CU of a kernel (occupancy API, cached by the caller).
+template <class K>
+static int resident_blocks(K kernel, int threads, size_t lds) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds) != hipSuccess || nb < 1) nb = 1;
+  return nb;
+}
+
+static int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
 static void launch_pool_small(const ConvArgs& a, hipStream_t s) {
   const int th = a.cin == 16 ? 16 : 8;
-  const int64_t blocks = (int64_t)a.n * ((a.oh + th - 1) / th) * ((a.ow + 15) / 16);
-  if (a.cin == 16)
+  const int64_t tiles = (int64_t)a.n * ((a.oh + th - 1) / th) * ((a.ow + 15) / 16);
+  RTDM_REQUIRE(tiles < (1ll << 31), RTDM_E_CAPACITY, "conv: too many tiles");
+  // persistent blocks: exactly the resident count, each streaming tiles with its weights in registers
+  if (a.cin == 16) {
+    static const int per_cu = resident_blocks(conv3_pool_small<16, 32, 16, 4, 2>, 256, 0);
+    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cu_count());
     hipLaunchKernelGGL((conv3_pool_small<16, 32, 16, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-  else
+  } else {
+    static const int per_cu = resident_blocks(conv3_pool_small<32, 64, 8, 4, 2>, 256, 0);
+    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cu_count());
     hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  }
 }
 
 static int direct_cc_log2(int cin) {
