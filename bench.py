@@ -130,6 +130,25 @@ def step_table(det, n):
     return h, rows
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*_traffic.json, written by tools/prof_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command;
+    FETCH_SIZE doubled per the gfx950 correction).  None when no pass covers it."""
+    import glob
+    base = kernel.split("<")[0]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), key=os.path.getmtime)
+    for path in reversed(files):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for k, t in d.items():
+            if k.split("<")[0] == base and "fetch_size_bytes_avg" in t and "write_size_bytes_avg" in t:
+                return {"bytes_per_launch": t["hbm_bytes_avg"], "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def cpu_baseline(args, text, stream, sd):
     """Oracle leg: the torch-CPU restatement of the reference path (preprocess + classifier +
     Darknet + decode + NMS) on a bounded sample of the same workload."""
@@ -213,6 +232,8 @@ def main():
     det_ms = sum(ms) / max(1, calls.value)
     avg_ms = t_ms / launches
     achieved_tflops = (flop / launches) / (avg_ms * 1e-3) / 1e12
+    tr = pmc_traffic(dom)
+    traffic = round(tr["bytes_per_launch"]) if tr else None
     frames_total = world * b * args.steps
     value = frames_total / elapsed
     pipe_flop = det.flop_per_image + CLASSIFIER_FLOP[args.classifier]
@@ -230,8 +251,10 @@ def main():
                    "parallelism": f"dp{world} (frame shards, no data-path collective)"},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved_tflops, 2),
                      "peak": MFMA_F16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved_tflops / MFMA_F16_DENSE_PEAK_TFLOPS, 4), "traffic": None,
-                     "avg_launch_ms": round(avg_ms, 4), "launches": launches},
+                     "frac": round(achieved_tflops / MFMA_F16_DENSE_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "avg_launch_ms": round(avg_ms, 4), "launches": launches,
+                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tr["source"] if tr else None,
+                     "algorithmic_bytes_per_launch": round(byt / launches)},
         "pipeline": {"flop_per_frame": pipe_flop,
                      "pipeline_tflops": round(pipe_flop * value / world / 1e12, 2),
                      "pipeline_frac": round(pipe_flop * value / world / 1e12 / MFMA_F16_DENSE_PEAK_TFLOPS, 4),

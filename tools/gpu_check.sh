@@ -11,7 +11,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 has() { [[ " $STAGES " == *" $1 "* ]]; }
 if has tests; then
-  echo "== tests"; timeout -k 10 900 python -m pytest $R/tests -m gpu -x -q > $OUT/gpu_tests_$TAG.log 2>&1
+  echo "== tests"; timeout -k 10 900 python -u -m pytest $R/tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/gpu_tests_$TAG.log 2>&1
   rc=$?; tail -3 $OUT/gpu_tests_$TAG.log; [ $rc -eq 0 ] || exit $rc
 fi
 if has smoke; then
