@@ -106,6 +106,11 @@ int rtdm_abi_version(void);
 const char* rtdm_last_error(void);
 /* gfx arch string the code objects were built for ("gfx950"). */
 const char* rtdm_build_arch(void);
+/* Kernel-selection knobs for A/B measurement (no reference counterpart; the
+ * defaults are the tuned choice).  key "conv_pipe": 1 = pipelined 256x128
+ * implicit GEMM for Cin%64==0 convs (default), 0 = conv_glds_f16 128x128.
+ * Takes effect for handles created afterwards.                                  */
+rtdm_status rtdm_set_tuning(const char* key, int value);
 
 /* ---- classifier ------------------------------------------------------------ */
 /* params: the reference state_dict (e.g. weights/squeeze-ernet-state_dict.pt),

@@ -22,6 +22,16 @@ const char* rtdm_last_error(void) { return get_error(); }
 
 const char* rtdm_build_arch(void) { return "gfx950"; }
 
+rtdm_status rtdm_set_tuning(const char* key, int value) {
+  return guard([&] {
+    RTDM_REQUIRE(key, RTDM_E_INVALID, "set_tuning: NULL key");
+    if (!strcmp(key, "conv_pipe"))
+      set_conv_pipe_mode(value);
+    else
+      throw Error{RTDM_E_INVALID, std::string("set_tuning: unknown key ") + key};
+  });
+}
+
 rtdm_status rtdm_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const float* anchors, int img_h,
                              int img_w, float* io, int io_rows, int row_offset, void* stream) {
   return guard([&] {

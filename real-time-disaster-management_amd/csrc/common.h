@@ -169,6 +169,11 @@ struct ConvArgs {
 
 // Launchers (conv.hip).  dtype = RTDM_F16 / RTDM_F32 (activation + weight type).
 void launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
+// conv_pipe.hip: pipelined 256x128 implicit GEMM for Cin % 64 == 0 layers
+bool conv_pipe_ok(const ConvArgs& a);
+void launch_conv_pipe(const ConvArgs& a, hipStream_t s);
+int conv_pipe_mode();
+void set_conv_pipe_mode(int v);
 // Kernel symbol (template instantiation) launch_conv will pick for a / dtype.
 const char* conv_kernel_name(const ConvArgs& a, int dtype);
 // Row geometry helpers shared by host planners.

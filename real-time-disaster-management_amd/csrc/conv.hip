@@ -18,246 +18,11 @@
 // fused as a x2 store), the YOLOLayer decode (:252-258, fused into the head
 // conv) and ACFF's fused 1x1 conv -> LeakyReLU(0.01) -> BatchNorm
 // (disaster_detection/model/acff.py:49-53, BN applied as a post-activation affine).
-#include "common.h"
+#include "conv_epi.h"
 
 #include <algorithm>
 
 namespace rtdm {
-
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-typedef float f4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-template <typename T>
-__device__ __forceinline__ float ldf(const T* p) {
-  return (float)(*p);
-}
-template <typename T>
-__device__ __forceinline__ void stf(T* p, float v) {
-  *p = (T)v;
-}
-
-__device__ __forceinline__ void row_to_pix(const ConvArgs& a, int m, int& n, int& oy, int& ox) {
-  if (a.quad) {
-    const int q = m >> 2, d = m & 3;
-    const int t = fdiv(q, a.fd_qw);
-    const int qx = q - t * a.qw;
-    n = fdiv(t, a.fd_qh);
-    const int qy = t - n * a.qh;
-    oy = 2 * qy + (d >> 1);
-    ox = 2 * qx + (d & 1);
-  } else {
-    const int t = fdiv(m, a.fd_ow);
-    ox = m - t * a.ow;
-    n = fdiv(t, a.fd_oh);
-    oy = t - n * a.oh;
-  }
-}
-
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
-
-// Pixel of row m0 + r given the pixel (n, oy0, ox0) of row m0 (m0 % 4 == 0):
-// quad order -> the 2x2 quad; linear order -> the next pixels of the same image
-// row when they exist (row_to_pix otherwise).
-__device__ __forceinline__ void row_pix4(const ConvArgs& a, int m0, int r, int n0, int oy0, int ox0, int& n, int& oy,
-                                         int& ox) {
-  if (a.quad) {
-    n = n0;
-    oy = oy0 + (r >> 1);
-    ox = ox0 + (r & 1);
-  } else if (ox0 + r < a.ow) {
-    n = n0;
-    oy = oy0;
-    ox = ox0 + r;
-  } else {
-    row_to_pix(a, m0 + r, n, oy, ox);
-  }
-}
-
-// Epilogue for the 4 accumulator values of rows m0..m0+3 (m0 % 4 == 0) in
-// output channel c.  In quad mode the 4 rows are one 2x2 pixel quad.
-template <typename T>
-__device__ __forceinline__ void epi4(const ConvArgs& a, int m0, int c, f4 v) {
-  const Epilogue& e = a.e;
-  if (m0 >= a.M) return;
-  const float bias = e.bias ? e.bias[c] : 0.f;
-  const float sc = e.scale ? e.scale[c] : 1.f;
-  const float sh = e.scale ? e.shift[c] : 0.f;
-  float pmax = -INFINITY;
-  int n0, oy0, ox0;
-  row_to_pix(a, m0, n0, oy0, ox0);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int m = m0 + r;
-    if (m < a.M) {
-      int n, oy, ox;
-      row_pix4(a, m0, r, n0, oy0, ox0, n, oy, ox);
-      float x = v[r] + bias;
-      if (e.act == ACT_LEAKY) {
-        x = x > 0.f ? x : x * e.slope;
-      } else if (e.act == ACT_SWISH) {
-        x = x * sigmoidf_(x);
-      }
-      if (e.scale) x = x * sc + sh;
-      const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
-      if (e.res.ptr) x += ldf((const T*)e.res.ptr + pix * e.res.cs + e.res.co + c);
-      pmax = fmaxf(pmax, x);
-      if (e.full.ptr) stf((T*)e.full.ptr + pix * e.full.cs + e.full.co + c, x);
-      if (e.up.ptr) {
-        const int uw = a.ow * 2;
-        const size_t u0 = ((size_t)n * a.oh * 2 + 2 * oy) * uw + 2 * ox;
-        T* up = (T*)e.up.ptr + e.up.co + c;
-        const T hv = (T)x;
-        up[u0 * e.up.cs] = hv;
-        up[(u0 + 1) * e.up.cs] = hv;
-        up[(u0 + uw) * e.up.cs] = hv;
-        up[(u0 + uw + 1) * e.up.cs] = hv;
-      }
-      if (e.io) {
-        const int ai = c / e.no, k = c - ai * e.no;
-        float o;
-        if (k < 2) {
-          o = (sigmoidf_(x) + (float)(k == 0 ? ox : oy)) * e.ystride;
-        } else if (k < 4) {
-          o = (expf(x) * e.anchor_vec[2 * ai + (k - 2)]) * e.ystride;
-        } else {
-          o = sigmoidf_(x);
-        }
-        const size_t row = (size_t)e.io_off + ((size_t)ai * a.oh + oy) * a.ow + ox;
-        e.io[((size_t)n * e.io_rows + row) * e.no + k] = o;
-      }
-    }
-  }
-  if (e.pool.ptr && a.quad) {
-    const size_t pp = ((size_t)n0 * a.qh + (oy0 >> 1)) * a.qw + (ox0 >> 1);
-    stf((T*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c, pmax);
-  }
-}
-
-// Vector epilogue for a 2x2 quad / 4 consecutive rows (m0..m0+3) x 8 consecutive
-// channels (c0..c0+7) of an fp16 output: bias -> act -> affine -> residual, then
-// 16-byte stores of the full / pooled / upsampled views when they are 8-aligned
-// (channel stride and offset multiples of 8), scalar stores otherwise; YOLO
-// decode channels go to io as fp32 scalars.
-typedef _Float16 h8v __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ void epi_vec8(const ConvArgs& a, int m0, int c0, const float (&v)[4][8]) {
-  const Epilogue& e = a.e;
-  const int nc = a.cout - c0 < 8 ? a.cout - c0 : 8;
-  float bias[8], sc[8], sh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bool cv = j < nc;
-    bias[j] = (e.bias && cv) ? e.bias[c0 + j] : 0.f;
-    sc[j] = (e.scale && cv) ? e.scale[c0 + j] : 1.f;
-    sh[j] = (e.scale && cv) ? e.shift[c0 + j] : 0.f;
-  }
-  const bool full8 = nc == 8;
-  float pmax[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) pmax[j] = -INFINITY;
-  int pn, poy, pox;
-  row_to_pix(a, m0, pn, poy, pox);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int m = m0 + r;
-    if (m >= a.M) continue;
-    int n, oy, ox;
-    row_pix4(a, m0, r, pn, poy, pox, n, oy, ox);
-    const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
-    float x[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float t = v[r][j] + bias[j];
-      if (e.act == ACT_LEAKY)
-        t = t > 0.f ? t : t * e.slope;
-      else if (e.act == ACT_SWISH)
-        t = t * sigmoidf_(t);
-      x[j] = t * sc[j] + sh[j];
-    }
-    if (e.res.ptr) {
-      const _Float16* rp = (const _Float16*)e.res.ptr + pix * e.res.cs + e.res.co + c0;
-      if (full8 && ((e.res.cs | e.res.co) & 7) == 0) {
-        const h8v rv = *(const h8v*)rp;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] += (float)rv[j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < nc) x[j] += (float)rp[j];
-      }
-    }
-    h8v hv;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      hv[j] = (_Float16)x[j];
-      pmax[j] = fmaxf(pmax[j], x[j]);
-    }
-    if (e.full.ptr) {
-      _Float16* fp = (_Float16*)e.full.ptr + pix * e.full.cs + e.full.co + c0;
-      if (full8 && ((e.full.cs | e.full.co) & 7) == 0) {
-        *(h8v*)fp = hv;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < nc) fp[j] = hv[j];
-      }
-    }
-    if (e.up.ptr) {
-      const int uw = a.ow * 2;
-      const size_t u0 = ((size_t)n * a.oh * 2 + 2 * oy) * uw + 2 * ox;
-      _Float16* up = (_Float16*)e.up.ptr + e.up.co + c0;
-      const size_t uo[4] = {u0, u0 + 1, u0 + uw, u0 + uw + 1};
-      if (full8 && ((e.up.cs | e.up.co) & 7) == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) *(h8v*)(up + uo[q] * e.up.cs) = hv;
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (j < nc) up[uo[q] * e.up.cs + j] = hv[j];
-      }
-    }
-    if (e.io) {
-      // (anchor, field) of channel c0 by one division, then stepped per channel;
-      // fp16 path: hardware exp / reciprocal (well inside the fp16 tolerance)
-      int ai = c0 / e.no, k = c0 - ai * e.no;
-      const size_t pix_io = (size_t)n * e.io_rows + e.io_off + (size_t)oy * a.ow + ox;
-      const size_t plane = (size_t)a.oh * a.ow;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (j < nc) {
-          float o;
-          if (k < 2)
-            o = (__frcp_rn(1.f + __expf(-x[j])) + (float)(k == 0 ? ox : oy)) * e.ystride;
-          else if (k < 4)
-            o = (__expf(x[j]) * e.anchor_vec[2 * ai + (k - 2)]) * e.ystride;
-          else
-            o = __frcp_rn(1.f + __expf(-x[j]));
-          e.io[(pix_io + (size_t)ai * plane) * e.no + k] = o;
-        }
-        if (++k == e.no) {
-          k = 0;
-          ++ai;
-        }
-      }
-    }
-  }
-  if (e.pool.ptr && a.quad && m0 < a.M) {
-    const size_t pp = ((size_t)pn * a.qh + (poy >> 1)) * a.qw + (pox >> 1);
-    _Float16* qp = (_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0;
-    if (full8 && ((e.pool.cs | e.pool.co) & 7) == 0) {
-      h8v pv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pv[j] = (_Float16)pmax[j];
-      *(h8v*)qp = pv;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < nc) qp[j] = (_Float16)pmax[j];
-    }
-  }
-}
 
 // --------------------------------------------------------------------------
 // fp16 MFMA implicit GEMM.  BM x BN block tile, BK-deep K-blocks, WM x WN waves.
@@ -735,8 +500,6 @@ __global__ __launch_bounds__(256) void conv_valu(ConvArgs a) {
 // ds_read_b128 lane group touches then cover all 64 banks.  Out-of-image taps,
 // K padding and rows past M read a 16-byte zero block (a.zero) instead.
 // --------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 template <int BM, int NS>
 __global__ __launch_bounds__(BM * 2, (BM == 128 && NS == 2) ? 2 : 1) void conv_glds_f16(ConvArgs a) {
@@ -1449,6 +1212,23 @@ static bool stem_ok(const ConvArgs& a) {
   return stem3_lds_bytes(a) <= 64 * 1024;
 }
 
+// Pipelined 256x128 kernel (conv_pipe.hip) for the Cin % 64 == 0 layers; 0 = off
+// (conv_glds_f16 takes them).  RTDM_CONV_PIPE in the environment, or
+// rtdm_set_tuning("conv_pipe", v), for A/B runs.
+static int g_conv_pipe = -1;
+int conv_pipe_mode() {
+  if (g_conv_pipe < 0) {
+    const char* e = getenv("RTDM_CONV_PIPE");
+    g_conv_pipe = e ? atoi(e) : 1;
+  }
+  return g_conv_pipe;
+}
+void set_conv_pipe_mode(int v) { g_conv_pipe = v < 0 ? 0 : v; }
+
+static bool use_pipe(const ConvArgs& a, int dtype) {
+  return dtype == RTDM_F16 && conv_pipe_mode() > 0 && conv_pipe_ok(a);
+}
+
 const char* conv_kernel_name(const ConvArgs& a, int dtype) {
   if (dtype == RTDM_F16 && stem_ok(a)) {
     static const char* names[2][3] = {{"conv_stem3<false,1>", "conv_stem3<false,2>", "conv_stem3<false,4>"},
@@ -1462,6 +1242,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     const int bn = direct_cfg(a.cout_pad).bn;
     return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
   }
+  if (use_pipe(a, dtype)) return "conv_pipe_f16";
   if (dtype == RTDM_F16 && glds_ok(a)) {
     static const char* names[2][2] = {{"conv_glds_f16<128,2>", "conv_glds_f16<128,3>"},
                                       {"conv_glds_f16<256,2>", "conv_glds_f16<256,3>"}};
@@ -1498,6 +1279,8 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     launch_pool_small(a, s);
   } else if (dtype == RTDM_F16 && direct_ok(a)) {
     launch_direct(a, s);
+  } else if (use_pipe(a, dtype)) {
+    launch_conv_pipe(a, s);
   } else if (dtype == RTDM_F16 && glds_ok(a)) {
     const GldsCfg c = glds_cfg();
     const int64_t nblk = (int64_t)((a.M + c.bm - 1) / c.bm) * (a.cout_pad / 128);

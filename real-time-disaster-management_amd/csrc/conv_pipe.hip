@@ -1,0 +1,306 @@
+// Pipelined fp16 implicit-GEMM convolution for the MFMA-bound Darknet layers
+// (3x3 / 1x1, Cin % 64 == 0): the conv_glds_f16 data path (direct
+// global->LDS buffer loads, source-swizzled LDS image, scalar tap cursor) in a
+// schedule built for one workgroup per CU.
+//
+//   tile        256 (pixels) x 128 (output channels), BK = 64
+//   waves       8 = 4 (M) x 2 (N), 64 x 64 outputs each (FM x FN = 4 x 4
+//               accumulators of v_mfma_f32_16x16x32_f16), 2 waves per SIMD.
+//               (Measured alternative: 4 waves of 128 x 64 — 3/4 of the LDS read
+//               bytes per FLOP — ran 30 % slower: one wave per SIMD, and hipcc
+//               spills the 128 accumulators into AGPR copy chains in the loop.)
+//   LDS         3 stages x 48 KB: loads of K-block kb+2 are issued while kb is
+//               multiplied and kb+1 is landing; a counted "s_waitcnt vmcnt(VM)"
+//               (VM = buffer->LDS ops per thread per stage) retires kb+1 while
+//               kb+2 stays in flight across the one raw s_barrier per K-block
+//   fragments   two register sets: the LDS reads of the next half K-block are
+//               interleaved with the MFMAs of the current one
+//
+// Replaces the same reference ops as conv.hip (victim_localization/yolov3/
+// models.py:23-44 conv + BN + LeakyReLU as run by Darknet.forward :345-347,
+// with the fused epilogues of conv_epi.h).
+#include "conv_epi.h"
+
+#include <type_traits>
+
+namespace rtdm {
+
+namespace {
+constexpr int kPBM = 256, kPBN = 128, kPBK = 64, kPNS = 3;
+constexpr int kPStage = (kPBM + kPBN) * kPBK;  // halfs per stage
+constexpr int kPCstr = kPBN + 4;
+constexpr int kPSmem = kPNS * kPStage * 2 > kPBM * kPCstr * 4 ? kPNS * kPStage * 2 : kPBM * kPCstr * 4;
+
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+  if constexpr (N == 6)
+    asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 12)
+    asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+}  // namespace
+
+// ABL: ablation bits for diagnostic builds only (outputs are wrong when non-zero):
+// 1 = no buffer->LDS loads in the K-loop, 2 = no fragment ds_reads in the K-loop,
+// 4 = no wait + barrier in the K-loop.
+template <int ABL>
+__global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
+  constexpr int WM = 4, WN = 2;
+  constexpr int BM = kPBM, BN = kPBN, BK = kPBK;
+  constexpr int WAVES = WM * WN, NT = 64 * WAVES;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // accumulators per wave
+  constexpr int NA = BM * BK * 2 / (NT * 16);          // A buffer->LDS ops per thread per stage
+  constexpr int NB = BN * BK * 2 / (NT * 16);          // B ops
+  constexpr int VM = NA + NB;
+  static_assert(VM == 6 || VM == 12, "wait literal");
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kPSmem];
+  _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntn = a.cout_pad / BN;
+  int bid = blockIdx.x;
+  {  // bijective XCD remap: each XCD runs a contiguous run of tiles (shared A panels in its L2)
+    const int nblk = gridDim.x, xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int mt = bid / ntn;
+  const int m_base = mt * BM, n_base = (bid - mt * ntn) * BN;
+
+  // ---- per-lane staging state.  A op j of wave w fills tile rows 8(NA w + j) + lane/8,
+  //      B op j rows 8(NB w + j) + lane/8; LDS slot lane%8 of a row holds k-vector
+  //      slot ^ ((row >> 1) & 7) (the read side applies the same involution). ----
+  const int slot = lane & 7;
+  int voff_a[NA];
+  uint32_t vmask[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int r = 8 * (NA * wid + j) + (lane >> 3);
+    const int kofs = 8 * (slot ^ ((r >> 1) & 7));
+    const int m = m_base + r;
+    int n = 0, oy = 0, ox = 0;
+    if (m < a.M) row_to_pix(a, m, n, oy, ox);
+    const int iy0 = m < a.M ? oy * a.stride - a.pad : -(1 << 28);
+    const int ix0 = ox * a.stride - a.pad;
+    voff_a[j] = m < a.M ? ((n * a.ih * a.iw + iy0 * a.iw + ix0) * a.in_cs + kofs) * 2 : 0;
+    uint32_t msk = 0;
+    for (int t = 0; t < a.ks * a.ks; ++t) {
+      const int kh = a.ks == 3 ? (t * 11) >> 5 : 0, kw = t - kh * a.ks;
+      const int iy = iy0 + kh, ix = ix0 + kw;
+      if ((unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw) msk |= 1u << t;
+    }
+    vmask[j] = msk;
+  }
+  int voff_b[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int r = 8 * (NB * wid + j) + (lane >> 3);
+    voff_b[j] = (r * a.kpad + 8 * (slot ^ ((r >> 1) & 7))) * 2;
+  }
+  const _Float16* in = (const _Float16*)a.in + a.in_co;
+  const int64_t in_bytes = ((int64_t)a.n * a.ih * a.iw * a.in_cs - a.in_co) * 2;
+  const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const _Float16*)a.w + (size_t)n_base * a.kpad), 0, BN * a.kpad * 2, 0x00020000);
+  const int nk = a.kpad / BK;
+  const int cpt = a.cin / BK;  // K-blocks per tap
+  int st_tap = 0, st_c = 0, st_buf = 0, st_kb = 0;
+
+  // Issue the VM buffer->LDS ops of the next K-block (cursor st_*) into stage st_buf.
+  auto stage = [&]() {
+    _Float16* As = smem + st_buf * kPStage;
+    _Float16* Bs = As + BM * BK;
+    const int kh = a.ks == 3 ? (st_tap * 11) >> 5 : 0, kw = st_tap - kh * a.ks;
+    const int tapoff = ((kh * a.iw + kw) * a.in_cs + st_c * BK) * 2;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int vo = ((vmask[j] >> st_tap) & 1u) ? voff_a[j] + tapoff : (int)0x80000000;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(As + 8 * (NA * wid + j) * BK), 16, vo, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j],
+                                               st_kb * BK * 2, 0, 0);
+    if (++st_c == cpt) {
+      st_c = 0;
+      ++st_tap;
+    }
+    ++st_kb;
+    st_buf = st_buf == kPNS - 1 ? 0 : st_buf + 1;
+  };
+
+  const int fr = lane & 15, g = lane >> 4;
+  const int rsw = (fr >> 1) & 7;
+  const int so0 = 8 * ((0 + g) ^ rsw), so1 = 8 * ((4 + g) ^ rsw);
+  const int a_row = (wm * (BM / WM) + fr) * BK, b_row = (BM + wn * (BN / WN) + fr) * BK;
+
+  f4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  h8 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
+  auto read0 = [&](int buf) {
+    const _Float16* S = smem + buf * kPStage;
+#pragma unroll
+    for (int t = 0; t < FM; ++t) fa0[t] = *(const h8*)(S + a_row + t * 16 * BK + so0);
+#pragma unroll
+    for (int t = 0; t < FN; ++t) fb0[t] = *(const h8*)(S + b_row + t * 16 * BK + so0);
+  };
+  auto read1 = [&](int buf) {
+    const _Float16* S = smem + buf * kPStage;
+#pragma unroll
+    for (int t = 0; t < FM; ++t) fa1[t] = *(const h8*)(S + a_row + t * 16 * BK + so1);
+#pragma unroll
+    for (int t = 0; t < FN; ++t) fb1[t] = *(const h8*)(S + b_row + t * 16 * BK + so1);
+  };
+  constexpr int NMF = FM * FN, NRD = FM + FN;
+  // MFMA / DS-read interleave of one cluster: NRD reads spread over the NMF MFMAs
+  auto interleave_reads = [&]() {
+    constexpr int per = NMF / NRD > 0 ? NMF / NRD : 1;
+#pragma unroll
+    for (int i = 0; i < NRD; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, per, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // DS read
+    }
+  };
+
+  // prologue: K-blocks 0 and 1 in flight, wait for 0
+  stage();
+  if (nk > 1) {
+    stage();
+    wait_vm_lgkm0<VM>();
+  } else {
+    wait_vm_lgkm0<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  read0(0);
+
+  // Cluster A (half 0 of kb): MFMAs on fa0/fb0, interleaved with the reads of half 1
+  // (fa1/fb1) and the buffer->LDS loads of kb+2.  Cluster B (half 1): MFMAs on
+  // fa1/fb1, interleaved with the reads of half 0 of kb+1 (after the barrier that
+  // publishes kb+1).  The loop is peeled so the steady-state body is one basic
+  // block (interleave groups do not cross branches): STG = loads of kb+2 go out,
+  // NXT = kb+1 exists (wait for it, barrier, read its half 0).
+  int cur = 0;
+  auto body = [&](auto stg, auto nxt_c) {
+    constexpr bool STG = decltype(stg)::value, NXT = decltype(nxt_c)::value;
+    const int nxt = cur == kPNS - 1 ? 0 : cur + 1;
+    if constexpr (!(ABL & 2)) read1(cur);
+    if constexpr (STG && !(ABL & 1)) stage();
+#pragma unroll
+    for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < FN; ++tn)
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa0[tm], fb0[tn], acc[tm][tn], 0, 0, 0);
+    if constexpr (STG && !(ABL & 1)) {
+      // reads in the first half of the cluster, the VM loads in the second
+      constexpr int half = NMF / 2;
+      constexpr int per_r = half / NRD > 0 ? half / NRD : 1;
+      constexpr int per_v = (NMF - half) / VM > 0 ? (NMF - half) / VM : 1;
+#pragma unroll
+      for (int i = 0; i < NRD; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, per_r, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < VM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, per_v, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
+    } else {
+      interleave_reads();
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NXT) {
+      // retire kb+1 (kb+2 stays in flight); lgkmcnt(0): this stage's reads are done
+      // in every wave before any wave restages it (kb+3, issued after this barrier)
+      if constexpr (!(ABL & 4)) {
+        if constexpr (STG)
+          wait_vm_lgkm0<VM>();
+        else
+          wait_vm_lgkm0<0>();
+        __builtin_amdgcn_s_barrier();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(ABL & 2)) read0(nxt);
+    }
+#pragma unroll
+    for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < FN; ++tn)
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa1[tm], fb1[tn], acc[tm][tn], 0, 0, 0);
+    if constexpr (NXT) interleave_reads();
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    cur = nxt;
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  for (int kb = 0; kb + 2 < nk; ++kb) body(T_{}, T_{});
+  if (nk >= 2) body(F_{}, T_{});
+  body(F_{}, F_{});
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: accumulators -> LDS C tile (fp32) -> 4 rows x 8 channels per thread ----
+  float* Cs = reinterpret_cast<float*>(smem_raw);
+  const int rq = g * 4;
+#pragma unroll
+  for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < FN; ++tn) {
+      const int row = wm * (BM / WM) + tm * 16 + rq;
+      const int col = wn * (BN / WN) + tn * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Cs[(row + j) * kPCstr + col] = acc[tm][tn][j];
+    }
+  __syncthreads();
+  constexpr int CG = BN / 8;
+  constexpr int UNITS = (BM / 4) * CG;
+  for (int u = tid; u < UNITS; u += NT) {
+    const int q = u / CG, gg = u - (u / CG) * CG;
+    const int m0 = m_base + q * 4, c0 = n_base + gg * 8;
+    if (m0 >= a.M || c0 >= a.cout) continue;
+    float v[4][8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[r][j] = Cs[(q * 4 + r) * kPCstr + gg * 8 + j];
+    epi_vec8(a, m0, c0, v);
+  }
+}
+
+
+bool conv_pipe_ok(const ConvArgs& a) {
+  if (!a.zero || a.in_kind != IN_NHWC || a.w_f32 || (a.in_cs | a.in_co) % 8 != 0) return false;
+  if (a.cin % 64 != 0 || a.cout_pad % kPBN != 0 || (a.ks != 1 && a.ks != 3)) return false;
+  if (a.kpad != a.ks * a.ks * a.cin) return false;
+  const int64_t elems = (int64_t)a.n * a.ih * a.iw * a.in_cs;
+  return elems < (1ll << 30) && (int64_t)a.cout_pad * a.kpad * 2 < (1ll << 31);
+}
+
+// mode (conv_pipe_mode): 1 = the kernel; 2..5 = ablation builds for diagnostics
+// (tools/ab_conv.py; outputs wrong): 2 no loads, 3 no ds_reads, 4 neither, 5 no
+// barrier.
+void launch_conv_pipe(const ConvArgs& a, hipStream_t s) {
+  const int64_t nblk = (int64_t)((a.M + kPBM - 1) / kPBM) * (a.cout_pad / kPBN);
+  RTDM_REQUIRE(nblk < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
+  const dim3 grid((unsigned)nblk);
+  switch (conv_pipe_mode()) {
+    case 2: hipLaunchKernelGGL((conv_pipe_f16<1>), grid, dim3(512), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((conv_pipe_f16<2>), grid, dim3(512), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((conv_pipe_f16<3>), grid, dim3(512), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((conv_pipe_f16<4>), grid, dim3(512), 0, s, a); break;
+    default: hipLaunchKernelGGL((conv_pipe_f16<0>), grid, dim3(512), 0, s, a); break;
+  }
+}
+
+}  // namespace rtdm

@@ -1,10 +1,14 @@
 """Two-stage classify -> detect pipeline over a batch of uint8 frames.
 
-Per batch, all on one stream, no host synchronisation:
+Per batch, no host synchronisation:
   classifier: CLI transform (resize/crop/normalize) + ACFF model -> logits, probs
+              (on a side stream forked from the caller's stream: the two stages are
+              independent, so the classifier's small, latency-bound kernels fill the
+              CUs the detector's GEMM tails and launch gaps leave idle)
   detector:   Darknet forward with the /255 fused into the stem, YOLO decode fused
-              into the head convs -> io
-  NMS:        per-image greedy NMS -> det [B,max_det,6], idx, count
+              into the head convs -> io (caller's stream)
+  NMS:        per-image greedy NMS -> det [B,max_det,6], idx, count (caller's stream,
+              which then waits for the classifier's event: every output is ready on it)
 The reference has no code joining the two stages; this composes
 aider-predict.py's predict() and detect.py's forward + non_max_suppression.
 """
@@ -27,6 +31,13 @@ class TwoStagePipeline:
         self.multi_label = multi_label
         self.agnostic = agnostic
         self._bufs = {}
+        self._side = {}
+
+    def _side_stream(self, device):
+        key = str(device)
+        if key not in self._side:
+            self._side[key] = (torch.cuda.Stream(device=device), torch.cuda.Event(), torch.cuda.Event())
+        return self._side[key]
 
     def _buffers(self, n, device):
         key = (n, str(device))
@@ -45,13 +56,20 @@ class TwoStagePipeline:
         """frames: [B,H,W,3] uint8 CUDA (H,W = detector img_size)."""
         n = frames.shape[0]
         b = self._buffers(n, frames.device)
-        sp = L.stream_ptr(stream)
         with torch.cuda.device(frames.device):
+            main = stream if stream is not None else torch.cuda.current_stream()
+            side, forked, joined = self._side_stream(frames.device)
+            forked.record(main)
+            side.wait_event(forked)
             hc = self.classifier._get_handle(n)
             L.check(L.lib().rtdm_classify(hc, L.ptr(frames), L.RTDM_INPUT_FRAME_U8, n, frames.shape[1],
-                                          frames.shape[2], L.ptr(b["logits"]), L.ptr(b["probs"]), sp))
+                                          frames.shape[2], L.ptr(b["logits"]), L.ptr(b["probs"]),
+                                          L.stream_ptr(side)))
+            joined.record(side)
             hd = self.detector.handle(n)
-            L.check(L.lib().rtdm_detect(hd, L.ptr(frames), L.RTDM_INPUT_FRAME_U8, n, L.ptr(b["io"]), sp))
-        nms_batched(b["io"], self.conf_thres, self.iou_thres, self.multi_label, None, self.agnostic, self.max_det,
-                    out=(b["det"], b["idx"], b["count"]), stream=stream)
+            L.check(L.lib().rtdm_detect(hd, L.ptr(frames), L.RTDM_INPUT_FRAME_U8, n, L.ptr(b["io"]),
+                                        L.stream_ptr(main)))
+            nms_batched(b["io"], self.conf_thres, self.iou_thres, self.multi_label, None, self.agnostic,
+                        self.max_det, out=(b["det"], b["idx"], b["count"]), stream=main)
+            main.wait_event(joined)
         return b
