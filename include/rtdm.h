@@ -108,8 +108,9 @@ const char* rtdm_last_error(void);
 const char* rtdm_build_arch(void);
 /* Kernel-selection knobs for A/B measurement (no reference counterpart; the
  * defaults are the tuned choice).  key "conv_pipe": 1 = pipelined 256x128
- * implicit GEMM for Cin%64==0 convs (default), 0 = conv_glds_f16 128x128.
- * Takes effect for handles created afterwards.                                  */
+ * implicit GEMM for Cin%64==0 convs (default), 0 = conv_glds_f16 128x128;
+ * key "fuse_head": 1 = conv -> 1x1 head conv -> [yolo] planned as one launch
+ * (default), 0 = separate head conv.  Take effect for handles created afterwards. */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 
 /* ---- classifier ------------------------------------------------------------ */

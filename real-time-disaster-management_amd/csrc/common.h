@@ -165,6 +165,13 @@ struct ConvArgs {
   FastDiv fd_cin;                // set by conv_set_rows
   int glds_uni = 0;              // conv_glds_f16: uniform-tap staging (set by launch_conv)
   Epilogue e;
+  // Fused YOLO head (conv_pipe_f16 only): a 1x1 conv over this conv's activated
+  // output (cout <= 128 = one N tile), head_w fp16 [head_cout_pad][cout_pad] (k = c),
+  // applied in the epilogue with head_e (bias, activation, YOLO decode into io);
+  // this conv's own output is then never written.
+  const void* head_w = nullptr;
+  int head_cout = 0;
+  Epilogue head_e;
 };
 
 // Launchers (conv.hip).  dtype = RTDM_F16 / RTDM_F32 (activation + weight type).
@@ -174,6 +181,9 @@ bool conv_pipe_ok(const ConvArgs& a);
 void launch_conv_pipe(const ConvArgs& a, hipStream_t s);
 int conv_pipe_mode();
 void set_conv_pipe_mode(int v);
+// detector.cpp: plan conv -> 1x1 head -> [yolo] as one fused launch (default 1)
+int fuse_head();
+void set_fuse_head(int v);
 // Kernel symbol (template instantiation) launch_conv will pick for a / dtype.
 const char* conv_kernel_name(const ConvArgs& a, int dtype);
 // Row geometry helpers shared by host planners.

@@ -1226,7 +1226,7 @@ int conv_pipe_mode() {
 void set_conv_pipe_mode(int v) { g_conv_pipe = v < 0 ? 0 : v; }
 
 static bool use_pipe(const ConvArgs& a, int dtype) {
-  return dtype == RTDM_F16 && conv_pipe_mode() > 0 && conv_pipe_ok(a);
+  return dtype == RTDM_F16 && (conv_pipe_mode() > 0 || a.head_w) && conv_pipe_ok(a);
 }
 
 const char* conv_kernel_name(const ConvArgs& a, int dtype) {
@@ -1242,7 +1242,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     const int bn = direct_cfg(a.cout_pad).bn;
     return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
   }
-  if (use_pipe(a, dtype)) return "conv_pipe_f16";
+  if (use_pipe(a, dtype)) return a.head_w ? "conv_pipe_f16+head" : "conv_pipe_f16";
   if (dtype == RTDM_F16 && glds_ok(a)) {
     static const char* names[2][2] = {{"conv_glds_f16<128,2>", "conv_glds_f16<128,3>"},
                                       {"conv_glds_f16<256,2>", "conv_glds_f16<256,3>"}};
@@ -1260,6 +1260,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
 
 void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
   if (a.M <= 0) return;
+  RTDM_REQUIRE(!a.head_w || use_pipe(a, dtype), RTDM_E_INVALID, "conv: fused head on a shape conv_pipe_f16 does not take");
   RTDM_REQUIRE(!a.quad || (a.oh >= 2 && a.ow >= 2), RTDM_E_INVALID, "conv: quad ordering needs >= 2x2 output");
   RTDM_REQUIRE(!a.e.pool.ptr || a.quad, RTDM_E_INVALID, "conv: pooled output needs quad ordering");
   if (dtype == RTDM_F16 && stem_ok(a)) {

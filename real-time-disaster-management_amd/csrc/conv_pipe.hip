@@ -42,9 +42,39 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
 }
 }  // namespace
 
+// Fused-head epilogue for the 4 rows m0..m0+3 of head channel c (YOLOLayer
+// inference branch, models.py:252-258): bias -> activation -> decode -> io.
+__device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v) {
+  const Epilogue& e = a.head_e;
+  if (m0 >= a.M) return;
+  const float bias = e.bias[c];
+  const int ai = c / e.no, k = c - ai * e.no;
+  const float anc = k == 2 || k == 3 ? e.anchor_vec[2 * ai + (k - 2)] : 0.f;
+  int n0, oy0, ox0;
+  row_to_pix(a, m0, n0, oy0, ox0);
+  const size_t plane = (size_t)a.oh * a.ow;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (m0 + r >= a.M) break;
+    int n, oy, ox;
+    row_pix4(a, m0, r, n0, oy0, ox0, n, oy, ox);
+    float x = v[r] + bias;
+    if (e.act == ACT_LEAKY) x = x > 0.f ? x : x * e.slope;
+    float o;
+    if (k < 2)
+      o = (__frcp_rn(1.f + __expf(-x)) + (float)(k == 0 ? ox : oy)) * e.ystride;
+    else if (k < 4)
+      o = (__expf(x) * anc) * e.ystride;
+    else
+      o = __frcp_rn(1.f + __expf(-x));
+    const size_t row = (size_t)n * e.io_rows + e.io_off + (size_t)ai * plane + (size_t)oy * a.ow + ox;
+    e.io[row * e.no + k] = o;
+  }
+}
+
 // ABL: ablation bits for diagnostic builds only (outputs are wrong when non-zero):
 // 1 = no buffer->LDS loads in the K-loop, 2 = no fragment ds_reads in the K-loop,
-// 4 = no wait + barrier in the K-loop.
+// 4 = no wait + barrier in the K-loop.  Bit 8 (not an ablation): fused YOLO head.
 template <int ABL>
 __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
   constexpr int WM = 4, WN = 2;
@@ -250,6 +280,63 @@ __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
+  if constexpr ((ABL & 8) != 0) {
+    // ---- fused head: activated conv output (fp16, the value the unfused path would
+    //      store) -> LDS tile [256][128] (16-B slot swizzle: slot ^ (row & 15)) ->
+    //      1x1 head GEMM on MFMA -> YOLO decode -> io.  Same fp16 operands and K
+    //      order as the unfused head conv.
+    _Float16* Hs = smem;
+    const Epilogue& e = a.e;
+#pragma unroll
+    for (int tn = 0; tn < FN; ++tn) {
+      const int col = wn * (BN / WN) + tn * 16 + fr;
+      const bool cv = col < a.cout;
+      const float bias = cv ? e.bias[col] : 0.f;
+      const float sc = (cv && e.scale) ? e.scale[col] : 1.f;
+      const float sh = (cv && e.scale) ? e.shift[col] : 0.f;
+#pragma unroll
+      for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = wm * (BM / WM) + tm * 16 + g * 4 + j;
+          float x = acc[tm][tn][j] + bias;
+          if (e.act == ACT_LEAKY) x = x > 0.f ? x : x * e.slope;
+          x = cv ? x * sc + sh : 0.f;
+          Hs[row * BN + 8 * ((col >> 3) ^ (row & 15)) + (col & 7)] = (_Float16)x;
+        }
+    }
+    __syncthreads();
+    f4 hacc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) hacc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    const _Float16* hw = (const _Float16*)a.head_w;  // [32][128]
+#pragma unroll
+    for (int ks = 0; ks < BN / 32; ++ks) {
+      h8 af[2], bf[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int row = 32 * wid + 16 * t + fr;
+        af[t] = *(const h8*)(Hs + row * BN + 8 * ((4 * ks + g) ^ (row & 15)));
+        bf[t] = *(const h8*)(hw + (16 * t + fr) * BN + 32 * ks + 8 * g);
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tq = 0; tq < 2; ++tq)
+          hacc[tm][tq] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[tm], bf[tq], hacc[tm][tq], 0, 0, 0);
+    }
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+      for (int tq = 0; tq < 2; ++tq) {
+        const int c = 16 * tq + fr;
+        if (c < a.head_cout) head_epi4(a, m_base + 32 * wid + 16 * tm + 4 * g, c, hacc[tm][tq]);
+      }
+    return;
+  }
+
   // ---- epilogue: accumulators -> LDS C tile (fp32) -> 4 rows x 8 channels per thread ----
   float* Cs = reinterpret_cast<float*>(smem_raw);
   const int rq = g * 4;
@@ -284,7 +371,12 @@ bool conv_pipe_ok(const ConvArgs& a) {
   if (a.cin % 64 != 0 || a.cout_pad % kPBN != 0 || (a.ks != 1 && a.ks != 3)) return false;
   if (a.kpad != a.ks * a.ks * a.cin) return false;
   const int64_t elems = (int64_t)a.n * a.ih * a.iw * a.in_cs;
-  return elems < (1ll << 30) && (int64_t)a.cout_pad * a.kpad * 2 < (1ll << 31);
+  if (elems >= (1ll << 30) || (int64_t)a.cout_pad * a.kpad * 2 >= (1ll << 31)) return false;
+  if (a.head_w) {  // fused head: one N tile, head K = 128, output only through the head
+    if (a.cout_pad != kPBN || a.head_cout < 1 || a.head_cout > 32 || !a.head_e.io || !a.head_e.bias) return false;
+    if (a.e.full.ptr || a.e.pool.ptr || a.e.up.ptr || a.e.res.ptr || a.e.io || a.quad) return false;
+  }
+  return true;
 }
 
 // mode (conv_pipe_mode): 1 = the kernel; 2..5 = ablation builds for diagnostics
@@ -294,6 +386,10 @@ void launch_conv_pipe(const ConvArgs& a, hipStream_t s) {
   const int64_t nblk = (int64_t)((a.M + kPBM - 1) / kPBM) * (a.cout_pad / kPBN);
   RTDM_REQUIRE(nblk < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
   const dim3 grid((unsigned)nblk);
+  if (a.head_w) {
+    hipLaunchKernelGGL((conv_pipe_f16<8>), grid, dim3(512), 0, s, a);
+    return;
+  }
   switch (conv_pipe_mode()) {
     case 2: hipLaunchKernelGGL((conv_pipe_f16<1>), grid, dim3(512), 0, s, a); break;
     case 3: hipLaunchKernelGGL((conv_pipe_f16<2>), grid, dim3(512), 0, s, a); break;

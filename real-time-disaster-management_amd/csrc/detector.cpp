@@ -108,6 +108,14 @@ struct Step {
   int full_t = -1, pool_t = -1, up_t = -1, res_t = -1;
   int yolo = -1;  // index into yolo heads
   bool quad = false;
+  // fused 1x1 head conv (layer + 1) feeding a [yolo] (layer + 2): conv_pipe_f16 head
+  // epilogue; this conv's own output is not materialised
+  bool head = false;
+  int head_cout = 0, head_act = ACT_LINEAR;
+  bool head_bn = false;
+  const float *h_beta = nullptr, *h_gamma = nullptr, *h_mean = nullptr, *h_var = nullptr, *h_bias = nullptr,
+              *h_W = nullptr;
+  PackedConv hpc;
   bool bn = false;  // raw darknet weights (host), packed after planning
   const float *w_beta = nullptr, *w_gamma = nullptr, *w_mean = nullptr, *w_var = nullptr, *w_bias = nullptr,
               *w_W = nullptr;
@@ -151,6 +159,10 @@ struct rtdm_detector_s {
 };
 
 namespace rtdm {
+
+static int g_fuse_head = 1;
+int fuse_head() { return g_fuse_head; }
+void set_fuse_head(int v) { g_fuse_head = v ? 1 : 0; }
 
 static size_t esize_of(int dtype) { return dtype == RTDM_F16 ? 2 : 4; }
 
@@ -310,6 +322,64 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
           h.layer_tensor[i] = -1;        // the pre-add conv output is never materialised
           h.layer_tensor[i + 1] = full;  // conv output with the residual added
           need_full = !consumers[i + 1].empty();
+        } else if (f16 && fuse_head() && nx.type == "convolutional" && only_next && i + 2 < L && defs[i + 2].type == "yolo" &&
+                   consumers[i + 1].size() == 1 && consumers[i + 1][0] == i + 2 && consumers[i + 2].empty() &&
+                   nx.i("size", 1) == 1 && nx.i("stride", 1) == 1 && nx.i("groups", 1) == 1 &&
+                   nx.i("filters", 0) <= 32 && filters > 64 && filters <= 128 &&
+                   s.cin % 64 == 0 && (size == 1 || size == 3) &&
+                   (nx.str("activation", "linear") == "linear" || nx.str("activation", "linear") == "leaky")) {
+          // conv -> 1x1 head conv -> YOLOLayer (models.py:185-258): the head GEMM and the
+          // decode run in this conv's epilogue (conv_pipe_f16 head variant)
+          const int hf = nx.i("filters", 0);
+          const int hbn = nx.i("batch_normalize", 0);
+          s.head = true;
+          s.head_cout = hf;
+          s.head_act = nx.str("activation", "linear") == "leaky" ? ACT_LEAKY : ACT_LINEAR;
+          s.head_bn = hbn != 0;
+          if (hbn) {
+            s.h_beta = take_w(hf);
+            s.h_gamma = take_w(hf);
+            s.h_mean = take_w(hf);
+            s.h_var = take_w(hf);
+          } else {
+            s.h_bias = take_w(hf);
+          }
+          s.h_W = take_w((int64_t)hf * filters);
+          h.flop += 2.0 * s.oh * s.ow * (double)hf * filters;
+          const CfgBlock& yb = defs[i + 2];
+          YoloHead yh;
+          yh.layer = i + 2;
+          const std::vector<int> mask = yb.ints("mask");
+          const std::vector<double> anc = yb.floats("anchors");
+          const int ncls = yb.i("classes", 0);
+          yh.na = (int)mask.size();
+          yh.no = ncls + 5;
+          yh.ny = s.oh;
+          yh.nx = s.ow;
+          RTDM_REQUIRE(yh.na > 0 && yh.na <= 8, RTDM_E_UNSUPPORTED, "cfg: yolo with more than 8 anchors");
+          RTDM_REQUIRE(hf == yh.na * yh.no, RTDM_E_INVALID,
+                       "cfg: yolo head conv has " + std::to_string(hf) + " filters, expected na*(nc+5)");
+          RTDM_REQUIRE(nc_all < 0 || nc_all == ncls, RTDM_E_UNSUPPORTED, "cfg: yolo heads disagree on classes");
+          nc_all = ncls;
+          const double isz = std::max(h.img_h, h.img_w);
+          const double ystride = isz / (double)std::max(s.oh, s.ow);
+          yh.ystride = (float)ystride;
+          for (int a : mask) {
+            RTDM_REQUIRE(2 * a + 1 < (int)anc.size(), RTDM_E_INVALID, "cfg: yolo mask out of range");
+            yh.anchor_vec.push_back((float)anc[2 * a] / (float)ystride);
+            yh.anchor_vec.push_back((float)anc[2 * a + 1] / (float)ystride);
+          }
+          yh.io_off = h.n_anchors_total;
+          h.n_anchors_total += yh.na * yh.ny * yh.nx;
+          s.yolo = (int)h.heads.size();
+          h.heads.push_back(yh);
+          const int ht = new_tensor(hf, s.oh, s.ow, "conv" + std::to_string(i + 1));
+          fused[i + 1] = true;
+          fused[i + 2] = true;
+          h.layer_tensor[i] = -1;
+          h.layer_tensor[i + 1] = ht;  // never materialised: only the decoded io leaves the kernel
+          h.layer_tensor[i + 2] = ht;
+          need_full = false;
         } else if (nx.type == "yolo" && only_next) {
           // YOLOLayer (models.py:185-258) fused into this head conv
           YoloHead yh;
@@ -345,6 +415,11 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         }
       }
       h.tensors[full].materialised = need_full || (s.pool_t < 0 && s.up_t < 0 && s.yolo < 0);
+      if (s.head) {
+        // shape bookkeeping continues from the head conv's output (layer i+2 = yolo)
+        cur_c = s.head_cout;
+        cur_t = h.layer_tensor[i + 1];
+      }
       if (!h.tensors[full].materialised) s.full_t = -1;
       if (s.quad && h.tensors[full].materialised) {
         RTDM_REQUIRE(s.oh % 2 == 0 && s.ow % 2 == 0, RTDM_E_INVALID, "internal: quad with odd full output");
@@ -509,6 +584,22 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       }
       st.pc = pack_conv(blob, st.w_W, filters, st.cin, size, st.bn ? sc.data() : nullptr, use_mfma);
       st.pc.b_off = blob.add_f32(b);
+      if (st.head) {
+        std::vector<double> hsc(st.head_cout, 1.0);
+        std::vector<float> hb(st.head_cout);
+        for (int o = 0; o < st.head_cout; ++o) {
+          if (st.head_bn) {
+            hsc[o] = (double)st.h_gamma[o] / std::sqrt((double)st.h_var[o] + 1e-4);
+            hb[o] = (float)((double)st.h_beta[o] - (double)st.h_mean[o] * hsc[o]);
+          } else {
+            hb[o] = st.h_bias[o];
+          }
+        }
+        // [cout_pad(32)][kpad(128)] fp16, k = input channel: the head GEMM's B operand
+        st.hpc = pack_conv(blob, st.h_W, st.head_cout, filters, 1, st.head_bn ? hsc.data() : nullptr, true);
+        st.hpc.b_off = blob.add_f32(hb);
+        RTDM_REQUIRE(st.hpc.kpad == 128 && st.hpc.cout_pad == 32, RTDM_E_INVALID, "internal: head packing");
+      }
       if (stem) st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr);
     } else {
       st.pc.cout = filters;
@@ -520,6 +611,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       if (stem) st.pc.stem_off = 0;  // planning only: marks the stem kernel for step_info
     }
     st.w_beta = st.w_gamma = st.w_mean = st.w_var = st.w_bias = st.w_W = nullptr;
+    st.h_beta = st.h_gamma = st.h_mean = st.h_var = st.h_bias = st.h_W = nullptr;
   }
   for (YoloHead& y : h.heads) y.anchor_off = blob.add_f32(y.anchor_vec);
   if (weights) {
@@ -602,7 +694,21 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       a.e.pool = tensor_view(h, st.pool_t);
       a.e.up = tensor_view(h, st.up_t);
       a.e.res = tensor_view(h, st.res_t);
-      if (st.yolo >= 0) {
+      if (st.head) {
+        const YoloHead& y = h.heads[st.yolo];
+        a.head_w = h.blob.at<void>(st.hpc.w_off);
+        a.head_cout = st.head_cout;
+        a.head_e.bias = h.blob.at<float>(st.hpc.b_off);
+        a.head_e.act = st.head_act;
+        a.head_e.slope = 0.1f;
+        a.head_e.io = io;
+        a.head_e.io_rows = h.n_anchors_total;
+        a.head_e.io_off = y.io_off;
+        a.head_e.na = y.na;
+        a.head_e.no = y.no;
+        a.head_e.ystride = y.ystride;
+        a.head_e.anchor_vec = h.blob.at<float>(y.anchor_off);
+      } else if (st.yolo >= 0) {
         const YoloHead& y = h.heads[st.yolo];
         a.e.io = io;
         a.e.io_rows = h.n_anchors_total;
@@ -670,16 +776,24 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     a.e.pool = view_geom(h, st.pool_t);
     a.e.up = view_geom(h, st.up_t);
     a.e.res = view_geom(h, st.res_t);
-    if (st.yolo >= 0) a.e.io = (float*)64;
+    if (st.head) {
+      a.head_w = (const void*)64;
+      a.head_cout = st.head_cout;
+      a.head_e.io = (float*)64;
+      a.head_e.bias = (const float*)64;
+    } else if (st.yolo >= 0) {
+      a.e.io = (float*)64;
+    }
     name = conv_kernel_name(a, h.dtype);
-    flop = 2.0 * st.oh * st.ow * (double)st.cout * st.cin * st.ks * st.ks;
+    flop = 2.0 * st.oh * st.ow * (double)st.cout * st.cin * st.ks * st.ks +
+           (st.head ? 2.0 * st.oh * st.ow * (double)st.head_cout * st.cout : 0.0);
     double out = 0;
     if (st.full_t >= 0) out += (double)st.oh * st.ow * st.cout;
     if (st.pool_t >= 0) out += (double)(st.oh / 2) * (st.ow / 2) * st.cout;
     if (st.up_t >= 0) out += 4.0 * st.oh * st.ow * st.cout;
     if (st.res_t >= 0) out += (double)st.oh * st.ow * st.cout;
     const double in = (double)st.ih * st.iw * st.cin * (st.in_t < 0 ? 1.0 / es : 1.0);
-    bytes = (in + out) * es + (st.yolo >= 0 ? (double)st.oh * st.ow * st.cout * 4.0 : 0.0);
+    bytes = (in + out) * es + (st.yolo >= 0 ? (double)st.oh * st.ow * (st.head ? st.head_cout : st.cout) * 4.0 : 0.0);
   } else if (st.kind == ST_MAXPOOL) {
     name = "maxpool_kernel";
     flop = 0;
@@ -711,6 +825,7 @@ static std::string describe(const rtdm_detector_s& h) {
       o << "conv" << st.ks << "x" << st.ks << "/" << st.stride << " " << st.cin << "->" << st.cout << " "
         << (st.pc.mfma ? "mfma" : "valu") << (st.quad ? " quad" : "") << " in=" << (st.in_t < 0 ? "input" : tn(st.in_t))
         << " full=" << tn(st.full_t) << " pool=" << tn(st.pool_t) << " up=" << tn(st.up_t) << " res=" << tn(st.res_t);
+      if (st.head) o << " head1x1->" << st.head_cout;
       if (st.yolo >= 0) o << " yolo" << st.yolo << "(off " << h.heads[st.yolo].io_off << ")";
     } else if (st.kind == ST_MAXPOOL) {
       o << "maxpool k" << st.k << " s" << st.s << (st.zero_rb ? " zeropad" : "") << " " << tn(st.in_t) << " -> "

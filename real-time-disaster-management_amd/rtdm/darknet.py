@@ -170,6 +170,14 @@ class Darknet(torch.nn.Module):
             L.check(L.lib().rtdm_detect(h, L.ptr(x), kind, n, L.ptr(out), L.stream_ptr(stream)))
         return out, None
 
+    def describe(self) -> str:
+        """Text dump of the launch plan (steps, fusions, buffers) of the current handle."""
+        h = self._handle if self._handle is not None else self.handle(1)
+        need = L.lib().rtdm_detector_describe(h, None, 0)
+        buf = ctypes.create_string_buffer(int(need) + 1)
+        L.lib().rtdm_detector_describe(h, buf, len(buf))
+        return buf.value.decode()
+
     def layer_output(self, layer: int, n: int) -> torch.Tensor:
         """NCHW fp32 copy of cfg layer `layer`'s output from the last forward (debug/parity)."""
         h = self._handle

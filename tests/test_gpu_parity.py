@@ -212,6 +212,26 @@ def test_detector_golden_full(dev, det_golden, case, half):
         assert matched / len(ref) >= (0.9 if half else 0.99), (case, matched, len(ref))
 
 
+@pytest.mark.parametrize("size", [608, 256])
+def test_detector_fused_head_matches_unfused(dev, size):
+    """conv -> 1x1 head -> [yolo] fused into one conv_pipe_f16 launch gives the same
+    io bits as the separate head conv (same fp16 activations, same MFMA K order)."""
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    x = torch.from_numpy(synth_frames(3, size, size, seed=11)).to(dev)
+    outs = {}
+    try:
+        for fuse in (0, 1):
+            L.check(L.lib().rtdm_set_tuning(b"fuse_head", fuse))
+            m, _, _ = _darknet("yolov4-tiny-aider-416", size, True)
+            io, _ = m(x)
+            assert ("head1x1" in m.describe()) == bool(fuse)
+            outs[fuse] = io.cpu()
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"fuse_head", 1))
+    assert torch.equal(outs[0], outs[1])
+
+
 def _iou(a, b):
     iw = np.clip(np.minimum(a[2], b[:, 2]) - np.maximum(a[0], b[:, 0]), 0, None)
     ih = np.clip(np.minimum(a[3], b[:, 3]) - np.maximum(a[1], b[:, 1]), 0, None)
