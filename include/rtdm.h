@@ -110,7 +110,9 @@ const char* rtdm_build_arch(void);
  * defaults are the tuned choice).  key "conv_pipe": 1 = pipelined 256x128
  * implicit GEMM for Cin%64==0 convs (default), 0 = conv_glds_f16 128x128;
  * key "fuse_head": 1 = conv -> 1x1 head conv -> [yolo] planned as one launch
- * (default), 0 = separate head conv.  Take effect for handles created afterwards. */
+ * (default), 0 = separate head conv (takes effect for handles created
+ * afterwards); key "acff_persist": 1 = persistent ACFF kernel for the large
+ * classifier maps (default), 0 = 8x8-tile fused ACFF kernel (at launch).        */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 
 /* ---- classifier ------------------------------------------------------------ */

@@ -25,11 +25,14 @@
 //            lane's 4 accumulator rows are one quad and the pool is in-lane.
 #include "common.h"
 
+#include <algorithm>
+
 namespace rtdm {
 
 namespace {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 8;              // output tile side
 constexpr int kHalo = kTile + 6;      // staged input tile side
@@ -225,6 +228,335 @@ __global__ __launch_bounds__(256) void acff_fused(AcffArgs a) {
       }
     }
   }
+}
+
+// --------------------------------------------------------------------------
+// acff_persist: the same block for the large-map ACFF layers (ErNET acff1..3,
+// Squeeze acff1..3), built for throughput:
+//   * persistent blocks (occupancy-sized grid) walk (tile, channel chunk) work
+//     items; the next item's input halo is prefetched into registers while the
+//     current one is computed (double-buffered LDS halo);
+//   * 8 x 16 output tiles (halo 14 x 22: 2.4x input reads per output instead of
+//     3x for 8 x 8);
+//   * depthwise: one wave owns an 8-channel group for 64 pixels (lane = pixel),
+//     so the 27 tap weights of a branch are wave-uniform scalar loads (SGPR
+//     operands of the FMAs), inputs one ds_read_b128 per tap;
+//   * the 1x1 GEMM accumulates over channel chunks of CC channels: K order
+//     (chunk, branch, channel) — weights repacked host-side to match — on
+//     v_mfma_f32_16x16x32_f16, B fragments straight from global (L2-resident).
+// Tile pixels are in 2x2-quad order, so the pooled epilogue stays in-lane.
+// --------------------------------------------------------------------------
+struct AcffPArgs {
+  const _Float16* in;
+  int in_cs, in_co;
+  int n, h, w, cin;
+  int lim_h, lim_w;
+  const float* dw_wt;   // [3][9][cin]
+  const float* dw_b;    // [3][cin]
+  const _Float16* pw;   // [cout_pad][nch * KC], k = chunk*KC + branch*CC + c
+  int cout, cout_pad;
+  const float* bias;
+  const float* scale;
+  const float* shift;
+  float slope;
+  _Float16* out;
+  int out_cs, pool;
+};
+
+// Wave-uniform reads through the constant address space become scalar loads
+// (SGPR operands of the depthwise FMAs).
+typedef const __attribute__((address_space(4))) float* cfloat_p;
+
+template <int CC>
+struct AcffPGeom {
+  static constexpr int TH = 8, TW = 16, HH = TH + 6, HW = TW + 6, NPIX = TH * TW;
+  static constexpr int PS = CC + 8;                    // halo pixel stride (halfs)
+  static constexpr int CG = CC / 8;                    // 8-channel groups per chunk
+  static constexpr int KC = (3 * CC + 31) / 32 * 32;   // K per chunk (zero-padded)
+  static constexpr int AS = KC + 8;                    // A-tile row stride (halfs)
+  static constexpr int HALO = HH * HW * CG;            // 16-byte vectors per halo chunk
+  static constexpr int PV = (HALO + 255) / 256;        // prefetch registers per thread
+  static constexpr int XS = HH * HW * PS;              // halfs per halo buffer
+};
+
+// fp32 = w (SGPR f32) * x (f16, low / high half of a packed pair) + acc, exact like
+// cvt + fma but one VOP3P instruction.
+__device__ __forceinline__ float fma_mix_lo(float w, uint32_t x2, float acc) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(d) : "s"(w), "v"(x2), "v"(acc));
+  return d;
+}
+__device__ __forceinline__ float fma_mix_hi(float w, uint32_t x2, float acc) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "s"(w), "v"(x2), "v"(acc));
+  return d;
+}
+
+template <int CC, int NF, int ABL = 0>  // ABL (diagnostics, wrong outputs): 1 no taps, 2 no GEMM
+__global__ __launch_bounds__(256, 2) void acff_persist(AcffPArgs a) {
+  using G = AcffPGeom<CC>;
+  constexpr int TH = G::TH, TW = G::TW, HW = G::HW, PS = G::PS, CG = G::CG, KC = G::KC, AS = G::AS;
+  constexpr int HALO = G::HALO, PV = G::PV, XS = G::XS;
+  __shared__ __attribute__((aligned(16))) _Float16 xs[2 * XS];
+  __shared__ __attribute__((aligned(16))) _Float16 At[G::NPIX * AS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, g = lane >> 4;
+  const int oh = a.h - 2, ow = a.w - 2;
+  const int tiles_x = (a.lim_w + TW - 1) / TW, tiles_y = (a.lim_h + TH - 1) / TH;
+  const int ntiles = a.n * tiles_x * tiles_y;
+  const int nch = a.cin / CC;
+  const int ktot = nch * KC;
+  if (KC > 3 * CC) {  // zero K padding of the A tile (never overwritten)
+    constexpr int padw = KC - 3 * CC;
+    for (int i = tid; i < G::NPIX * padw; i += 256) At[(i / padw) * AS + 3 * CC + i % padw] = (_Float16)0.f;
+  }
+  const _Float16* __restrict__ in = a.in + a.in_co;
+  // work item j of this block: tile blockIdx.x + (j / nch) * gridDim.x, channel chunk j % nch
+  auto item_tile = [&](int j) { return (int)blockIdx.x + (j / nch) * (int)gridDim.x; };
+  auto prefetch = [&](u32x4(&pre)[PV], int j) {
+    const int tile = item_tile(j), ch = j % nch;
+    const int tx = tile % tiles_x, t1 = tile / tiles_x;
+    const int ty = t1 % tiles_y, n = t1 / tiles_y;
+#pragma unroll
+    for (int k = 0; k < PV; ++k) {
+      const int i = tid + 256 * k;
+      const int pix = i / CG, v = i - pix * CG;
+      const int r = pix / HW, c = pix - r * HW;
+      const int y = ty * TH - 2 + r, x = tx * TW - 2 + c;
+      u32x4 d = {0u, 0u, 0u, 0u};
+      if (i < HALO && (unsigned)y < (unsigned)a.h && (unsigned)x < (unsigned)a.w)
+        d = *(const u32x4*)(in + ((size_t)(n * a.h + y) * a.w + x) * a.in_cs + ch * CC + v * 8);
+      pre[k] = d;
+    }
+  };
+  auto stage = [&](const u32x4(&pre)[PV], _Float16* xb) {
+#pragma unroll
+    for (int k = 0; k < PV; ++k) {
+      const int i = tid + 256 * k;
+      if (i < HALO) {
+        const int pix = i / CG, v = i - pix * CG;
+        *(u32x4*)(xb + pix * PS + v * 8) = pre[k];
+      }
+    }
+  };
+  const int wm = wid >> 1, wn = wid & 1;
+  f4 acc[4][NF];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jn = 0; jn < NF; ++jn) acc[i][jn] = f4{0.f, 0.f, 0.f, 0.f};
+  h8 bf[KC / 32][NF];
+  int bf_ch = -1;
+  // 1x1 weight fragments of item j's chunk (global, L2-resident; once when nch == 1).
+  // Issued BEFORE the halo prefetch of j+2: vmcnt retires in order, so waiting for
+  // these never waits for the prefetch.
+  auto load_bf = [&](int j) {
+    const int ch = j % nch;
+    if (ch == bf_ch) return;
+#pragma unroll
+    for (int ks = 0; ks < KC / 32; ++ks)
+#pragma unroll
+      for (int tn = 0; tn < NF; ++tn)
+        bf[ks][tn] = *(const h8*)(a.pw + (size_t)(wn * NF * 16 + tn * 16 + fr) * ktot + ch * KC + ks * 32 + g * 8);
+    bf_ch = ch;
+  };
+  // epilogue constants of this lane's channels, hoisted out of the item loop (a load
+  // in the loop would wait for the in-flight prefetch)
+  float e_b[NF], e_s[NF], e_t[NF];
+  bool e_ok[NF];
+#pragma unroll
+  for (int tn = 0; tn < NF; ++tn) {
+    const int c = wn * NF * 16 + tn * 16 + fr;
+    const bool cv = c < a.cout;
+    e_ok[tn] = cv;
+    e_b[tn] = cv ? a.bias[c] : 0.f;
+    e_s[tn] = (cv && a.scale) ? a.scale[c] : 1.f;
+    e_t[tn] = (cv && a.scale) ? a.shift[c] : 0.f;
+  }
+
+  auto process = [&](int j, const _Float16* xb) {
+    const int tile = item_tile(j), ch = j % nch;
+    // ---- depthwise branches -> A tile (fp16) ----
+#pragma unroll
+    for (int u0 = 0; u0 < 2 * CG; u0 += 4) {
+      const int u = u0 + wid;
+      if (u < 2 * CG) {
+        const int cg = u % CG, pb = u / CG;
+        const int m = pb * 64 + lane;
+        const int q = m >> 2, dq = m & 3;
+        const int py = 2 * (q >> 3) + (dq >> 1), px = 2 * (q & 7) + (dq & 1);
+        const int cbase = ch * CC + cg * 8;
+#pragma unroll
+        for (int br = 0; br < 3; ++br) {
+          const int d = br + 1;
+          const cfloat_p bp = (cfloat_p)(a.dw_b + br * a.cin + cbase);
+          float s8[8];
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) s8[jj] = bp[jj];
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+              if constexpr ((ABL & 1) != 0) continue;
+              const int hr = py + 3 + (kh - 1) * d, hc = px + 3 + (kw - 1) * d;
+              const u32x4 xv = *(const u32x4*)(xb + (hr * HW + hc) * PS + cg * 8);
+              const cfloat_p wp = (cfloat_p)(a.dw_wt + (size_t)(br * 9 + kh * 3 + kw) * a.cin + cbase);
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj) {
+                s8[2 * jj] = fma_mix_lo(wp[2 * jj], xv[jj], s8[2 * jj]);
+                s8[2 * jj + 1] = fma_mix_hi(wp[2 * jj + 1], xv[jj], s8[2 * jj + 1]);
+              }
+            }
+          h8 o;
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) o[jj] = (_Float16)s8[jj];
+          *(h8*)(At + m * AS + br * CC + cg * 8) = o;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- 1x1 GEMM over this chunk: [128 px x KC] x [KC x cout_pad] ----
+#pragma unroll
+    for (int ks = 0; ks < ((ABL & 2) ? 0 : KC / 32); ++ks) {
+      h8 af[4];
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm) af[tm] = *(const h8*)(At + (wm * 64 + tm * 16 + fr) * AS + ks * 32 + g * 8);
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < NF; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[tm], bf[ks][tn], acc[tm][tn], 0, 0, 0);
+    }
+    if (ch == nch - 1) {
+      // ---- epilogue: bias -> LeakyReLU (0 < slope < 1: max(x, slope x)) -> BN affine ->
+      //      (2x2 max) -> fp16; 32-bit offsets from a per-image base ----
+      const int tx = tile % tiles_x, t1 = tile / tiles_x;
+      const int ty = t1 % tiles_y, n = t1 / tiles_y;
+      const int oy0 = ty * TH, ox0 = tx * TW;
+      const int ohp = oh >> 1, owp = ow >> 1;
+      _Float16* outn = a.out + (size_t)n * (a.pool ? ohp * owp : oh * ow) * a.out_cs + wn * NF * 16 + fr;
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm) {
+        const int qd = (wm * 64 + tm * 16 + g * 4) >> 2;
+        const int qy = qd >> 3, qx = qd & 7;
+        float v[NF][4];
+#pragma unroll
+        for (int tn = 0; tn < NF; ++tn)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = acc[tm][tn][r] + e_b[tn];
+            v[tn][r] = fmaxf(x, x * a.slope) * e_s[tn] + e_t[tn];
+          }
+        if (a.pool) {
+          const int py = (oy0 >> 1) + qy, px = (ox0 >> 1) + qx;
+          if (2 * py < a.lim_h && 2 * px < a.lim_w) {
+            _Float16* o = outn + (py * owp + px) * a.out_cs;
+#pragma unroll
+            for (int tn = 0; tn < NF; ++tn)
+              if (e_ok[tn]) o[tn * 16] = (_Float16)fmaxf(fmaxf(v[tn][0], v[tn][1]), fmaxf(v[tn][2], v[tn][3]));
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int y = oy0 + 2 * qy + (r >> 1), x = ox0 + 2 * qx + (r & 1);
+            if (y < a.lim_h && x < a.lim_w) {
+              _Float16* o = outn + (y * ow + x) * a.out_cs;
+#pragma unroll
+              for (int tn = 0; tn < NF; ++tn)
+                if (e_ok[tn]) o[tn * 16] = (_Float16)v[tn][r];
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NF; ++jn) acc[i][jn] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  // two register prefetch sets: item j+2's halo is in flight while item j computes
+  u32x4 preA[PV], preB[PV];
+  auto valid = [&](int j) { return item_tile(j) < ntiles; };
+  if (valid(0)) prefetch(preA, 0);
+  if (valid(1)) prefetch(preB, 1);
+  for (int j = 0; valid(j); ++j) {
+    stage(preA, xs);
+    __syncthreads();
+    load_bf(j);
+    if (valid(j + 2)) prefetch(preA, j + 2);
+    process(j, xs);
+    ++j;
+    if (!valid(j)) break;
+    stage(preB, xs + XS);
+    __syncthreads();
+    load_bf(j);
+    if (valid(j + 2)) prefetch(preB, j + 2);
+    process(j, xs + XS);
+  }
+}
+
+static int g_acff_persist = 1;
+int acff_persist_mode() { return g_acff_persist; }
+void set_acff_persist_mode(int v) { g_acff_persist = v < 0 ? 0 : v; }
+
+// Channel chunk of the persistent kernel for cin (0 = not eligible).
+int acff_persist_chunk(int cin, int cout_pad, int oh) {
+  if (cout_pad != 64 && cout_pad != 128) return 0;
+  if (oh < 24) return 0;  // small maps: 8 x 16 tiles would mostly idle
+  // 16-channel chunks for every cin: (CC = 32 chunks need ~40 more VGPRs and spill)
+  return cin % 16 == 0 ? 16 : 0;
+}
+
+void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int w, int cin, int lim_h, int lim_w,
+                         const float* dw_wt, const float* dw_b, const void* pwc, int cout, int cout_pad,
+                         const float* bias, const float* scale, const float* shift, float slope, void* out, int out_cs,
+                         int pool, hipStream_t s) {
+  const int cc = acff_persist_chunk(cin, cout_pad, h - 2);
+  RTDM_REQUIRE(cc > 0, RTDM_E_INVALID, "acff_persist: unsupported shape");
+  RTDM_REQUIRE((in_cs % 8) == 0 && (in_co % 8) == 0, RTDM_E_INVALID, "acff_persist: input view not 16-byte aligned");
+  RTDM_REQUIRE(!pool || ((lim_h | lim_w) & 1) == 0, RTDM_E_INVALID, "acff_persist: odd pooled limit");
+  AcffPArgs a;
+  a.in = (const _Float16*)in;
+  a.in_cs = in_cs;
+  a.in_co = in_co;
+  a.n = n;
+  a.h = h;
+  a.w = w;
+  a.cin = cin;
+  a.lim_h = lim_h;
+  a.lim_w = lim_w;
+  a.dw_wt = dw_wt;
+  a.dw_b = dw_b;
+  a.pw = (const _Float16*)pwc;
+  a.cout = cout;
+  a.cout_pad = cout_pad;
+  a.bias = bias;
+  a.scale = scale;
+  a.shift = shift;
+  a.slope = slope;
+  a.out = (_Float16*)out;
+  a.out_cs = out_cs;
+  a.pool = pool;
+  const int64_t tiles = (int64_t)n * ((lim_h + 7) / 8) * ((lim_w + 15) / 16);
+  if (tiles <= 0) return;
+  RTDM_REQUIRE(tiles < (1ll << 31), RTDM_E_CAPACITY, "acff_persist: too many tiles");
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  auto go = [&](auto kern) {
+    int per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cus);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  };
+  const int abl = acff_persist_mode() - 1;  // >1: diagnostic ablations
+  if (cc == 16) {
+    if (abl == 1) cout_pad == 64 ? go(acff_persist<16, 2, 1>) : go(acff_persist<16, 4, 1>);
+    else if (abl == 2) cout_pad == 64 ? go(acff_persist<16, 2, 2>) : go(acff_persist<16, 4, 2>);
+    else cout_pad == 64 ? go(acff_persist<16, 2>) : go(acff_persist<16, 4>);
+  }
+  RTDM_HIP(hipGetLastError());
 }
 
 // Largest staging chunk (32 / 16 / 8 channels) whose LDS footprint fits 64 KiB; 0 if none.

@@ -21,6 +21,8 @@ struct AcffStage {
   size_t dw_w = 0, dw_b = 0;            // [3][cin][9], [3][cin]
   size_t dw_wt = 0;                     // [3][9][cin] (tap-major copy for the fused kernel)
   bool fused = false;                   // fp16 fused ACFF kernel (acff.hip)
+  int persist_cc = 0;                   // acff_persist channel chunk (0 = acff_fused)
+  size_t pwc_off = 0;                   // 1x1 weights in (chunk, branch, channel) K order
   PackedConv pw;                        // fused 1x1 conv
   size_t d_buf = 0, out_buf = 0;        // arena offsets (elements) per image
   int oh = 0, ow = 0;                   // dw/1x1 output geometry
@@ -189,6 +191,19 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
     st.pw = pack_conv(blob, fw, sp.cout, 3 * sp.cin, 1, nullptr, f16);
     st.pw.b_off = blob.add(fb, sizeof(float) * sp.cout);
     st.fused = f16 && acff_fused_ok(sp.cin, st.pw.cout_pad, st.pw.kpad);
+    if (st.fused && !(sp.red && sp.red_before_pool)) st.persist_cc = acff_persist_chunk(sp.cin, st.pw.cout_pad, st.oh);
+    if (st.persist_cc) {
+      // [cout_pad][nch * KC] fp16, k = chunk*KC + branch*CC + c (zero K/row padding)
+      const int CCk = st.persist_cc, nch = sp.cin / CCk, KC = (3 * CCk + 31) / 32 * 32;
+      std::vector<_Float16> wc((size_t)st.pw.cout_pad * nch * KC, (_Float16)0.f);
+      for (int o = 0; o < sp.cout; ++o)
+        for (int chk = 0; chk < nch; ++chk)
+          for (int br = 0; br < 3; ++br)
+            for (int cl = 0; cl < CCk; ++cl)
+              wc[(size_t)o * nch * KC + chk * KC + br * CCk + cl] =
+                  (_Float16)fw[(size_t)o * 3 * sp.cin + br * sp.cin + chk * CCk + cl];
+      st.pwc_off = blob.add(wc.data(), wc.size() * sizeof(_Float16));
+    }
     st.d_buf = take((size_t)st.oh * st.ow * 3 * sp.cin);
     if (sp.red && sp.red_before_pool) {
       // acff2 -> conv_red2 -> pool2: BN affine folded into conv_red2
@@ -324,6 +339,11 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       const float* sh = st.affine ? h.blob.at<float>(st.pw.t_off) : nullptr;
       const bool pool_here = st.pool && !st.red_pool;
       void* dst = st.red && st.red_pool ? buf(st.mid_buf) : buf(st.out_buf);
+      if (st.persist_cc && acff_persist_mode())
+        launch_acff_persist(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_wt),
+                            h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pwc_off), st.cout, st.pw.cout_pad,
+                            h.blob.at<float>(st.pw.b_off), sc, sh, 0.01f, dst, st.cout, pool_here ? 1 : 0, s);
+      else
       launch_acff_fused(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_wt),
                         h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pw.w_off), st.pw.kpad, st.cout, st.pw.cout_pad,
                         h.blob.at<float>(st.pw.b_off), sc, sh, 0.01f, dst, st.cout, pool_here ? 1 : 0, s);

@@ -213,6 +213,15 @@ void launch_acff_fused(const void* in, int in_cs, int in_co, int n, int h, int w
                        const float* dw_wt /*[3][9][cin]*/, const float* dw_b /*[3][cin]*/, const void* pw, int kpad,
                        int cout, int cout_pad, const float* bias, const float* scale, const float* shift, float slope,
                        void* out, int out_cs, int pool, hipStream_t s);
+// acff.hip: persistent ACFF for the large maps (channel chunk from acff_persist_chunk;
+// pwc = 1x1 weights in (chunk, branch, channel) K order)
+int acff_persist_chunk(int cin, int cout_pad, int oh);
+void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int w, int cin, int lim_h, int lim_w,
+                         const float* dw_wt, const float* dw_b, const void* pwc, int cout, int cout_pad,
+                         const float* bias, const float* scale, const float* shift, float slope, void* out, int out_cs,
+                         int pool, hipStream_t s);
+int acff_persist_mode();
+void set_acff_persist_mode(int v);
 void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, int stride, int pad, int zero_pad_rb,
                     View ov, int oh, int ow, int dtype, hipStream_t s);
 void launch_upsample(View iv, int n, int h, int w, int c, int f, View ov, int dtype, hipStream_t s);
@@ -228,6 +237,8 @@ struct ResizePlan {  // Pillow 8bpc antialiased bilinear, restricted to a center
   int ksize_h = 0, ksize_v = 0;
   int row_first = 0, rows = 0;  // input rows needed by the vertical pass
   int band_rows = 0;            // max input rows of one 16-output-row band (fused kernel)
+  int band_rows8 = 0;           // ... of one 8-output-row band (staged kernel)
+  int col_first = 0, col_end = 0;  // input columns the crop reads
   DevBuf bounds_h, coef_h, bounds_v, coef_v;  // int32 device arrays
 };
 void build_resize_plan(ResizePlan& p, int in_h, int in_w, int out_size, bool upload);

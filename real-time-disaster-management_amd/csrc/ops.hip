@@ -498,6 +498,18 @@ void build_resize_plan(ResizePlan& p, int in_h, int in_w, int out_size, bool upl
   p.row_first = rmin;
   p.rows = rmax - rmin;
   for (int i = 0; i < out_size; ++i) cv[2 * i] -= rmin;
+  p.col_first = 1 << 30;
+  int col_end = 0;
+  for (int i = 0; i < out_size; ++i) {
+    p.col_first = std::min(p.col_first, ch[2 * i]);
+    col_end = std::max(col_end, ch[2 * i] + ch[2 * i + 1]);
+  }
+  p.col_end = col_end;
+  p.band_rows8 = 0;
+  for (int y0 = 0; y0 < out_size; y0 += 8) {  // kResizeBandS
+    const int y1 = std::min(out_size, y0 + 8) - 1;
+    p.band_rows8 = std::max(p.band_rows8, cv[2 * y1] + cv[2 * y1 + 1] - cv[2 * y0]);
+  }
   p.band_rows = 0;
   for (int y0 = 0; y0 < out_size; y0 += 16) {  // kResizeBand
     const int y1 = std::min(out_size, y0 + 16) - 1;
@@ -651,6 +663,90 @@ __global__ __launch_bounds__(256) void resize_fused_kernel(const uint8_t* __rest
   }
 }
 
+// Staged form of the fused kernel (used when each frame row is 16-byte aligned):
+// the band's input rows (only the columns the crop reads) are first copied into
+// LDS with coalesced 16-byte loads, so the horizontal taps read LDS instead of
+// issuing per-byte global loads.  Same integer arithmetic (bit-exact with Pillow).
+constexpr int kResizeBandS = 8;
+
+template <typename T>
+__global__ __launch_bounds__(256) void resize_staged_kernel(const uint8_t* __restrict__ frames, int in_h, int in_w,
+                                                            int row_first, int out, int kh_size, int kv_size,
+                                                            int col_first, int col_bytes16, const int* __restrict__ bh,
+                                                            const int* __restrict__ ch, const int* __restrict__ bv,
+                                                            const int* __restrict__ cv, T* __restrict__ dst, int nchw) {
+  extern __shared__ __attribute__((aligned(16))) int rs_lds[];
+  int* kcoef = rs_lds;                          // [out][kh_size]
+  int* kb = kcoef + out * kh_size;              // [out][2]
+  uint8_t* srow = (uint8_t*)(kb + 2 * out);     // [band input rows][col_bytes16]
+  const int bands = (out + kResizeBandS - 1) / kResizeBandS;
+  const int b = blockIdx.x / bands;
+  const int yy0 = (blockIdx.x - b * bands) * kResizeBandS;
+  const int yy1 = yy0 + kResizeBandS < out ? yy0 + kResizeBandS : out;
+  const int r0 = bv[2 * yy0];
+  const int r1 = bv[2 * (yy1 - 1)] + bv[2 * (yy1 - 1) + 1];
+  const int nrow = r1 - r0;
+  const int c0b = (col_first * 3) & ~15;        // first staged byte of a row (16-aligned)
+  const int delta = col_first * 3 - c0b;
+  const int v16 = col_bytes16 >> 4;
+  const uint8_t* fb = frames + ((size_t)b * in_h + row_first + r0) * in_w * 3 + c0b;
+  for (int i = threadIdx.x; i < nrow * v16; i += 256) {
+    const int r = i / v16, v = i - r * v16;
+    *(uint4*)(srow + (size_t)r * col_bytes16 + v * 16) = *(const uint4*)(fb + (size_t)r * in_w * 3 + v * 16);
+  }
+  for (int i = threadIdx.x; i < out * kh_size; i += 256) kcoef[i] = ch[i];
+  for (int i = threadIdx.x; i < 2 * out; i += 256) kb[i] = bh[i];
+  __syncthreads();
+  uint8_t* tmp = srow + (size_t)nrow * col_bytes16;  // [nrow][out][3]
+  for (int i = threadIdx.x; i < nrow * out; i += 256) {
+    const int r = i / out, xx = i - r * out;
+    const int xmin = kb[2 * xx], xmax = kb[2 * xx + 1];
+    const int* k = kcoef + xx * kh_size;
+    const uint8_t* src = srow + (size_t)r * col_bytes16 + delta + (xmin - col_first) * 3;
+    int s0 = 1 << (kPrecisionBits - 1), s1 = s0, s2 = s0;
+    for (int x = 0; x < xmax; ++x) {
+      const int kx = k[x];
+      s0 += src[x * 3 + 0] * kx;
+      s1 += src[x * 3 + 1] * kx;
+      s2 += src[x * 3 + 2] * kx;
+    }
+    uint8_t* d = tmp + (size_t)i * 3;
+    d[0] = (uint8_t)clip8(s0);
+    d[1] = (uint8_t)clip8(s1);
+    d[2] = (uint8_t)clip8(s2);
+  }
+  __syncthreads();
+  const float mean[3] = {0.485f, 0.456f, 0.406f};
+  const float stdv[3] = {0.229f, 0.224f, 0.225f};
+  for (int i = threadIdx.x; i < (yy1 - yy0) * out; i += 256) {
+    const int yr = i / out, xx = i - yr * out;
+    const int yy = yy0 + yr;
+    const int ymin = bv[2 * yy] - r0, ymax = bv[2 * yy + 1];
+    const int* k = cv + (size_t)yy * kv_size;
+    int acc[3] = {1 << (kPrecisionBits - 1), 1 << (kPrecisionBits - 1), 1 << (kPrecisionBits - 1)};
+    for (int y = 0; y < ymax; ++y) {
+      const uint8_t* t = tmp + ((size_t)(ymin + y) * out + xx) * 3;
+      const int ky = k[y];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) acc[c] += t[c] * ky;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = ((float)clip8(acc[c]) / 255.f - mean[c]) / stdv[c];
+      if (nchw)
+        dst[(((size_t)b * 3 + c) * out + yy) * out + xx] = (T)v;
+      else
+        dst[(((size_t)b * out + yy) * out + xx) * 3 + c] = (T)v;
+    }
+  }
+}
+
+// LDS of the staged kernel: coefficients + bounds + band source rows + band tmp rows.
+static size_t resize_staged_lds(const ResizePlan& p, int col_bytes16) {
+  return (size_t)p.out * p.ksize_h * 4 + (size_t)p.out * 2 * 4 + (size_t)p.band_rows8 * col_bytes16 +
+         (size_t)p.band_rows8 * p.out * 3;
+}
+
 static size_t resize_fused_lds(const ResizePlan& p) {
   return (size_t)p.out * p.ksize_h * 4 + (size_t)p.out * 2 * 4 + (size_t)p.band_rows * p.out * 3;
 }
@@ -658,6 +754,26 @@ static size_t resize_fused_lds(const ResizePlan& p) {
 void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_t* tmp, void* out, int out_layout,
                        int dtype, hipStream_t s) {
   if (n <= 0) return;
+  // staged path: 16-byte aligned frame rows, band fits the LDS budget
+  const int c0b = (p.col_first * 3) & ~15;
+  const int col_bytes16 = (int)round_up((int64_t)p.col_end * 3 - c0b, 16);
+  const bool rows16 = (p.in_w * 3) % 16 == 0 && ((uintptr_t)frames & 15) == 0 &&
+                      c0b + col_bytes16 <= p.in_w * 3;
+  const size_t slds = resize_staged_lds(p, col_bytes16);
+  if (rows16 && slds <= 64 * 1024) {
+    const int blocks = n * ((p.out + kResizeBandS - 1) / kResizeBandS);
+    if (out_layout == 1 || dtype == RTDM_F32)
+      hipLaunchKernelGGL(resize_staged_kernel<float>, dim3(blocks), dim3(256), slds, s, frames, p.in_h, p.in_w,
+                         p.row_first, p.out, p.ksize_h, p.ksize_v, p.col_first, col_bytes16, p.bounds_h.as<int>(),
+                         p.coef_h.as<int>(), p.bounds_v.as<int>(), p.coef_v.as<int>(), (float*)out,
+                         out_layout == 1 ? 1 : 0);
+    else
+      hipLaunchKernelGGL(resize_staged_kernel<_Float16>, dim3(blocks), dim3(256), slds, s, frames, p.in_h, p.in_w,
+                         p.row_first, p.out, p.ksize_h, p.ksize_v, p.col_first, col_bytes16, p.bounds_h.as<int>(),
+                         p.coef_h.as<int>(), p.bounds_v.as<int>(), p.coef_v.as<int>(), (_Float16*)out, 0);
+    RTDM_HIP(hipGetLastError());
+    return;
+  }
   const size_t lds = resize_fused_lds(p);
   if (lds <= 64 * 1024) {
     const int blocks = n * ((p.out + kResizeBand - 1) / kResizeBand);
