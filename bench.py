@@ -258,7 +258,7 @@ def main():
         "pipeline": {"flop_per_frame": pipe_flop,
                      "pipeline_tflops": round(pipe_flop * value / world / 1e12, 2),
                      "pipeline_frac": round(pipe_flop * value / world / 1e12 / MFMA_F16_DENSE_PEAK_TFLOPS, 4),
-                     "detector_ms_per_step": round(det_ms, 4),
+                     "detector_kernel_ms_per_step": round(det_ms, 4),
                      "detections_per_frame": round(float(counts.float().mean()), 2)},
     }
     if rank == 0 and world == 1 and args.cpu_baseline:

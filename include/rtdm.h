@@ -112,7 +112,9 @@ const char* rtdm_build_arch(void);
  * key "fuse_head": 1 = conv -> 1x1 head conv -> [yolo] planned as one launch
  * (default), 0 = separate head conv (takes effect for handles created
  * afterwards); key "acff_persist": 1 = persistent ACFF kernel for the large
- * classifier maps (default), 0 = 8x8-tile fused ACFF kernel (at launch).        */
+ * classifier maps (default), 0 = 8x8-tile fused ACFF kernel (at launch); key
+ * "two_streams": 1 = detector head branches on a side stream (default), 0 = one
+ * stream (takes effect for handles created afterwards).                         */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 
 /* ---- classifier ------------------------------------------------------------ */

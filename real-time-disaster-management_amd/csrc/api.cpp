@@ -29,6 +29,8 @@ rtdm_status rtdm_set_tuning(const char* key, int value) {
       set_conv_pipe_mode(value);
     else if (!strcmp(key, "fuse_head"))
       set_fuse_head(value);
+    else if (!strcmp(key, "two_streams"))
+      set_two_streams_mode(value);
     else if (!strcmp(key, "acff_persist"))
       set_acff_persist_mode(value);
     else

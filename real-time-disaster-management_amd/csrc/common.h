@@ -184,6 +184,9 @@ void set_conv_pipe_mode(int v);
 // detector.cpp: plan conv -> 1x1 head -> [yolo] as one fused launch (default 1)
 int fuse_head();
 void set_fuse_head(int v);
+// detector.cpp: run independent branches (heads) on a second stream (default 1)
+int two_streams_mode();
+void set_two_streams_mode(int v);
 // Kernel symbol (template instantiation) launch_conv will pick for a / dtype.
 const char* conv_kernel_name(const ConvArgs& a, int dtype);
 // Row geometry helpers shared by host planners.

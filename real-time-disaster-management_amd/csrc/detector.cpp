@@ -119,6 +119,10 @@ struct Step {
   bool bn = false;  // raw darknet weights (host), packed after planning
   const float *w_beta = nullptr, *w_gamma = nullptr, *w_mean = nullptr, *w_var = nullptr, *w_bias = nullptr,
               *w_W = nullptr;
+  // two-stream schedule (schedule_streams): stream 0 = the caller's, 1 = the side stream
+  int stream = 0;
+  std::vector<int> deps;    // earlier steps writing a buffer this step reads
+  bool signal = false;      // a step on the other stream waits for this one
   // maxpool / upsample / copy
   int out_t = -1;
   int k = 0, s = 0, p = 0, zero_rb = 0, f = 0;
@@ -149,12 +153,24 @@ struct rtdm_detector_s {
   rtdm::DevBuf arena;
   rtdm::DevBuf zero;  // 256 zero bytes: padding source of the glds conv kernel
   int last_n = 0;
-  // optional per-step timing: events[call][step+1] recorded on the launch stream
+  // optional per-step timing: events[call][2*step + {0,1}] recorded around each step
+  // on the stream it runs on
   bool timing = false;
   int timing_cap = 0, timing_calls = 0;
   std::vector<hipEvent_t> events;
+  // two-stream execution of independent branches (heads): side stream + one
+  // event per signalling step, plus fork / join events
+  bool two_streams = false;
+  hipStream_t side = nullptr;
+  std::vector<hipEvent_t> step_ev;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   ~rtdm_detector_s() {
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : step_ev)
+      if (e) (void)hipEventDestroy(e);
+    if (fork_ev) (void)hipEventDestroy(fork_ev);
+    if (join_ev) (void)hipEventDestroy(join_ev);
+    if (side) (void)hipStreamDestroy(side);
   }
 };
 
@@ -654,12 +670,22 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
     throw Error{RTDM_E_INVALID, "detect: unknown input kind"};
   hipEvent_t* ev = nullptr;
   if (h.timing && h.timing_calls < h.timing_cap) {
-    ev = &h.events[(size_t)h.timing_calls * (h.steps.size() + 1)];
+    ev = &h.events[(size_t)h.timing_calls * 2 * h.steps.size()];
     ++h.timing_calls;
-    RTDM_HIP(hipEventRecord(ev[0], s));
   }
+  const bool two = h.two_streams && h.side;
+  if (two) {  // the side stream starts after everything already queued on s (input, previous call)
+    RTDM_HIP(hipEventRecord(h.fork_ev, s));
+    RTDM_HIP(hipStreamWaitEvent(h.side, h.fork_ev, 0));
+  }
+  hipStream_t s0 = s;
   for (size_t si = 0; si < h.steps.size(); ++si) {
     const Step& st = h.steps[si];
+    s = two && st.stream == 1 ? h.side : s0;
+    if (two)
+      for (int d : st.deps)
+        if (h.steps[d].stream != st.stream) RTDM_HIP(hipStreamWaitEvent(s, h.step_ev[d], 0));
+    if (ev) RTDM_HIP(hipEventRecord(ev[2 * si], s));
     if (st.kind == ST_CONV) {
       ConvArgs a;
       if (st.in_t < 0) {
@@ -733,7 +759,12 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       o.co += st.k;
       launch_copy_slice(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, o, h.dtype, s);
     }
-    if (ev) RTDM_HIP(hipEventRecord(ev[si + 1], s));
+    if (ev) RTDM_HIP(hipEventRecord(ev[2 * si + 1], s));
+    if (two && st.signal) RTDM_HIP(hipEventRecord(h.step_ev[si], s));
+  }
+  if (two) {  // everything on the side stream finishes before later work on the caller's stream
+    RTDM_HIP(hipEventRecord(h.join_ev, h.side));
+    RTDM_HIP(hipStreamWaitEvent(s0, h.join_ev, 0));
   }
   h.last_n = n;
 }
@@ -805,6 +836,91 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
   }
 }
 
+// Two-stream schedule of the step list.  Dependencies come from the buffers each
+// step reads and writes (a route concat is one buffer written by several
+// producers).  A step's primary producer is its latest dependency; among the
+// steps sharing a primary producer, the one with the longest remaining path
+// (FLOP + 312 FLOP per HBM byte ~ time at the chip's peaks) stays on the
+// producer's stream and the others run on the other stream — in the YOLO
+// graphs these are the detection-head branches, which then overlap the trunk.
+static int g_two_streams = 1;
+int two_streams_mode() { return g_two_streams; }
+void set_two_streams_mode(int v) { g_two_streams = v ? 1 : 0; }
+
+static void schedule_streams(rtdm_detector_s& h) {
+  const int ns = (int)h.steps.size();
+  auto buf_of = [&](int t) { return t < 0 ? -1 : (h.tensors[t].home >= 0 ? h.tensors[t].home : t); };
+  std::vector<std::vector<int>> reads(ns), writes(ns);
+  std::vector<double> cost(ns, 0.0);
+  for (int i = 0; i < ns; ++i) {
+    const Step& st = h.steps[i];
+    auto rd = [&](int t) {
+      if (buf_of(t) >= 0) reads[i].push_back(buf_of(t));
+    };
+    auto wr = [&](int t) {
+      if (t >= 0 && h.tensors[t].materialised) writes[i].push_back(buf_of(t));
+    };
+    rd(st.in_t);
+    if (st.kind == ST_CONV) {
+      rd(st.res_t);
+      wr(st.full_t);
+      wr(st.pool_t);
+      wr(st.up_t);
+    } else {
+      wr(st.out_t);
+    }
+    std::string name;
+    double f = 0, b = 0;
+    step_info(h, st, name, f, b);
+    cost[i] = f + 312.0 * b;
+  }
+  for (int i = 0; i < ns; ++i) {
+    Step& st = h.steps[i];
+    st.deps.clear();
+    for (int j = 0; j < i; ++j) {
+      bool dep = false;
+      for (int rb : reads[i])
+        for (int wb : writes[j]) dep = dep || rb == wb;
+      if (dep) st.deps.push_back(j);
+    }
+  }
+  std::vector<double> lp(ns, 0.0);  // longest path from step i to the end
+  for (int i = ns - 1; i >= 0; --i) {
+    double m = 0.0;
+    for (int j = i + 1; j < ns; ++j)
+      for (int d : h.steps[j].deps)
+        if (d == i) m = std::max(m, lp[j]);
+    lp[i] = cost[i] + m;
+  }
+  for (int i = 0; i < ns; ++i) {
+    Step& st = h.steps[i];
+    st.stream = 0;
+    st.signal = false;
+    if (st.deps.empty()) continue;
+    const int p = st.deps.back();
+    // the heaviest child of p keeps p's stream
+    int best = -1;
+    for (int j = p + 1; j < ns; ++j)
+      if (!h.steps[j].deps.empty() && h.steps[j].deps.back() == p && (best < 0 || lp[j] > lp[best])) best = j;
+    st.stream = best == i ? h.steps[p].stream : 1 - h.steps[p].stream;
+  }
+  bool any_side = false;
+  for (int i = 0; i < ns; ++i) {
+    any_side = any_side || h.steps[i].stream == 1;
+    for (int d : h.steps[i].deps)
+      if (h.steps[d].stream != h.steps[i].stream) h.steps[d].signal = true;
+  }
+  h.two_streams = any_side && two_streams_mode();
+  if (h.two_streams && !h.planning_only) {
+    RTDM_HIP(hipStreamCreateWithFlags(&h.side, hipStreamNonBlocking));
+    h.step_ev.assign(ns, nullptr);
+    for (int i = 0; i < ns; ++i)
+      if (h.steps[i].signal) RTDM_HIP(hipEventCreateWithFlags(&h.step_ev[i], hipEventDisableTiming));
+    RTDM_HIP(hipEventCreateWithFlags(&h.fork_ev, hipEventDisableTiming));
+    RTDM_HIP(hipEventCreateWithFlags(&h.join_ev, hipEventDisableTiming));
+  }
+}
+
 static std::string describe(const rtdm_detector_s& h) {
   std::ostringstream o;
   o << "darknet plan: img " << h.img_h << "x" << h.img_w << " dtype " << (h.dtype == RTDM_F16 ? "f16" : "f32")
@@ -826,6 +942,7 @@ static std::string describe(const rtdm_detector_s& h) {
         << (st.pc.mfma ? "mfma" : "valu") << (st.quad ? " quad" : "") << " in=" << (st.in_t < 0 ? "input" : tn(st.in_t))
         << " full=" << tn(st.full_t) << " pool=" << tn(st.pool_t) << " up=" << tn(st.up_t) << " res=" << tn(st.res_t);
       if (st.head) o << " head1x1->" << st.head_cout;
+      if (h.two_streams && st.stream == 1) o << " [side stream]";
       if (st.yolo >= 0) o << " yolo" << st.yolo << "(off " << h.heads[st.yolo].io_off << ")";
     } else if (st.kind == ST_MAXPOOL) {
       o << "maxpool k" << st.k << " s" << st.s << (st.zero_rb ? " zeropad" : "") << " " << tn(st.in_t) << " -> "
@@ -866,6 +983,7 @@ rtdm_status rtdm_detector_create(const char* cfg_text, int img_h, int img_w, int
     RTDM_REQUIRE(net.i("channels", 3) == 3, RTDM_E_UNSUPPORTED, "cfg: only 3-channel input supported");
     h->defs.assign(defs.begin() + 1, defs.end());
     plan(*h, weights, n_floats);
+    schedule_streams(*h);
     *out = h.release();
   });
 }
@@ -925,7 +1043,7 @@ rtdm_status rtdm_detector_enable_timing(rtdm_detector h, int max_calls) {
     h->timing = max_calls > 0;
     h->timing_cap = max_calls > 0 ? max_calls : 0;
     h->timing_calls = 0;
-    const size_t ne = (size_t)h->timing_cap * (h->steps.size() + 1);
+    const size_t ne = (size_t)h->timing_cap * 2 * h->steps.size();
     h->events.resize(ne);
     for (size_t i = 0; i < ne; ++i) RTDM_HIP(hipEventCreateWithFlags(&h->events[i], hipEventDisableSystemFence));
   });
@@ -937,11 +1055,11 @@ rtdm_status rtdm_detector_read_timing(rtdm_detector h, double* ms_per_step, int*
     const size_t ns = h->steps.size();
     for (size_t i = 0; i < ns; ++i) ms_per_step[i] = 0.0;
     for (int c = 0; c < h->timing_calls; ++c) {
-      hipEvent_t* ev = &h->events[(size_t)c * (ns + 1)];
-      RTDM_HIP(hipEventSynchronize(ev[ns]));
+      hipEvent_t* ev = &h->events[(size_t)c * 2 * ns];
       for (size_t i = 0; i < ns; ++i) {
         float ms = 0.f;
-        RTDM_HIP(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+        RTDM_HIP(hipEventSynchronize(ev[2 * i + 1]));
+        RTDM_HIP(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
         ms_per_step[i] += ms;
       }
     }
