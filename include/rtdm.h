@@ -23,6 +23,9 @@
  *   rtdm_yolo_decode         <- YOLOLayer inference branch (models.py:252-258) on raw
  *                               head maps; also the TensorRT plugin enqueue
  *                               victim_localization/tensorrt_inference/plugins/yolo_layer.cu:308-327
+ *   rtdm_detect_trt          <- context.execute_async() of a YOLO engine with YoloLayer_TRT
+ *                               victim_localization/tensorrt_inference/utils/yolo_with_plugins.py:268-282
+ *   rtdm_yolo_layer_trt      <- YoloLayerPlugin::enqueue   tensorrt_inference/plugins/yolo_layer.cu:323-327
  *   rtdm_nms                 <- non_max_suppression()   victim_localization/yolov3/utils/utils.py:488-557
  *                               (+ torchvision.ops.boxes.nms, utils.py:552)
  *
@@ -160,6 +163,19 @@ rtdm_status rtdm_detector_enable_timing(rtdm_detector h, int max_calls);
 rtdm_status rtdm_detector_read_timing(rtdm_detector h, double* ms_per_step, int* calls);
 /* io: [n, n_anchors_total, no] fp32, exactly the reference's torch.cat(io, 1). */
 rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float* io, void* stream);
+/* Raw head predictions: p [n, n_anchors_total, no] fp32 in io's row order, i.e. the
+ * YOLOLayer training-branch output p.view(bs,na,no,ny,nx).permute(0,1,3,4,2)
+ * (models.py:240-250) of every head, concatenated like io.                      */
+rtdm_status rtdm_detect_raw(rtdm_detector h, const void* x, int x_kind, int n, float* p, void* stream);
+/* TensorRT-layout detections: dets [n, n_anchors_total, 7] Detection records
+ * {x, y, w, h, det_confidence, class_id, class_confidence} (yolo_layer.h:26-31),
+ * per head exactly the YoloLayer_TRT plugin output (CalDetection, or
+ * CalDetection_NewCoords when the [yolo] block sets new_coords=1; scale_x_y from
+ * the cfg, default 1), heads in cfg order = the engine's output bindings
+ * concatenated (yolo_with_plugins.py:115-119).  Replaces context.execute_async
+ * (yolo_with_plugins.py:268-282) for trt_yolo.py.  Allocates a raw-head scratch
+ * buffer on the first call.                                                      */
+rtdm_status rtdm_detect_trt(rtdm_detector h, const void* x, int x_kind, int n, float* dets, void* stream);
 /* Debug/parity: copy cfg layer `layer`'s output of the LAST rtdm_detect call as
  * NCHW fp32 [n,C,H,W] into out (only for layers whose full-resolution output is
  * materialised; returns RTDM_E_UNSUPPORTED otherwise).                          */
@@ -171,6 +187,16 @@ rtdm_status rtdm_detector_layer_output(rtdm_detector h, int layer, int n, float*
  * Writes io rows [row_offset, row_offset + na*ny*nx) of io [n, io_rows, no].     */
 rtdm_status rtdm_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const float* anchors,
                              int img_h, int img_w, float* io, int io_rows, int row_offset, void* stream);
+
+/* ---- TensorRT YoloLayer_TRT plugin (yolo_layer.cu:308-327 enqueue) --------------
+ * input: one head's raw map NCHW [batch, num_anchors*(5+num_classes), yolo_height,
+ * yolo_width] fp32.  anchors: [num_anchors*2] pixels (host; copied into the launch).
+ * output: [batch, num_anchors*yolo_height*yolo_width, 7] Detection records.  The
+ * engine input size is yolo_{width,height} * input_multiplier (createPlugin,
+ * yolo_layer.cu:416); its asserts (:409-413) become RTDM_E_INVALID.               */
+rtdm_status rtdm_yolo_layer_trt(const float* input, int batch, int yolo_width, int yolo_height, int num_anchors,
+                                const float* anchors, int num_classes, int input_multiplier, float scale_x_y,
+                                int new_coords, float* output, void* stream);
 
 /* ---- NMS (non_max_suppression, utils.py:488-557, method 'vision_batch') -------
  * io: [n, n_anchors, no] fp32 (no = 5 + nc).

@@ -74,10 +74,12 @@ class DarknetRef:
         assert ptr == stream.size, (ptr, stream.size)
 
     @torch.no_grad()
-    def forward(self, x: torch.Tensor, keep_layers=False):
-        """x: [N,3,H,W] fp32 in [0,1] -> io [N, sum(A*ny*nx), 5+nc] (and per-layer outputs)."""
+    def forward(self, x: torch.Tensor, keep_layers=False, raw=False):
+        """x: [N,3,H,W] fp32 in [0,1] -> io [N, sum(A*ny*nx), 5+nc] (and per-layer outputs).
+        raw=True: the undecoded p rows instead (YOLOLayer training branch, models.py:240-250)."""
         img_size = x.shape[-2:]
         out, io_list = [], []
+        self.heads = []  # per [yolo]: grid and masked anchors (the TRT plugin's fields)
         for i, m in enumerate(self.mdefs):
             t = m["type"]
             if t == "convolutional":
@@ -106,12 +108,22 @@ class DarknetRef:
             elif t == "shortcut":
                 x = x + out[m["from"][0]]
             elif t == "yolo":
-                io_list.append(self._yolo(m, x, img_size))
+                self.heads.append({"na": len(m["mask"]), "ny": x.shape[2], "nx": x.shape[3],
+                                   "anchors": [tuple(m["anchors"][a]) for a in m["mask"]],
+                                   "scale_x_y": float(m.get("scale_x_y", 1.0)),
+                                   "new_coords": int(m.get("new_coords", 0))})
+                io_list.append(self._raw(m, x) if raw else self._yolo(m, x, img_size))
             else:
                 raise ValueError(t)
             out.append(x if (keep_layers or i in self.routs) else [])
         io = torch.cat(io_list, 1)
         return (io, out) if keep_layers else io
+
+    @staticmethod
+    def _raw(m, p):
+        na, no = len(m["mask"]), int(m["classes"]) + 5
+        bs, _, ny, nx = p.shape
+        return p.view(bs, na, no, ny, nx).permute(0, 1, 3, 4, 2).reshape(bs, -1, no)
 
     @staticmethod
     def _yolo(m, p, img_size):

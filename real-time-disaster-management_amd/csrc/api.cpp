@@ -60,6 +60,39 @@ rtdm_status rtdm_yolo_decode(const float* p, int n, int na, int no, int ny, int 
   });
 }
 
+rtdm_status rtdm_yolo_layer_trt(const float* input, int batch, int yolo_width, int yolo_height, int num_anchors,
+                                const float* anchors, int num_classes, int input_multiplier, float scale_x_y,
+                                int new_coords, float* output, void* stream) {
+  return guard([&] {
+    if (batch == 0) return;
+    // YoloPluginCreator::createPlugin checks (yolo_layer.cu:409-413), as status codes
+    RTDM_REQUIRE(input && output && anchors, RTDM_E_INVALID, "yolo_layer_trt: NULL pointer");
+    RTDM_REQUIRE(batch > 0 && yolo_width > 0 && yolo_height > 0, RTDM_E_INVALID, "yolo_layer_trt: bad shape");
+    RTDM_REQUIRE(num_anchors > 0 && num_anchors <= kTrtMaxAnchors, RTDM_E_INVALID,
+                 "yolo_layer_trt: num_anchors must be in [1, 6]");
+    RTDM_REQUIRE(anchors[0] > 0.f && anchors[1] > 0.f, RTDM_E_INVALID, "yolo_layer_trt: anchors must be positive");
+    RTDM_REQUIRE(num_classes > 0, RTDM_E_INVALID, "yolo_layer_trt: num_classes must be positive");
+    RTDM_REQUIRE(input_multiplier == 8 || input_multiplier == 16 || input_multiplier == 32, RTDM_E_INVALID,
+                 "yolo_layer_trt: input_multiplier must be 8, 16 or 32");
+    RTDM_REQUIRE(scale_x_y >= 1.0f, RTDM_E_INVALID, "yolo_layer_trt: scale_x_y must be >= 1");
+    TrtYoloArgs t;
+    t.n_heads = 1;
+    t.rows = num_anchors * yolo_width * yolo_height;
+    t.no = 5 + num_classes;
+    t.nc = num_classes;
+    TrtYoloHead& d = t.h[0];
+    d.na = num_anchors;
+    d.ny = yolo_height;
+    d.nx = yolo_width;
+    d.in_w = yolo_width * input_multiplier;
+    d.in_h = yolo_height * input_multiplier;
+    d.scale_xy = scale_x_y;
+    d.new_coords = new_coords ? 1 : 0;
+    for (int j = 0; j < 2 * num_anchors; ++j) d.anchors[j] = anchors[j];
+    launch_yolo_trt(input, batch, t, 1, output, (hipStream_t)stream);
+  });
+}
+
 size_t rtdm_nms_workspace_size(int n, int n_anchors, int nc) {
   if (n <= 0 || n_anchors <= 0 || nc <= 0) return 0;
   return nms_workspace_size(n, n_anchors, nc);

@@ -122,6 +122,9 @@ struct Epilogue {
   int io_rows = 0, io_off = 0, na = 0, no = 0;
   float ystride = 0.f;
   const float* anchor_vec = nullptr;  // device [na][2]: anchors / stride, fp32 like models.py:431
+  // raw = 1: write the head conv's output itself (no decode) into the io rows: the
+  // YOLOLayer training-branch p (models.py:249-250) that the TensorRT plugin decodes
+  int raw = 0;
 };
 
 // Branch-free unsigned division by a runtime-invariant divisor (round-up
@@ -251,6 +254,26 @@ void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_
 
 void launch_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const float* anchor_vec, float ystride,
                         float* io, int io_rows, int row_off, hipStream_t s);
+
+// TensorRT YoloLayer_TRT decode (CalDetection / CalDetection_NewCoords,
+// tensorrt_inference/plugins/yolo_layer.cu:203-306) -> Detection records of 7 floats
+static constexpr int kTrtMaxHeads = 8;
+static constexpr int kTrtMaxAnchors = 6;  // MAX_ANCHORS, yolo_layer.h:11
+struct TrtYoloHead {
+  int row0 = 0, na = 0, ny = 0, nx = 0;  // rows [row0, row0 + na*ny*nx) of the row layout
+  int in_w = 0, in_h = 0;                // mInputWidth / mInputHeight
+  float scale_xy = 1.f;
+  int new_coords = 0;
+  float anchors[2 * kTrtMaxAnchors] = {};  // pixels
+};
+struct TrtYoloArgs {
+  int n_heads = 0, rows = 0, no = 0, nc = 0;
+  TrtYoloHead h[kTrtMaxHeads];
+};
+// nchw = 0: in = rows [n, rows, no] (the raw YOLOLayer p of every head, io order);
+// nchw = 1: in = one head's map [n, na*no, ny, nx] (the plugin's input binding).
+// out: [n, rows, 7] (plugin output order: anchor, then grid cell).
+void launch_yolo_trt(const float* in, int n, const TrtYoloArgs& t, int nchw, float* out, hipStream_t s);
 
 size_t nms_workspace_size(int n, int n_anchors, int nc);
 void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label,

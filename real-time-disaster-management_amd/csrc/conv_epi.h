@@ -100,7 +100,9 @@ __device__ __forceinline__ void epi4(const ConvArgs& a, int m0, int c, f4 v) {
       if (e.io) {
         const int ai = c / e.no, k = c - ai * e.no;
         float o;
-        if (k < 2) {
+        if (e.raw) {
+          o = x;
+        } else if (k < 2) {
           o = (sigmoidf_(x) + (float)(k == 0 ? ox : oy)) * e.ystride;
         } else if (k < 4) {
           o = (expf(x) * e.anchor_vec[2 * ai + (k - 2)]) * e.ystride;
@@ -212,7 +214,9 @@ __device__ __forceinline__ void epi_vec8(const ConvArgs& a, int m0, int c0, cons
       for (int j = 0; j < 8; ++j) {
         if (j < nc) {
           float o;
-          if (k < 2)
+          if (e.raw)
+            o = x[j];
+          else if (k < 2)
             o = (__frcp_rn(1.f + __expf(-x[j])) + (float)(k == 0 ? ox : oy)) * e.ystride;
           else if (k < 4)
             o = (__expf(x[j]) * e.anchor_vec[2 * ai + (k - 2)]) * e.ystride;

@@ -61,7 +61,9 @@ __device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v
     float x = v[r] + bias;
     if (e.act == ACT_LEAKY) x = x > 0.f ? x : x * e.slope;
     float o;
-    if (k < 2)
+    if (e.raw)
+      o = x;
+    else if (k < 2)
       o = (__frcp_rn(1.f + __expf(-x)) + (float)(k == 0 ? ox : oy)) * e.ystride;
     else if (k < 4)
       o = (__expf(x) * anc) * e.ystride;

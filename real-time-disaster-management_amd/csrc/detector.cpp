@@ -132,6 +132,11 @@ struct YoloHead {
   int layer = 0, na = 0, no = 0, ny = 0, nx = 0, io_off = 0;
   float ystride = 0.f;
   std::vector<float> anchor_vec;
+  // TensorRT YoloLayer_TRT fields for rtdm_detect_trt (yolo_layer.cu:352-419): masked
+  // anchors in pixels, [yolo] scale_x_y / new_coords (default 1 / 0)
+  std::vector<float> anchor_px;
+  float scale_xy = 1.f;
+  int new_coords = 0;
   size_t anchor_off = 0;  // device copy in the weight blob
 };
 
@@ -152,6 +157,7 @@ struct rtdm_detector_s {
   rtdm::DevBlob blob;
   rtdm::DevBuf arena;
   rtdm::DevBuf zero;  // 256 zero bytes: padding source of the glds conv kernel
+  rtdm::DevBuf raw_buf;  // raw head rows for rtdm_detect_trt (allocated on first use)
   int last_n = 0;
   // optional per-step timing: events[call][2*step + {0,1}] recorded around each step
   // on the stream it runs on
@@ -384,7 +390,11 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
             RTDM_REQUIRE(2 * a + 1 < (int)anc.size(), RTDM_E_INVALID, "cfg: yolo mask out of range");
             yh.anchor_vec.push_back((float)anc[2 * a] / (float)ystride);
             yh.anchor_vec.push_back((float)anc[2 * a + 1] / (float)ystride);
+            yh.anchor_px.push_back((float)anc[2 * a]);
+            yh.anchor_px.push_back((float)anc[2 * a + 1]);
           }
+          yh.scale_xy = yb.has("scale_x_y") ? (float)std::stod(yb.str("scale_x_y")) : 1.f;
+          yh.new_coords = yb.i("new_coords", 0);
           yh.io_off = h.n_anchors_total;
           h.n_anchors_total += yh.na * yh.ny * yh.nx;
           s.yolo = (int)h.heads.size();
@@ -420,7 +430,11 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
             RTDM_REQUIRE(2 * a + 1 < (int)anc.size(), RTDM_E_INVALID, "cfg: yolo mask out of range");
             yh.anchor_vec.push_back((float)anc[2 * a] / (float)ystride);
             yh.anchor_vec.push_back((float)anc[2 * a + 1] / (float)ystride);
+            yh.anchor_px.push_back((float)anc[2 * a]);
+            yh.anchor_px.push_back((float)anc[2 * a + 1]);
           }
+          yh.scale_xy = nx.has("scale_x_y") ? (float)std::stod(nx.str("scale_x_y")) : 1.f;
+          yh.new_coords = nx.i("new_coords", 0);
           yh.io_off = h.n_anchors_total;
           h.n_anchors_total += yh.na * yh.ny * yh.nx;
           s.yolo = (int)h.heads.size();
@@ -653,7 +667,8 @@ static View tensor_view(const rtdm_detector_s& h, int t) {
   return View{base + x.off * es * h.max_batch, x.c, 0};
 }
 
-static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, float* io, hipStream_t s) {
+static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, float* io, hipStream_t s,
+                         int raw = 0) {
   RTDM_REQUIRE(!h.planning_only, RTDM_E_INVALID, "detect: handle was created without weights");
   RTDM_REQUIRE(n >= 0 && n <= h.max_batch, RTDM_E_CAPACITY,
                "detect: batch " + std::to_string(n) + " exceeds max_batch " + std::to_string(h.max_batch));
@@ -734,6 +749,7 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
         a.head_e.no = y.no;
         a.head_e.ystride = y.ystride;
         a.head_e.anchor_vec = h.blob.at<float>(y.anchor_off);
+        a.head_e.raw = raw;
       } else if (st.yolo >= 0) {
         const YoloHead& y = h.heads[st.yolo];
         a.e.io = io;
@@ -743,6 +759,7 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
         a.e.no = y.no;
         a.e.ystride = y.ystride;
         a.e.anchor_vec = h.blob.at<float>(y.anchor_off);
+        a.e.raw = raw;
       }
       // the mfma/valu choice was fixed when the weights were packed
       a.w_f32 = st.pc.mfma ? 0 : 1;
@@ -1071,6 +1088,49 @@ rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float
   return guard([&] {
     RTDM_REQUIRE(h, RTDM_E_INVALID, "detect: NULL handle");
     run_detector(*h, x, x_kind, n, io, (hipStream_t)stream);
+  });
+}
+
+rtdm_status rtdm_detect_raw(rtdm_detector h, const void* x, int x_kind, int n, float* p, void* stream) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "detect_raw: NULL handle");
+    run_detector(*h, x, x_kind, n, p, (hipStream_t)stream, 1);
+  });
+}
+
+rtdm_status rtdm_detect_trt(rtdm_detector h, const void* x, int x_kind, int n, float* dets, void* stream) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "detect_trt: NULL handle");
+    RTDM_REQUIRE(!h->planning_only, RTDM_E_INVALID, "detect_trt: handle was created without weights");
+    RTDM_REQUIRE(n >= 0 && n <= h->max_batch, RTDM_E_CAPACITY, "detect_trt: batch exceeds max_batch");
+    if (n == 0) return;
+    RTDM_REQUIRE(dets, RTDM_E_INVALID, "detect_trt: NULL dets");
+    RTDM_REQUIRE((int)h->heads.size() <= kTrtMaxHeads, RTDM_E_UNSUPPORTED, "detect_trt: too many [yolo] heads");
+    TrtYoloArgs t;
+    t.n_heads = (int)h->heads.size();
+    t.rows = h->n_anchors_total;
+    t.no = h->no;
+    t.nc = h->nc;
+    for (int k = 0; k < t.n_heads; ++k) {
+      const YoloHead& y = h->heads[k];
+      RTDM_REQUIRE(y.na <= kTrtMaxAnchors, RTDM_E_UNSUPPORTED,
+                   "detect_trt: more than 6 anchors per head (yolo_layer.h MAX_ANCHORS)");
+      TrtYoloHead& d = t.h[k];
+      d.row0 = y.io_off;
+      d.na = y.na;
+      d.ny = y.ny;
+      d.nx = y.nx;
+      // the engine's input size is yolo_width * inputMultiplier (yolo_layer.cu:416)
+      d.in_w = y.nx * (h->img_w / y.nx);
+      d.in_h = y.ny * (h->img_h / y.ny);
+      d.scale_xy = y.scale_xy;
+      d.new_coords = y.new_coords;
+      for (int j = 0; j < 2 * y.na; ++j) d.anchors[j] = y.anchor_px[j];
+    }
+    const size_t need = (size_t)h->max_batch * h->n_anchors_total * h->no * sizeof(float);
+    if (h->raw_buf.bytes < need) h->raw_buf.alloc(need);
+    run_detector(*h, x, x_kind, n, h->raw_buf.as<float>(), (hipStream_t)stream, 1);
+    launch_yolo_trt(h->raw_buf.as<float>(), n, t, 0, dets, (hipStream_t)stream);
   });
 }
 

@@ -839,6 +839,81 @@ void launch_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, c
   RTDM_HIP(hipGetLastError());
 }
 
+// ------------------------------------------------- TensorRT YOLO plugin decode --
+// CalDetection / CalDetection_NewCoords (tensorrt_inference/plugins/yolo_layer.cu:
+// 203-306): one thread per (image, anchor, cell) -> Detection {x, y, w, h (top-left,
+// normalised to the input), det_confidence, class_id, class_confidence}.  class id =
+// first maximum raw class logit; sigmoid applied to it (not to each class) and to
+// the objectness, which is not multiplied in.
+__global__ __launch_bounds__(256) void yolo_trt_kernel(const float* __restrict__ in, int n, TrtYoloArgs t, int nchw,
+                                                       float* __restrict__ out) {
+  const int64_t total = (int64_t)n * t.rows;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(idx / t.rows);
+    const int row = (int)(idx - (int64_t)b * t.rows);
+    int hk = 0;
+    while (hk + 1 < t.n_heads && row >= t.h[hk + 1].row0) ++hk;
+    const TrtYoloHead& hd = t.h[hk];
+    const int grids = hd.ny * hd.nx;
+    const int r = row - hd.row0;
+    const int ai = r / grids, cell = r - ai * grids;
+    const int gy = cell / hd.nx, gx = cell - gy * hd.nx;
+    // field k of this record: row layout (contiguous) or the plugin's NCHW plane
+    const float* src;
+    int64_t step;
+    if (nchw) {
+      src = in + ((int64_t)b * hd.na + ai) * t.no * grids + cell;
+      step = grids;
+    } else {
+      src = in + idx * t.no;
+      step = 1;
+    }
+    int cls = 0;
+    float best = -INFINITY;
+    for (int c = 0; c < t.nc; ++c) {
+      const float l = src[(5 + c) * step];
+      if (l > best) {
+        best = l;
+        cls = c;
+      }
+    }
+    const float tx = src[0], ty = src[step], tw = src[2 * step], th = src[3 * step], to = src[4 * step];
+    const float sxy = hd.scale_xy, off = (sxy - 1.0f) * 0.5f;
+    float bx, by, bw, bh, det_conf, cls_conf;
+    if (!hd.new_coords) {
+      bx = ((float)gx + (sxy * (1.0f / (1.0f + expf(-tx))) - off)) / (float)hd.nx;
+      by = ((float)gy + (sxy * (1.0f / (1.0f + expf(-ty))) - off)) / (float)hd.ny;
+      bw = expf(tw) * hd.anchors[2 * ai] / (float)hd.in_w;
+      bh = expf(th) * hd.anchors[2 * ai + 1] / (float)hd.in_h;
+      det_conf = 1.0f / (1.0f + expf(-to));
+      cls_conf = 1.0f / (1.0f + expf(-best));
+    } else {  // scaled-YOLOv4 coordinates: the head already applied the sigmoid
+      bx = ((float)gx + (sxy * tx - off)) / (float)hd.nx;
+      by = ((float)gy + (sxy * ty - off)) / (float)hd.ny;
+      bw = tw * tw * 4 * hd.anchors[2 * ai] / (float)hd.in_w;
+      bh = th * th * 4 * hd.anchors[2 * ai + 1] / (float)hd.in_h;
+      det_conf = to;
+      cls_conf = best;
+    }
+    float* o = out + idx * 7;
+    o[0] = bx - bw / 2;
+    o[1] = by - bh / 2;
+    o[2] = bw;
+    o[3] = bh;
+    o[4] = det_conf;
+    o[5] = (float)cls;
+    o[6] = cls_conf;
+  }
+}
+
+void launch_yolo_trt(const float* in, int n, const TrtYoloArgs& t, int nchw, float* out, hipStream_t s) {
+  const int64_t total = (int64_t)n * t.rows;
+  if (total <= 0) return;
+  hipLaunchKernelGGL(yolo_trt_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, in, n, t, nchw, out);
+  RTDM_HIP(hipGetLastError());
+}
+
 // -------------------------------------------------------------------- NMS --
 // non_max_suppression (utils.py:488-557, method 'vision_batch') with the
 // greedy kernel of torchvision.ops.boxes.nms (CPU: descending score order,

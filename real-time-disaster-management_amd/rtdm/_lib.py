@@ -70,6 +70,10 @@ SIGNATURES = {
     "rtdm_detector_enable_timing": (c_int, [c_void_p, c_int]),
     "rtdm_detector_read_timing": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int)]),
     "rtdm_detect": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "rtdm_detect_raw": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "rtdm_detect_trt": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "rtdm_yolo_layer_trt": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_float), c_int, c_int, c_float,
+                                    c_int, c_void_p, c_void_p]),
     "rtdm_detector_layer_output": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int64, POINTER(c_int),
                                            POINTER(c_int), POINTER(c_int), c_void_p]),
     "rtdm_yolo_decode": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, POINTER(c_float), c_int, c_int,

@@ -170,6 +170,33 @@ class Darknet(torch.nn.Module):
             L.check(L.lib().rtdm_detect(h, L.ptr(x), kind, n, L.ptr(out), L.stream_ptr(stream)))
         return out, None
 
+    def _run(self, fn, x: torch.Tensor, width: int, stream=None):
+        if not x.is_cuda:
+            raise RuntimeError("rtdm Darknet runs on the GPU: move the input to a cuda device")
+        if x.dtype == torch.uint8:
+            if x.dim() != 4 or x.shape[3] != 3 or tuple(x.shape[1:3]) != self.img_size:
+                raise ValueError(f"uint8 frames must be [N,{self.img_size[0]},{self.img_size[1]},3]")
+            kind = L.RTDM_INPUT_FRAME_U8
+        else:
+            if x.dim() != 4 or x.shape[1] != 3 or tuple(x.shape[2:]) != self.img_size:
+                raise ValueError(f"input must be [N,3,{self.img_size[0]},{self.img_size[1]}] (planned size)")
+            kind = L.RTDM_INPUT_NCHW_F32 if x.dtype == torch.float32 else L.RTDM_INPUT_NCHW_F16
+        x = x.contiguous()
+        n = x.shape[0]
+        out = torch.empty((n, self.n_anchors, width), device=x.device, dtype=torch.float32)
+        with torch.cuda.device(x.device):
+            L.check(fn(self.handle(n), L.ptr(x), kind, n, L.ptr(out), L.stream_ptr(stream)))
+        return out
+
+    def forward_raw(self, x: torch.Tensor, stream=None) -> torch.Tensor:
+        """Raw head predictions [N, sum(A*ny*nx), 5+nc] (YOLOLayer training-branch p of every
+        head, models.py:240-250, in io's row order)."""
+        return self._run(L.lib().rtdm_detect_raw, x, self.no, stream)
+
+    def forward_trt(self, x: torch.Tensor, stream=None) -> torch.Tensor:
+        """YoloLayer_TRT Detection records [N, sum(A*ny*nx), 7] (yolo_layer.cu:203-306)."""
+        return self._run(L.lib().rtdm_detect_trt, x, 7, stream)
+
     def describe(self) -> str:
         """Text dump of the launch plan (steps, fusions, buffers) of the current handle."""
         h = self._handle if self._handle is not None else self.handle(1)

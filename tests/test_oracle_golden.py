@@ -111,3 +111,57 @@ def test_preprocess_restatement_matches_pillow(cls_golden):
     # the stored crops are exactly resize + crop of the stored sources? (real images not stored whole)
     c = cls_golden["squeeze-ernet/crops"]
     assert c.dtype == np.uint8 and c.shape[1:] == (140, 140, 3)
+
+
+def test_trt_decode_oracle_pinned_by_reference_io(det_golden):
+    """CalDetection restatement vs the reference YOLOLayer golden io through the
+    identities that hold at scale_x_y = 1: det_conf = io[4], class_conf = max io[5:]
+    (first maximum), w = io[2] / W, x = io[0] / W - w / 2 (yolo_layer.cu:203-249 vs
+    models.py:252-258)."""
+    from oracle.darknet import DarknetRef
+    from oracle import trt_yolo as OT
+    from rtdm.synth import load_calibration, synth_darknet_weights
+    case = "yolov4-tiny-aider-416@256"
+    text = cfg_text("yolov4-tiny-aider-416")
+    ref = DarknetRef(text, synth_darknet_weights(text, calib=load_calibration("yolov4-tiny-aider-416")))
+    frames = det_golden[f"{case}/frames"]
+    raw = ref.forward(torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0, raw=True).numpy()
+    io = det_golden[f"{case}/io"]
+    assert raw.shape == io.shape
+    det = OT.cal_detection_rows(raw, ref.heads, 256, 256)
+    W = 256.0
+    assert np.allclose(det[..., 4], io[..., 4], rtol=2e-6, atol=1e-7)
+    assert np.allclose(det[..., 6], io[..., 5:].max(-1), rtol=2e-6, atol=1e-7)
+    amb = np.sort(io[..., 5:], -1)
+    clear = amb[..., -1] - amb[..., -2] > 1e-6
+    assert np.array_equal(det[..., 5][clear], io[..., 5:].argmax(-1)[clear].astype(np.float32))
+    assert np.allclose(det[..., 2], io[..., 2] / W, rtol=1e-5, atol=1e-7)
+    assert np.allclose(det[..., 3], io[..., 3] / W, rtol=1e-5, atol=1e-7)
+    assert np.allclose(det[..., 0], io[..., 0] / W - det[..., 2] / 2, rtol=1e-5, atol=2e-6)
+    assert np.allclose(det[..., 1], io[..., 1] / W - det[..., 3] / 2, rtol=1e-5, atol=2e-6)
+
+
+def test_trt_postprocess_product_matches_oracle():
+    """Host post-processing of rtdm.trt_yolo (vectorised) vs the loop restatement of
+    _postprocess_yolo / _nms_boxes on seeded Detection records (no score ties)."""
+    from oracle import trt_yolo as OT
+    from rtdm.trt_yolo import postprocess_yolo
+    rng = np.random.default_rng(11)
+    for letter_box, (ih, iw) in ((False, (416, 416)), (True, (300, 500)), (True, (500, 300))):
+        n = 600
+        d = np.zeros((n, 7), np.float32)
+        d[:, 0:2] = rng.uniform(-0.05, 0.95, (n, 2))
+        d[:, 2:4] = rng.uniform(0.01, 0.3, (n, 2))
+        d[:, 4] = rng.uniform(0, 1, n)
+        d[:, 5] = rng.integers(0, 3, n)
+        d[:, 6] = rng.uniform(0.2, 1, n)
+        s = d[:, 4] * d[:, 6]
+        assert len(np.unique(s)) == n
+        outs = [d[:250], d[250:]]
+        got = postprocess_yolo(outs, iw, ih, 0.3, 0.5, (416, 416), letter_box)
+        exp = OT.postprocess_yolo(outs, iw, ih, 0.3, 0.5, (416, 416), letter_box)
+        assert len(got[0]) == len(exp[0]) > 10
+        for g, e in zip(got, exp):
+            assert np.array_equal(g, e)
+    empty = postprocess_yolo([np.zeros((5, 7), np.float32)], 416, 416, 0.3, 0.5, (416, 416))
+    assert empty[0].shape == (0, 4)
