@@ -82,7 +82,7 @@ struct DevBuf {
   }
 };
 
-inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+__host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // ------------------------------------------------------------ activations ----
 enum Act : int { ACT_LINEAR = 0, ACT_LEAKY = 1, ACT_SWISH = 2 };
@@ -248,6 +248,9 @@ struct ResizePlan {  // Pillow 8bpc antialiased bilinear, restricted to a center
   DevBuf bounds_h, coef_h, bounds_v, coef_v;  // int32 device arrays
 };
 void build_resize_plan(ResizePlan& p, int in_h, int in_w, int out_size, bool upload);
+// 1 = streaming resize kernel (default), 0 = the staged band kernel (A/B knob)
+int resize_stream_mode();
+void set_resize_stream_mode(int v);
 // frames -> tmp (horizontal pass) -> out (vertical pass + crop + ToTensor + Normalize)
 void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_t* tmp, void* out,
                        int out_layout /*0: NHWC dtype, 1: NCHW f32*/, int dtype, hipStream_t s);
@@ -276,6 +279,7 @@ struct TrtYoloArgs {
 void launch_yolo_trt(const float* in, int n, const TrtYoloArgs& t, int nchw, float* out, hipStream_t s);
 
 size_t nms_workspace_size(int n, int n_anchors, int nc);
+void set_nms_variant(int v);  // diagnostics: bit 0 = bitonic sort only, bit 1 = no bitmask path
 void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label,
                 int agnostic, uint64_t class_mask, int max_det, void* ws, float* det, int32_t* idx,
                 int32_t* count, hipStream_t s);

@@ -315,9 +315,9 @@ void launch_to_nchw_f32(View iv, int n, int h, int w, int c, float* out, int dty
 // --------------------------------------------------------- classifier tail --
 // conv2 1x1 C->5 (no bias) -> AvgPool2d(5, 1, pool_pad) (count_include_pad:
 // divisor 25) -> view(-1, 5*ph*pw) in NCHW order -> Linear -> Softmax
-// (squeeze_ernet.py:33-41, ernet.py:38-45).  One 256-thread block per image.
+// (squeeze_ernet.py:33-41, ernet.py:38-45).  One 1024-thread block per image.
 template <typename T>
-__global__ __launch_bounds__(256) void cls_tail_kernel(const T* __restrict__ in, int h, int w, int c,
+__global__ __launch_bounds__(1024) void cls_tail_kernel(const T* __restrict__ in, int h, int w, int c,
                                                        const float* __restrict__ w2, int pool_pad, int ph, int pw,
                                                        const float* __restrict__ fcw, const float* __restrict__ fcb,
                                                        float* __restrict__ logits, float* __restrict__ probs) {
@@ -327,13 +327,23 @@ __global__ __launch_bounds__(256) void cls_tail_kernel(const T* __restrict__ in,
   const int b = blockIdx.x;
   const int hw = h * w;
   const T* src = in + (size_t)b * hw * c;
-  for (int t = threadIdx.x; t < 5 * hw; t += blockDim.x) {
-    const int o = t / hw, p = t - o * hw;
+  // conv2: one wave per pixel, lanes stride the channels (coalesced), wave sum
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int p = wid; p < hw; p += blockDim.x >> 6) {
     const T* x = src + (size_t)p * c;
-    const float* wr = w2 + (size_t)o * c;
-    float acc = 0.f;
-    for (int ch = 0; ch < c; ++ch) acc = fmaf(ldf(x + ch), wr[ch], acc);
-    conv[o * hw + p] = acc;
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int ch = lane; ch < c; ch += 64) {
+      const float xv = ldf(x + ch);
+#pragma unroll
+      for (int o = 0; o < 5; ++o) acc[o] = fmaf(xv, w2[(size_t)o * c + ch], acc[o]);
+    }
+#pragma unroll
+    for (int o = 0; o < 5; ++o) {
+      float v = acc[o];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) conv[o * hw + p] = v;
+    }
   }
   __syncthreads();
   const int nf = 5 * ph * pw;
@@ -377,10 +387,10 @@ void launch_cls_tail(const void* in, int n, int h, int w, int c, const float* w2
   RTDM_REQUIRE(h * w <= 64 && ph * pw <= 16, RTDM_E_UNSUPPORTED, "classifier tail: feature map too large");
   if (n <= 0) return;
   if (dtype == RTDM_F16)
-    hipLaunchKernelGGL(cls_tail_kernel<_Float16>, dim3(n), dim3(256), 0, s, (const _Float16*)in, h, w, c, w2,
+    hipLaunchKernelGGL(cls_tail_kernel<_Float16>, dim3(n), dim3(1024), 0, s, (const _Float16*)in, h, w, c, w2,
                        pool_pad, ph, pw, fcw, fcb, logits, probs);
   else
-    hipLaunchKernelGGL(cls_tail_kernel<float>, dim3(n), dim3(256), 0, s, (const float*)in, h, w, c, w2, pool_pad, ph,
+    hipLaunchKernelGGL(cls_tail_kernel<float>, dim3(n), dim3(1024), 0, s, (const float*)in, h, w, c, w2, pool_pad, ph,
                        pw, fcw, fcb, logits, probs);
   RTDM_HIP(hipGetLastError());
 }
@@ -741,6 +751,148 @@ __global__ __launch_bounds__(256) void resize_staged_kernel(const uint8_t* __res
   }
 }
 
+// Streaming form: one thread per output column, one block per (image, band of
+// kRsBand output rows).
+//   rows    the band's input rows (the crop's columns) stream by buffer->LDS
+//           DMA through a kRsRing-slot LDS ring, kRsDepth rows in flight;
+//   H pass  each thread keeps its column's horizontal taps in registers and
+//           writes the clip8'ed result of every input row (Pillow's uint8
+//           intermediate) as one packed dword into an LDS column image;
+//   V pass  per output row, taps unrolled with the band's coefficients staged in
+//           LDS (broadcast reads; zero weights past ymax read rows that exist in
+//           the padded image).
+// Integer sums are Pillow's (bit-exact: zero-weight taps add 0); no divisions,
+// one barrier per input row.
+constexpr int kRsBand = 16;   // output rows per block (= kResizeBand: ResizePlan::band_rows)
+constexpr int kRsTaps = 7;    // max taps per pass (ksize) held unrolled
+constexpr int kRsDepth = 6;   // input rows in flight (buffer->LDS) per wave
+constexpr int kRsRing = 8;    // LDS ring slots (>= kRsDepth + 2), power of two
+constexpr int kRsRowB = 2048; // ring slot bytes: 128 16-byte chunks (2 issuing waves)
+
+// ABL (diagnostic builds only, outputs wrong when non-zero): 1 = no H-pass LDS reads,
+// 2 = no V pass / output stores (one store per thread), 4 = no row DMA.
+template <typename T, int ABL>
+__global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __restrict__ frames, int in_h, int in_w,
+                                                            int row_first, int out, int kh_size, int kv_size,
+                                                            int col_first, int c0b, int v16, int band_rows,
+                                                            const int* __restrict__ bh, const int* __restrict__ ch,
+                                                            const int* __restrict__ bv, const int* __restrict__ cv,
+                                                            T* __restrict__ dst, int nchw) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t rsx_lds[];
+  const int rstride = kRsRowB;                             // ring slot (zero-weight taps may read past v16*16)
+  uint8_t* ring = rsx_lds;                                  // [kRsRing][kRsRowB]
+  uint32_t* himg = (uint32_t*)(rsx_lds + kRsRing * kRsRowB);  // [band_rows + kRsTaps][256] packed (r,g,b)
+  int* kv = (int*)(himg + (band_rows + kRsTaps) * 256);    // [kRsBand][kRsTaps]
+  const int bands = (out + kRsBand - 1) / kRsBand;
+  const int b = blockIdx.x / bands;
+  const int yy0 = (blockIdx.x - b * bands) * kRsBand;
+  const int nyy = out - yy0 < kRsBand ? out - yy0 : kRsBand;
+  const int r0 = bv[2 * yy0];
+  const int r1 = bv[2 * (yy0 + nyy - 1)] + bv[2 * (yy0 + nyy - 1) + 1];
+  const int xx = threadIdx.x;
+  const bool col = xx < out;
+  for (int i = xx; i < kRsBand * kRsTaps; i += 256) {
+    const int j = i / kRsTaps, t = i - j * kRsTaps;
+    kv[i] = j < nyy && t < bv[2 * (yy0 + j) + 1] && t < kv_size ? cv[(yy0 + j) * kv_size + t] : 0;
+  }
+  // rows past the band (read with zero weight) must hold finite data: zero them
+  for (int i = xx; i < kRsTaps * 256; i += 256) himg[(r1 - r0) * 256 + i] = 0u;
+  // this column's horizontal filter (zero weights past xmax)
+  int kx[kRsTaps];
+  int xoff;
+  {
+    const int xc = col ? xx : 0;
+    const int xmax = bh[2 * xc + 1];
+    xoff = (bh[2 * xc] - col_first) * 3 + (col_first * 3 - c0b);
+#pragma unroll
+    for (int t = 0; t < kRsTaps; ++t) kx[t] = (col && t < xmax && t < kh_size) ? ch[xc * kh_size + t] : 0;
+  }
+  const size_t rowb = (size_t)in_w * 3;
+  // Rows arrive by buffer->LDS DMA into a kRsRing-slot ring, kRsDepth rows ahead of
+  // the row being filtered.  Wave w's lane l carries 16-byte chunk 64w + l of a row
+  // (lanes past the row get an out-of-range offset: the DMA writes zeros).  The
+  // loads retire in order, so "row r landed" is one counted vmcnt per wave + a raw
+  // barrier.  Row r+kRsDepth goes to the slot last read for row r+kRsDepth-kRsRing
+  // <= r-2, released by row r-1's barrier.
+  typedef __attribute__((address_space(3))) void* lds_t;
+  const int wid = xx >> 6, chunk = xx;
+  const bool issuer = wid * 64 < v16;  // wave-uniform
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(frames + (size_t)b * in_h * rowb), 0, (int)(in_h * rowb), 0x00020000);
+  auto issue = [&](int r, int slot) {
+    if (issuer && !(ABL & 4)) {
+      const int rr = r < r1 ? r : r1 - 1;
+      const int vo = chunk < v16 ? (int)((row_first + rr) * rowb) + c0b + chunk * 16 : (int)0x80000000;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_t)(ring + slot * rstride + wid * 1024), 16, vo, 0, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < kRsDepth; ++q) issue(r0 + q, q);
+  int slot = 0, islot = kRsDepth;
+  for (int r = r0; r < r1; ++r) {
+    issue(r + kRsDepth, islot);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRsDepth) : "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const uint8_t* src = ring + slot * rstride + xoff;
+    int s0 = 1 << (kPrecisionBits - 1), s1 = s0, s2 = s0;
+    if constexpr ((ABL & 1) != 0) {
+      himg[(r - r0) * 256 + xx] = (uint32_t)(r + xx);
+    } else {
+#pragma unroll
+    for (int t = 0; t < kRsTaps; ++t) {
+      // bytes x non-negative 22-bit weights: 24-bit multiplies (full rate)
+      s0 += (int)__umul24(src[3 * t + 0], kx[t]);
+      s1 += (int)__umul24(src[3 * t + 1], kx[t]);
+      s2 += (int)__umul24(src[3 * t + 2], kx[t]);
+    }
+    himg[(r - r0) * 256 + xx] = (uint32_t)clip8(s0) | ((uint32_t)clip8(s1) << 8) | ((uint32_t)clip8(s2) << 16);
+    }
+    slot = (slot + 1) & (kRsRing - 1);
+    islot = (islot + 1) & (kRsRing - 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!col) return;
+  if constexpr ((ABL & 2) != 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < r1 - r0; ++i) acc += himg[i * 256 + xx];
+    dst[((size_t)b * out + yy0) * out * 3 + xx] = (T)(float)acc;
+    return;
+  }
+  const float mean[3] = {0.485f, 0.456f, 0.406f};
+  const float stdv[3] = {0.229f, 0.224f, 0.225f};
+#pragma unroll
+  for (int j = 0; j < kRsBand; ++j) {
+    if (j < nyy) {
+      const int yy = yy0 + j;
+      const uint32_t* hp = himg + (bv[2 * yy] - r0) * 256 + xx;
+      int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+#pragma unroll
+      for (int t = 0; t < kRsTaps; ++t) {
+        const uint32_t hv = hp[t * 256];
+        const int k = kv[j * kRsTaps + t];
+        a0 += (int)__umul24(hv & 255u, k);
+        a1 += (int)__umul24((hv >> 8) & 255u, k);
+        a2 += (int)__umul24(hv >> 16, k);
+      }
+      const int av[3] = {a0, a1, a2};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float v = ((float)clip8(av[c]) / 255.f - mean[c]) / stdv[c];
+        if (nchw)
+          dst[(((size_t)b * 3 + c) * out + yy) * out + xx] = (T)v;
+        else
+          dst[(((size_t)b * out + yy) * out + xx) * 3 + c] = (T)v;
+      }
+    }
+  }
+}
+
+static int g_resize_stream = 1;
+int resize_stream_mode() { return g_resize_stream; }
+void set_resize_stream_mode(int v) { g_resize_stream = v; }
+
 // LDS of the staged kernel: coefficients + bounds + band source rows + band tmp rows.
 static size_t resize_staged_lds(const ResizePlan& p, int col_bytes16) {
   return (size_t)p.out * p.ksize_h * 4 + (size_t)p.out * 2 * 4 + (size_t)p.band_rows8 * col_bytes16 +
@@ -760,6 +912,30 @@ void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_
   const bool rows16 = (p.in_w * 3) % 16 == 0 && ((uintptr_t)frames & 15) == 0 &&
                       c0b + col_bytes16 <= p.in_w * 3;
   const size_t slds = resize_staged_lds(p, col_bytes16);
+  if (rows16 && resize_stream_mode() && p.out <= 256 && p.ksize_h <= kRsTaps && p.ksize_v <= kRsTaps &&
+      col_bytes16 + 32 <= kRsRowB && (int64_t)p.in_h * p.in_w * 3 < (1ll << 31)) {
+    const int v16 = col_bytes16 / 16;
+    const size_t lds = (size_t)kRsRing * kRsRowB + (size_t)(p.band_rows + kRsTaps) * 256 * 4 + kRsBand * kRsTaps * 4;
+    const int blocks = n * ((p.out + kRsBand - 1) / kRsBand);
+    const int m = resize_stream_mode();
+    if (m > 1 && !(out_layout == 1 || dtype == RTDM_F32)) {  // diagnostic ablations (tools/ab_cls.py)
+      auto k = m == 2 ? resize_stream_kernel<_Float16, 1> : m == 3 ? resize_stream_kernel<_Float16, 2>
+             : m == 4 ? resize_stream_kernel<_Float16, 4> : resize_stream_kernel<_Float16, 7>;
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, s, frames, p.in_h, p.in_w, p.row_first, p.out, p.ksize_h,
+                         p.ksize_v, p.col_first, c0b, v16, p.band_rows, p.bounds_h.as<int>(), p.coef_h.as<int>(),
+                         p.bounds_v.as<int>(), p.coef_v.as<int>(), (_Float16*)out, 0);
+    } else if (out_layout == 1 || dtype == RTDM_F32)
+      hipLaunchKernelGGL((resize_stream_kernel<float, 0>), dim3(blocks), dim3(256), lds, s, frames, p.in_h, p.in_w,
+                         p.row_first, p.out, p.ksize_h, p.ksize_v, p.col_first, c0b, v16, p.band_rows, p.bounds_h.as<int>(),
+                         p.coef_h.as<int>(), p.bounds_v.as<int>(), p.coef_v.as<int>(), (float*)out,
+                         out_layout == 1 ? 1 : 0);
+    else
+      hipLaunchKernelGGL((resize_stream_kernel<_Float16, 0>), dim3(blocks), dim3(256), lds, s, frames, p.in_h, p.in_w,
+                         p.row_first, p.out, p.ksize_h, p.ksize_v, p.col_first, c0b, v16, p.band_rows, p.bounds_h.as<int>(),
+                         p.coef_h.as<int>(), p.bounds_v.as<int>(), p.coef_v.as<int>(), (_Float16*)out, 0);
+    RTDM_HIP(hipGetLastError());
+    return;
+  }
   if (rows16 && slds <= 64 * 1024) {
     const int blocks = n * ((p.out + kResizeBandS - 1) / kResizeBandS);
     if (out_layout == 1 || dtype == RTDM_F32)
@@ -926,6 +1102,8 @@ void launch_yolo_trt(const float* in, int n, const TrtYoloArgs& t, int nchw, flo
 static constexpr int kNmsThreads = 1024;
 static constexpr int kNmsLdsCap = 4096;
 static constexpr int kNmsMaskCap = 512;  // LDS IoU-bitmask path: n * ceil(n/64) * 8 B <= 32 KiB
+static constexpr int kNmsMaskCapG = 2048;  // workspace bitmask, scanned through LDS in chunks
+static constexpr int kNmsRankCap = 2048;   // rank sort up to this many candidates
 
 struct NmsWs {  // per-image slice of the workspace
   uint64_t* keys;
@@ -933,7 +1111,13 @@ struct NmsWs {  // per-image slice of the workspace
   float* area;
   uint32_t* supp;
   int* keep;
+  uint64_t* seg;  // candidate keys of anchor block k at seg + k * kNmsCandBlk * npa
+  int* segcnt;    // [n_anchors / kNmsCandBlk] candidates per anchor block
+  uint64_t* mask; // IoU bitmask [m][m/64], m = min(cap, kNmsMaskCapG)
 };
+
+// Candidate pass: one kNmsCandBlk-thread block per (image, anchor block).
+static constexpr int kNmsCandBlk = 256;
 
 static inline size_t nms_cap(int n_anchors, int nc) {
   size_t c = 1;
@@ -941,29 +1125,93 @@ static inline size_t nms_cap(int n_anchors, int nc) {
   return c < 64 ? 64 : c;
 }
 
-size_t nms_workspace_size(int n, int n_anchors, int nc) {
-  const size_t cap = nms_cap(n_anchors, nc);
-  const size_t per = cap * (8 + 16 + 4 + 4) + (cap / 32 + 1) * 4 + 256;
-  return per * (size_t)n;
+__host__ __device__ inline int nms_nblk(int n_anchors) { return (n_anchors + kNmsCandBlk - 1) / kNmsCandBlk; }
+
+__host__ __device__ inline size_t nms_per_image(size_t cap, int n_anchors, int nc) {
+  const size_t npa = nc > 1 ? nc : 1;
+  const size_t m = cap < (size_t)kNmsMaskCapG ? cap : (size_t)kNmsMaskCapG;
+  return cap * (8 + 16 + 4 + 4) + (cap / 32 + 1) * 4 + 256 +
+         round_up((int64_t)nms_nblk(n_anchors) * (kNmsCandBlk * npa * 8 + 4), 256) + m * (m / 64) * 8;
 }
 
-__device__ __forceinline__ NmsWs nms_ws(void* ws, int img, size_t cap) {
-  const size_t per = cap * (8 + 16 + 4 + 4) + (cap / 32 + 1) * 4 + 256;
-  char* base = (char*)ws + per * img;
+size_t nms_workspace_size(int n, int n_anchors, int nc) {
+  return nms_per_image(nms_cap(n_anchors, nc), n_anchors, nc) * (size_t)n;
+}
+
+__device__ __forceinline__ NmsWs nms_ws(void* ws, int img, size_t cap, int n_anchors, int nc) {
+  char* base = (char*)ws + nms_per_image(cap, n_anchors, nc) * img;
   NmsWs w;
   w.keys = (uint64_t*)base;
   w.box = (float4*)(base + cap * 8);
   w.area = (float*)(base + cap * 24);
   w.keep = (int*)(base + cap * 28);
   w.supp = (uint32_t*)(base + cap * 32);
+  char* sb = base + cap * 32 + (cap / 32 + 1) * 4 + 256;
+  w.seg = (uint64_t*)sb;
+  w.segcnt = (int*)(sb + (size_t)nms_nblk(n_anchors) * kNmsCandBlk * (nc > 1 ? nc : 1) * 8);
+  w.mask = (uint64_t*)(sb + round_up((int64_t)nms_nblk(n_anchors) * (kNmsCandBlk * (nc > 1 ? nc : 1) * 8 + 4), 256));
   return w;
+}
+
+// 1. candidates (utils.py:505-536), spread over the whole chip: each block filters
+// kNmsCandBlk anchors of one image and writes its keys to its own segment (+ count).
+__global__ __launch_bounds__(kNmsCandBlk) void nms_cand_kernel(const float* __restrict__ io, int n_anchors, int no,
+                                                               float conf, int multi_label, uint64_t class_mask,
+                                                               void* ws, size_t cap) {
+  __shared__ int s_n;
+  const int img = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
+  const int nc = no - 5;
+  const bool ml = multi_label && nc > 1;
+  const int npa = nc > 1 ? nc : 1;
+  NmsWs g = nms_ws(ws, img, cap, n_anchors, nc);
+  uint64_t* seg = g.seg + (size_t)blk * kNmsCandBlk * npa;
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+  const int a = blk * kNmsCandBlk + tid;
+  if (a < n_anchors) {
+    const float* r = io + ((size_t)img * n_anchors + a) * no;
+    const float obj = r[4];
+    const float w = r[2], h = r[3];
+    if ((obj > conf) && (w > 2.f) && (h > 2.f) && (w < 4096.f) && (h < 4096.f)) {
+      const float x = r[0], y = r[1];
+      const float hw = w / 2.f, hh = h / 2.f;
+      const bool box_finite = isfinite(x - hw) && isfinite(y - hh) && isfinite(x + hw) && isfinite(y + hh);
+      if (ml) {
+        for (int j = 0; j < nc; ++j) {
+          const float sc = r[5 + j] * obj;
+          if (!(sc > conf)) continue;
+          if (!((class_mask >> (j & 63)) & 1ull)) continue;
+          if (!box_finite || !isfinite(sc)) continue;
+          seg[atomicAdd(&s_n, 1)] = ((uint64_t)(~__float_as_uint(sc)) << 32) | (uint32_t)(a * nc + j);
+        }
+      } else {
+        float best = r[5] * obj;
+        int bj = 0;
+        for (int j = 1; j < nc; ++j) {
+          const float sc = r[5 + j] * obj;
+          if (sc > best) { best = sc; bj = j; }
+        }
+        if (((class_mask >> (bj & 63)) & 1ull) && box_finite && isfinite(best))
+          seg[atomicAdd(&s_n, 1)] = ((uint64_t)(~__float_as_uint(best)) << 32) | (uint32_t)(a * npa + bj);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) g.segcnt[blk] = s_n;
+}
+
+// 64-bit readlane (the builtin returns a signed int: widen it as unsigned)
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restrict__ io, int n_anchors, int no,
                                                           float conf, double iou_thr, int multi_label, int agnostic,
                                                           uint64_t class_mask, int max_det, void* ws, size_t cap,
                                                           float* __restrict__ det, int32_t* __restrict__ idx_out,
-                                                          int32_t* __restrict__ count) {
+                                                          int32_t* __restrict__ count, int variant) {
 #pragma clang fp contract(off)
   __shared__ uint64_t s_keys[kNmsLdsCap];
   __shared__ float4 s_box[kNmsLdsCap];
@@ -974,58 +1222,102 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
   const int img = blockIdx.x;
   const int tid = threadIdx.x;
   const int nc = no - 5;
-  const bool ml = multi_label && nc > 1;
   const float* P = io + (size_t)img * n_anchors * no;
-  NmsWs g = nms_ws(ws, img, cap);
-  if (tid == 0) s_n = 0;
-  __syncthreads();
+  NmsWs g = nms_ws(ws, img, cap, n_anchors, nc);
+  // phase timestamps (100 MHz s_memrealtime) in the slice's slack bytes: diagnostics
+  // for tools/nms_phases.py, 8 stores per image
+  uint64_t* stamps = (uint64_t*)((char*)g.supp + (cap / 32 + 1) * 4);
+#define NMS_STAMP(k) \
+  if (tid == 0) stamps[k] = __builtin_amdgcn_s_memrealtime()
+  NMS_STAMP(0);
+  __shared__ int s_off[kNmsThreads + 1];  // candidate offset of each anchor block (nms_cand_kernel)
+  __shared__ int s_wsum[kNmsThreads / 64];
 
-  // 1. candidates (utils.py:505-536)
-  for (int a = tid; a < n_anchors; a += kNmsThreads) {
-    const float* r = P + (size_t)a * no;
-    const float obj = r[4];
-    if (!(obj > conf)) continue;
-    const float w = r[2], h = r[3];
-    if (!((w > 2.f) && (h > 2.f) && (w < 4096.f) && (h < 4096.f))) continue;
-    const float x = r[0], y = r[1];
-    const float hw = w / 2.f, hh = h / 2.f;
-    const bool box_finite = isfinite(x - hw) && isfinite(y - hh) && isfinite(x + hw) && isfinite(y + hh);
-    if (ml) {
-      for (int j = 0; j < nc; ++j) {
-        const float sc = r[5 + j] * obj;
-        if (!(sc > conf)) continue;
-        if (!((class_mask >> (j & 63)) & 1ull)) continue;
-        if (!box_finite || !isfinite(sc)) continue;
-        const int pos = atomicAdd(&s_n, 1);
-        g.keys[pos] = ((uint64_t)(~__float_as_uint(sc)) << 32) | (uint32_t)(a * nc + j);
+  // 1b. gather the anchor blocks' candidate segments (any order: the sort decides)
+  const int nblk = nms_nblk(n_anchors);
+  const int npa = nc > 1 ? nc : 1;
+  int n = 0;
+  for (int b0 = 0; b0 < nblk; b0 += kNmsThreads) {
+    const int nb = nblk - b0 < kNmsThreads ? nblk - b0 : kNmsThreads;
+    {  // exclusive offsets: wave-level inclusive scans + a scan of the 16 wave totals
+      int v = tid < nb ? g.segcnt[b0 + tid] : 0;
+      const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(v, d);
+        if (lane >= d) v += u;
       }
-    } else {
-      float best = r[5] * obj;
-      int bj = 0;
-      for (int j = 1; j < nc; ++j) {
-        const float sc = r[5 + j] * obj;
-        if (sc > best) { best = sc; bj = j; }
+      if (lane == 63) s_wsum[wv] = v;
+      __syncthreads();
+      if (tid == 0) {
+        int acc = 0;
+        for (int k = 0; k < kNmsThreads / 64; ++k) {
+          const int t = s_wsum[k];
+          s_wsum[k] = acc;
+          acc += t;
+        }
       }
-      if (!((class_mask >> (bj & 63)) & 1ull)) continue;
-      if (!box_finite || !isfinite(best)) continue;
-      const int pos = atomicAdd(&s_n, 1);
-      g.keys[pos] = ((uint64_t)(~__float_as_uint(best)) << 32) | (uint32_t)(a * (nc > 1 ? nc : 1) + bj);
+      __syncthreads();
+      s_off[tid + 1] = v + s_wsum[wv];
+      if (tid == 0) s_off[0] = 0;
+      __syncthreads();
     }
+    const int tot = s_off[nb];
+    const bool lds_keys = n + tot <= kNmsLdsCap;  // uniform
+    for (int i = tid; i < tot; i += kNmsThreads) {
+      int lo = 0, hi = nb - 1;  // segment k with s_off[k] <= i < s_off[k+1]
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= i) lo = mid; else hi = mid - 1;
+      }
+      const uint64_t key = g.seg[(size_t)(b0 + lo) * kNmsCandBlk * npa + (i - s_off[lo])];
+      g.keys[n + i] = key;
+      if (lds_keys) s_keys[n + i] = key;
+    }
+    n += tot;
+    __syncthreads();
   }
-  __syncthreads();
-  const int n = s_n;
+  NMS_STAMP(1);
   int npow = 1;
   while (npow < n) npow <<= 1;
   const bool lds = npow <= kNmsLdsCap;
   uint64_t* K = lds ? s_keys : g.keys;
-  for (int i = tid; i < npow; i += kNmsThreads) {
-    uint64_t v = i < n ? g.keys[i] : ~0ull;
-    if (lds) s_keys[i] = v;
-    else if (i >= n) g.keys[i] = v;
-  }
+  for (int i = n + tid; i < npow; i += kNmsThreads) K[i] = ~0ull;  // sort padding
   __syncthreads();
 
-  // 2. bitonic sort, ascending key
+  // 2. sort, ascending key: bitonic network (diagnostic variant bit 0: rank sort —
+  // keys are unique, a key's rank = count of smaller keys; measured slower here).
+  if (n <= kNmsRankCap && (variant & 1)) {
+    uint64_t mine[kNmsRankCap / kNmsThreads];
+    int rk[kNmsRankCap / kNmsThreads];
+#pragma unroll
+    for (int q = 0; q < kNmsRankCap / kNmsThreads; ++q) {
+      const int i = tid + q * kNmsThreads;
+      mine[q] = i < n ? K[i] : ~0ull;
+      rk[q] = 0;
+    }
+    // 8 broadcast reads in flight per step (the loop is LDS-latency bound)
+    int j = 0;
+    for (; j + 8 <= n; j += 8) {
+      uint64_t kj[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) kj[u] = K[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int q = 0; q < kNmsRankCap / kNmsThreads; ++q) rk[q] += kj[u] < mine[q] ? 1 : 0;
+    }
+    for (; j < n; ++j) {
+      const uint64_t kj = K[j];
+#pragma unroll
+      for (int q = 0; q < kNmsRankCap / kNmsThreads; ++q) rk[q] += kj < mine[q] ? 1 : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kNmsRankCap / kNmsThreads; ++q)
+      if (tid + q * kNmsThreads < n) K[rk[q]] = mine[q];
+    __syncthreads();
+  } else
   for (int k = 2; k <= npow; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int i = tid; i < npow; i += kNmsThreads) {
@@ -1043,6 +1335,7 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
     }
   }
 
+  NMS_STAMP(2);
   // 3. offset boxes + areas (utils.py:547-552; torchvision areas)
   float4* B = lds ? s_box : g.box;
   float* A = lds ? s_area : g.area;
@@ -1065,14 +1358,22 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
   for (int i = tid; i < (n + 31) / 32; i += kNmsThreads) S[i] = 0u;
   __syncthreads();
 
+  NMS_STAMP(3);
   // 4. greedy suppression.
   // n <= kNmsMaskCap: the torchvision-CUDA formulation — every (i, 64-column
   // word) IoU bitmask in parallel into LDS, then one wave scans candidates in
   // score order, OR-ing the masks of kept boxes (no workgroup barrier per
   // candidate).  Same IoU arithmetic and the same keep set as the greedy loop.
+  // kNmsMaskCap < n <= kNmsMaskCapG: the same bitmask in the workspace, scanned in
+  // chunks of rows staged through the LDS mask buffer.
   int nkeep = 0;
-  if (n <= kNmsMaskCap) {
+  if (n <= ((variant & 2) ? -1 : kNmsMaskCapG)) {
     const int W = (n + 63) >> 6;
+    const bool in_lds = n <= kNmsMaskCap;
+    uint64_t* M = in_lds ? s_mask : g.mask;
+    // one wave per (row i, 64-column word w): lane = column j, the word is a ballot
+    // one (row i, 64-column word w) per thread; the division only where boxes meet
+    const bool thr_nonneg = iou_thr >= 0.0;
     for (int p = tid; p < n * W; p += kNmsThreads) {
       const int i = p / W, w = p - (p / W) * W;
       const float4 bi = B[i];
@@ -1089,27 +1390,61 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
         const float w2 = fmaxf(0.f, xx2 - xx1);
         const float h2 = fmaxf(0.f, yy2 - yy1);
         const float inter = w2 * h2;
-        const float ovr = inter / ((ai + A[j]) - inter);
-        if ((double)ovr > iou_thr) bits |= 1ull << (j - j0);
+        if (inter > 0.f || !thr_nonneg) {  // inter == 0: IoU 0 is never > a threshold >= 0
+          const float ovr = inter / ((ai + A[j]) - inter);
+          if ((double)ovr > iou_thr) bits |= 1ull << (j - j0);
+        }
       }
-      s_mask[p] = bits;
+      M[p] = bits;
     }
     __syncthreads();
-    if (tid < 64) {
-      uint64_t removed = 0;  // lane l < W holds word l
-      int nk = 0;
-      for (int i = 0; i < n; ++i) {
-        const int wi = i >> 6;
-        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)removed, wi);
-        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(removed >> 32), wi);
-        const uint64_t word = ((uint64_t)hi << 32) | lo;
-        if ((word >> (i & 63)) & 1ull) continue;
-        if (tid == 0) g.keep[nk] = i;
-        ++nk;
-        if (tid < W) removed |= s_mask[i * W + tid];
+    NMS_STAMP(4);
+    // rows per LDS chunk: whole 64-candidate words
+    const int rows = in_lds ? n : ((kNmsMaskCap * (kNmsMaskCap / 64)) / W) & ~63;
+    uint64_t removed = 0;  // wave 0: lane l < W holds word l of the suppressed set
+    int nk = 0;
+    for (int c0 = 0; c0 < n; c0 += rows) {
+      const int c1 = c0 + rows < n ? c0 + rows : n;
+      if (!in_lds) {
+        for (int p = tid; p < (c1 - c0) * W; p += kNmsThreads) s_mask[p] = g.mask[(size_t)c0 * W + p];
+        __syncthreads();
       }
-      if (tid == 0) s_n = nk;
+      if (tid < 64) {
+        // word by word: the in-word greedy pass on scalars (lane b holds row 64w+b's
+        // bits of word w), then every kept row's mask ORed into the later words
+        for (int w = c0 >> 6; w * 64 < c1; ++w) {
+          const int cnt = c1 - w * 64 < 64 ? c1 - w * 64 : 64;
+          const int i = w * 64 + tid;
+          const uint64_t mw = tid < cnt ? s_mask[(i - c0) * W + w] : 0ull;
+          uint64_t rem = readlane_u64(removed, w);
+          uint64_t kept = 0;
+          for (int b = 0; b < cnt; ++b) {
+            if ((rem >> b) & 1ull) continue;
+            kept |= 1ull << b;
+            rem |= readlane_u64(mw, b);
+          }
+          if ((kept >> tid) & 1ull) g.keep[nk + __popcll(kept & ((1ull << tid) - 1ull))] = i;
+          nk += __popcll(kept);
+          // kept rows' masks into the later words, 8 rows (LDS reads) in flight per step
+          const int tl = tid < W ? tid : W - 1;
+          for (uint64_t k = kept; k;) {
+            int bs[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              bs[u] = k ? __builtin_ctzll(k) : -1;
+              k &= k - 1;
+            }
+            uint64_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = s_mask[(w * 64 + (bs[u] < 0 ? bs[0] : bs[u]) - c0) * W + tl];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) removed |= bs[u] >= 0 ? v[u] : 0ull;
+          }
+        }
+      }
+      __syncthreads();  // the chunk's LDS rows are consumed before the next chunk lands
     }
+    if (tid == 0) s_n = nk;
     __syncthreads();
     nkeep = s_n;
   } else {
@@ -1137,6 +1472,7 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
   }
   __syncthreads();  // g.keep written by wave 0 / thread 0 -> read by all below
 
+  NMS_STAMP(5);
   // 5. rows [x1,y1,x2,y2,conf,cls] in kept (descending score) order
   const int nout = nkeep < max_det ? nkeep : max_det;
   for (int r = tid; r < nout; r += kNmsThreads) {
@@ -1159,8 +1495,12 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
     }
   }
   if (tid == 0) count[img] = nkeep;
+  NMS_STAMP(6);
+#undef NMS_STAMP
 }
 
+static int g_nms_variant = 0;
+void set_nms_variant(int v) { g_nms_variant = v; }
 void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label, int agnostic,
                 uint64_t class_mask, int max_det, void* ws, float* det, int32_t* idx, int32_t* count,
                 hipStream_t s) {
@@ -1168,8 +1508,10 @@ void launch_nms(const float* io, int n, int n_anchors, int no, float conf, doubl
   RTDM_REQUIRE(no >= 6, RTDM_E_INVALID, "nms: no must be >= 6 (5 + nc)");
   RTDM_REQUIRE(max_det >= 0, RTDM_E_INVALID, "nms: max_det < 0");
   const size_t cap = nms_cap(n_anchors, no - 5);
+  hipLaunchKernelGGL(nms_cand_kernel, dim3(nms_nblk(n_anchors), n), dim3(kNmsCandBlk), 0, s, io, n_anchors, no, conf,
+                     multi_label, class_mask, ws, cap);
   hipLaunchKernelGGL(nms_kernel, dim3(n), dim3(kNmsThreads), 0, s, io, n_anchors, no, conf, iou, multi_label,
-                     agnostic, class_mask, max_det, ws, cap, det, idx, count);
+                     agnostic, class_mask, max_det, ws, cap, det, idx, count, g_nms_variant);
   RTDM_HIP(hipGetLastError());
 }
 
