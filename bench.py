@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--conf", type=float, default=0.3)
     ap.add_argument("--iou", type=float, default=0.4)
     ap.add_argument("--max-det", type=int, default=300)
+    ap.add_argument("--overlap", type=int, default=1,
+                    help="1: classifier on a side stream beside the detector; 0: both stages serial")
+    ap.add_argument("--priority", type=int, default=0,
+                    help="1: detector + NMS on a high-priority stream, classifier on a low-priority one")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU oracle leg")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="CPU oracle leg: time chunks of 16 frames until this much CPU time has passed")
@@ -112,7 +116,8 @@ def build(args, world, rank):
     if args.dtype == "f16":
         det.half()
         cls.half()
-    pipe = TwoStagePipeline(cls, det, args.conf, args.iou, args.max_det)
+    pipe = TwoStagePipeline(cls, det, args.conf, args.iou, args.max_det, overlap=bool(args.overlap),
+                            priority=bool(args.priority))
     return pipe, det, cls, text, stream, sd
 
 

@@ -183,6 +183,9 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
 bool conv_pipe_ok(const ConvArgs& a);
 void launch_conv_pipe(const ConvArgs& a, hipStream_t s);
 int conv_pipe_mode();
+// diagnostics: conv_stem3 ablation builds (tools/ab_conv.py --key stem_abl)
+int stem_abl();
+void set_stem_abl(int v);
 void set_conv_pipe_mode(int v);
 // detector.cpp: plan conv -> 1x1 head -> [yolo] as one fused launch (default 1)
 int fuse_head();

@@ -209,22 +209,27 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_f16(ConvArgs a) {
 // One block = kStemRows output rows of one image, 4 waves stride over the
 // 16-pixel tiles of those rows.
 // --------------------------------------------------------------------------
-constexpr int kStemRows = 4;
+constexpr int kStemRows = 4;      // output rows per block, plain stem
+constexpr int kStemRowsPool = 4;  // output rows per block, pooled stem (2 waves per quad row; 8 measured slower)
+__host__ __device__ constexpr int stem_rows(bool pool) { return pool ? kStemRowsPool : kStemRows; }
 
 __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
   const _Float16 ha = (_Float16)a, hb = (_Float16)b;
   return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
 }
 
-template <bool POOL, int NTN>
+// ABL (diagnostic builds only, outputs wrong when non-zero): 1 = no frame loads,
+// 2 = no output stores, 4 = no MFMA.
+template <bool POOL, int NTN, int ABL = 0>
 __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint2 stem_lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int s = a.stride, pad = a.pad;
-  const int bpi = (a.oh + kStemRows - 1) / kStemRows;
+  constexpr int ROWS = stem_rows(POOL);
+  const int bpi = (a.oh + ROWS - 1) / ROWS;
   const int n = blockIdx.x / bpi;
-  const int oy0 = (blockIdx.x - n * bpi) * kStemRows;
-  const int nrows = (kStemRows - 1) * s + 3;
+  const int oy0 = (blockIdx.x - n * bpi) * ROWS;
+  const int nrows = (ROWS - 1) * s + 3;
   const int cols = (a.ow - 1) * s - pad + 5;  // LDS column = x + 1, x in [-1, (ow-1)*s - pad + 3]
   const int iy0 = oy0 * s - pad;
   const int H = a.ih, W = a.iw;
@@ -232,11 +237,11 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
   // ---- stage the input rows iy0 .. iy0+nrows-1 (fp16, 4 channels / pixel) ----
   if (a.in_kind == IN_FRAME_U8 && (W & 3) == 0 && cols >= W + 1) {
     const int gpr = W >> 2;  // 4-pixel groups per row (12 bytes)
-    for (int idx = tid; idx < nrows * gpr; idx += 256) {
-      const int r = idx / gpr, g = idx - r * gpr;
+    for (int r = 0; r < nrows; ++r)
+    for (int g = tid; g < gpr; g += 256) {
       const int y = iy0 + r;
       uint32_t d0 = 0, d1 = 0, d2 = 0;
-      if ((unsigned)y < (unsigned)H) {
+      if ((unsigned)y < (unsigned)H && !(ABL & 1)) {
         const uint32_t* src = (const uint32_t*)((const uint8_t*)a.in + ((size_t)(n * H + y) * W + 4 * g) * 3);
         d0 = src[0];
         d1 = src[1];
@@ -250,9 +255,10 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
       for (int p = 0; p < 4; ++p)
         dst[p] = make_uint2(pack_h2((float)b[3 * p], (float)b[3 * p + 1]), pack_h2((float)b[3 * p + 2], 0.f));
     }
-    for (int idx = tid; idx < nrows * cols; idx += 256) {  // padding columns
-      const int r = idx / cols, lc = idx - r * cols;
-      if (lc == 0 || lc > W) stem_lds[r * cols + lc] = make_uint2(0u, 0u);
+    const int npad = cols - W;  // LDS column 0 and columns W+1 .. cols-1 are padding
+    for (int idx = tid; idx < nrows * npad; idx += 256) {
+      const int r = idx / npad, k = idx - r * npad;
+      stem_lds[r * cols + (k == 0 ? 0 : W + k)] = make_uint2(0u, 0u);
     }
   } else {
     for (int idx = tid; idx < nrows * cols; idx += 256) {
@@ -315,8 +321,9 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
   };
   const int kh0 = g >> 1, pr0 = g & 1;
   if (POOL) {
-    // waves 0,1 -> quad row 0, waves 2,3 -> quad row 1 (kStemRows == 4); a wave's
+    // waves 0,1 -> quad row 0, waves 2,3 -> quad row 1 (ROWS == 4); a wave's
     // tiles are 4 consecutive quads, striding by 2 tiles.
+    static_assert(!POOL || ROWS == 4, "two waves per quad row");
     const int qw = a.ow >> 1, qh = a.oh >> 1;
     const int tr = wid >> 1;
     const int py = (oy0 >> 1) + tr;
@@ -338,20 +345,25 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
       const int oq = tx * 4 + g;  // pooled x of this lane's output quad
 #pragma unroll
       for (int t = 0; t < NTN; ++t) {
-        f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf0, wa[t][0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1, wa[t][1], acc, 0, 0, 0);
+        f4 acc;
+        if constexpr ((ABL & 4) != 0) {
+          acc = f4{(float)bf0[0], (float)bf0[1], (float)bf1[2], (float)bf1[3]};
+        } else {
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf0, wa[t][0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1, wa[t][1], acc, 0, 0, 0);
+        }
         // bias, LeakyReLU/linear and the positive 1/255 scale are monotone non-decreasing
         // (and so is their fp32 rounding): pool first, then one epilogue per quad
         const float m = e.scale || act == ACT_SWISH
                             ? fmaxf(fmaxf(epi(acc[0], t, 0), epi(acc[1], t, 0)), fmaxf(epi(acc[2], t, 0), epi(acc[3], t, 0)))
                             : epi(fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])), t, 0);
         const int c = 16 * t + p;
-        if (oq < qw && c < a.cout) pool_row[(size_t)oq * e.pool.cs + c] = (_Float16)m;
+        if (oq < qw && c < a.cout && (!(ABL & 2) || m == 12345.f)) pool_row[(size_t)oq * e.pool.cs + c] = (_Float16)m;
       }
     }
   } else {
     const int tiles_x = (a.ow + 15) >> 4;
-    const int ntiles = tiles_x * kStemRows;
+    const int ntiles = tiles_x * ROWS;
     for (int t = wid; t < ntiles; t += 4) {
       const int tr = t / tiles_x, tx = t - tr * tiles_x;
       const int oy = oy0 + tr;
@@ -391,7 +403,7 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
 }
 
 static size_t stem3_lds_bytes(const ConvArgs& a) {
-  const int nrows = (kStemRows - 1) * a.stride + 3;
+  const int nrows = (stem_rows(a.quad != 0) - 1) * a.stride + 3;
   const int cols = (a.ow - 1) * a.stride - a.pad + 5;
   return (size_t)nrows * cols * sizeof(uint2);
 }
@@ -1215,6 +1227,9 @@ static bool stem_ok(const ConvArgs& a) {
 // Pipelined 256x128 kernel (conv_pipe.hip) for the Cin % 64 == 0 layers; 0 = off
 // (conv_glds_f16 takes them).  RTDM_CONV_PIPE in the environment, or
 // rtdm_set_tuning("conv_pipe", v), for A/B runs.
+static int g_stem_abl = 0;
+int stem_abl() { return g_stem_abl; }
+void set_stem_abl(int v) { g_stem_abl = v; }
 static int g_conv_pipe = -1;
 int conv_pipe_mode() {
   if (g_conv_pipe < 0) {
@@ -1264,11 +1279,17 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
   RTDM_REQUIRE(!a.quad || (a.oh >= 2 && a.ow >= 2), RTDM_E_INVALID, "conv: quad ordering needs >= 2x2 output");
   RTDM_REQUIRE(!a.e.pool.ptr || a.quad, RTDM_E_INVALID, "conv: pooled output needs quad ordering");
   if (dtype == RTDM_F16 && stem_ok(a)) {
-    const int blocks = a.n * ((a.oh + kStemRows - 1) / kStemRows);
+    const int rows = stem_rows(a.quad != 0);
+    const int blocks = a.n * ((a.oh + rows - 1) / rows);
     const size_t lds = stem3_lds_bytes(a);
     const int ntn = a.cout_pad / 16;
     if (a.quad) {
-      if (ntn == 1) hipLaunchKernelGGL((conv_stem3<true, 1>), dim3(blocks), dim3(256), lds, s, a);
+      const int abl = stem_abl();
+      if (ntn == 1 && abl == 1) hipLaunchKernelGGL((conv_stem3<true, 1, 1>), dim3(blocks), dim3(256), lds, s, a);
+      else if (ntn == 1 && abl == 2) hipLaunchKernelGGL((conv_stem3<true, 1, 2>), dim3(blocks), dim3(256), lds, s, a);
+      else if (ntn == 1 && abl == 4) hipLaunchKernelGGL((conv_stem3<true, 1, 4>), dim3(blocks), dim3(256), lds, s, a);
+      else if (ntn == 1 && abl == 7) hipLaunchKernelGGL((conv_stem3<true, 1, 7>), dim3(blocks), dim3(256), lds, s, a);
+      else if (ntn == 1) hipLaunchKernelGGL((conv_stem3<true, 1>), dim3(blocks), dim3(256), lds, s, a);
       else if (ntn == 2) hipLaunchKernelGGL((conv_stem3<true, 2>), dim3(blocks), dim3(256), lds, s, a);
       else hipLaunchKernelGGL((conv_stem3<true, 4>), dim3(blocks), dim3(256), lds, s, a);
     } else {

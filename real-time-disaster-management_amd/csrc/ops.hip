@@ -791,6 +791,15 @@ __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __res
   const int r1 = bv[2 * (yy0 + nyy - 1)] + bv[2 * (yy0 + nyy - 1) + 1];
   const int xx = threadIdx.x;
   const bool col = xx < out;
+  // ToTensor + Normalize of the 256 possible uint8 values, per channel: the same
+  // float expression as the per-pixel form, evaluated once per block
+  float* lut = (float*)(kv + kRsBand * kRsTaps);  // [3][256]
+  {
+    const float mean[3] = {0.485f, 0.456f, 0.406f};
+    const float stdv[3] = {0.229f, 0.224f, 0.225f};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) lut[c * 256 + xx] = ((float)xx / 255.f - mean[c]) / stdv[c];
+  }
   for (int i = xx; i < kRsBand * kRsTaps; i += 256) {
     const int j = i / kRsTaps, t = i - j * kRsTaps;
     kv[i] = j < nyy && t < bv[2 * (yy0 + j) + 1] && t < kv_size ? cv[(yy0 + j) * kv_size + t] : 0;
@@ -834,17 +843,26 @@ __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __res
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRsDepth) : "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    const uint8_t* src = ring + slot * rstride + xoff;
     int s0 = 1 << (kPrecisionBits - 1), s1 = s0, s2 = s0;
     if constexpr ((ABL & 1) != 0) {
       himg[(r - r0) * 256 + xx] = (uint32_t)(r + xx);
     } else {
+    // the 21 tap bytes from 7 aligned dword reads, realigned with v_alignbyte (a
+    // byte-granular or misaligned wide LDS read costs far more than this)
+    const uint32_t* dw = (const uint32_t*)(ring + slot * rstride + (xoff & ~3));
+    const int sh = xoff & 3;
+    uint32_t d[7], wv[6];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) d[k] = dw[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) wv[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
 #pragma unroll
     for (int t = 0; t < kRsTaps; ++t) {
       // bytes x non-negative 22-bit weights: 24-bit multiplies (full rate)
-      s0 += (int)__umul24(src[3 * t + 0], kx[t]);
-      s1 += (int)__umul24(src[3 * t + 1], kx[t]);
-      s2 += (int)__umul24(src[3 * t + 2], kx[t]);
+      const int b0 = 3 * t, b1 = 3 * t + 1, b2 = 3 * t + 2;
+      s0 += (int)__umul24((wv[b0 >> 2] >> (8 * (b0 & 3))) & 255u, kx[t]);
+      s1 += (int)__umul24((wv[b1 >> 2] >> (8 * (b1 & 3))) & 255u, kx[t]);
+      s2 += (int)__umul24((wv[b2 >> 2] >> (8 * (b2 & 3))) & 255u, kx[t]);
     }
     himg[(r - r0) * 256 + xx] = (uint32_t)clip8(s0) | ((uint32_t)clip8(s1) << 8) | ((uint32_t)clip8(s2) << 16);
     }
@@ -855,13 +873,12 @@ __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __res
   __syncthreads();
   if (!col) return;
   if constexpr ((ABL & 2) != 0) {
+    (void)lut;
     uint32_t acc = 0;
     for (int i = 0; i < r1 - r0; ++i) acc += himg[i * 256 + xx];
     dst[((size_t)b * out + yy0) * out * 3 + xx] = (T)(float)acc;
     return;
   }
-  const float mean[3] = {0.485f, 0.456f, 0.406f};
-  const float stdv[3] = {0.229f, 0.224f, 0.225f};
 #pragma unroll
   for (int j = 0; j < kRsBand; ++j) {
     if (j < nyy) {
@@ -879,7 +896,7 @@ __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __res
       const int av[3] = {a0, a1, a2};
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const float v = ((float)clip8(av[c]) / 255.f - mean[c]) / stdv[c];
+        const float v = lut[c * 256 + clip8(av[c])];
         if (nchw)
           dst[(((size_t)b * 3 + c) * out + yy) * out + xx] = (T)v;
         else
@@ -915,7 +932,8 @@ void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_
   if (rows16 && resize_stream_mode() && p.out <= 256 && p.ksize_h <= kRsTaps && p.ksize_v <= kRsTaps &&
       col_bytes16 + 32 <= kRsRowB && (int64_t)p.in_h * p.in_w * 3 < (1ll << 31)) {
     const int v16 = col_bytes16 / 16;
-    const size_t lds = (size_t)kRsRing * kRsRowB + (size_t)(p.band_rows + kRsTaps) * 256 * 4 + kRsBand * kRsTaps * 4;
+    const size_t lds = (size_t)kRsRing * kRsRowB + (size_t)(p.band_rows + kRsTaps) * 256 * 4 + kRsBand * kRsTaps * 4 +
+                       3 * 256 * 4;
     const int blocks = n * ((p.out + kRsBand - 1) / kRsBand);
     const int m = resize_stream_mode();
     if (m > 1 && !(out_layout == 1 || dtype == RTDM_F32)) {  // diagnostic ablations (tools/ab_cls.py)
