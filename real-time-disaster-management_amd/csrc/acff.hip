@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void acff_fused(AcffArgs a) {
       for (int r = 0; r < 4; ++r) {
         float x = acc[i][j][r] + bb;
         x = x > 0.f ? x : x * a.slope;
-        v[r] = x * sc + sh;
+        v[r] = fmaf(x, sc, sh);  // explicit FMA: acff_chain repeats it bit for bit
       }
       if (a.pool) {
         const int py = (oy0 >> 1) + qy, px = (ox0 >> 1) + qx;
@@ -614,6 +614,311 @@ void launch_acff_fused(const void* in, int in_cs, int in_co, int n, int h, int w
     hipLaunchKernelGGL(acff_fused<4>, dim3((unsigned)blocks), dim3(256), lds, s, a);
   else
     hipLaunchKernelGGL(acff_fused<8>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+  RTDM_HIP(hipGetLastError());
+}
+
+
+// --------------------------------------------------------------------------
+// acff_chain: the classifier's small-map suffix in ONE launch, one 512-thread
+// block per image: ACFF stages without pooling (ErNET acff4..6, Squeeze acff4)
+// run back to back on an LDS-resident activation map, then the tail (conv2 1x1
+// -> AvgPool -> view -> Linear -> Softmax, squeeze_ernet.py:33-41 /
+// ernet.py:38-45).  Per stage, per dilation branch: depthwise taps (VALU, fp32
+// accumulate, same FMA order as acff_fused) -> fp16 A chunk [M][C] in LDS ->
+// this branch's K slice of the 1x1 GEMM on v_mfma_f32_16x16x32_f16 (B fragments
+// from the L2-resident packed weights; K order branch*C + c, so the fp32
+// accumulation sequence is acff_fused's) -> bias / LeakyReLU / BN affine ->
+// fp16 map for the next stage.  The activations never leave the CU: the
+// unfused path's 3 launches + tail and their HBM round trips become one launch,
+// bit-identical results.
+// --------------------------------------------------------------------------
+static constexpr int kChainMaxStages = 4;
+static constexpr int kChainThreads = 512;
+
+struct AcffChainStage {
+  const float* dw_wt;   // [3][9][cin]
+  const float* dw_b;    // [3][cin]
+  const _Float16* pw;   // [cout_pad][kpad], k = branch*cin + c
+  const float* bias;
+  const float* scale;
+  const float* shift;
+  int cin, cout, cout_pad, kpad, h;  // square input side h
+};
+
+struct AcffChainArgs {
+  const _Float16* in;
+  int in_cs, in_co;
+  int nst;
+  AcffChainStage st[kChainMaxStages];
+  float slope;
+  int act_bytes;  // bytes of each of the two LDS activation buffers
+  int a_bytes;    // bytes of the A chunk
+  // tail
+  const float* w2;  // [5][c]
+  int pool_pad, ph, pw;
+  const float* fcw;
+  const float* fcb;
+  float* logits;
+  float* probs;
+};
+
+__global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char chain_lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int img = blockIdx.x;
+  _Float16* buf[2] = {(_Float16*)chain_lds, (_Float16*)(chain_lds + a.act_bytes)};
+  _Float16* At = (_Float16*)(chain_lds + 2 * a.act_bytes);
+  float* wsm = (float*)(chain_lds + 2 * a.act_bytes + a.a_bytes);  // [3][9][C] then bias [3][C]
+
+  {  // input map of stage 0: [h*h][cin] fp16 from the NHWC view
+    const int h = a.st[0].h, C = a.st[0].cin, CG = C >> 3;
+    const _Float16* src = a.in + (size_t)img * h * h * a.in_cs + a.in_co;
+    for (int i = tid; i < h * h * CG; i += kChainThreads) {
+      const int px = i / CG, v = i - px * CG;
+      *(uint4*)(buf[0] + (size_t)px * C + v * 8) = *(const uint4*)(src + (size_t)px * a.in_cs + v * 8);
+    }
+  }
+  int cur = 0;
+  const int fr = lane & 15, g = lane >> 4;
+  for (int si = 0; si < a.nst; ++si) {
+    const AcffChainStage& st = a.st[si];
+    const int H = st.h, OH = H - 2, M = OH * OH, C = st.cin, CG = C >> 3, AS = C + 8;
+    for (int i = tid; i < 30 * C; i += kChainThreads) wsm[i] = i < 27 * C ? st.dw_wt[i] : st.dw_b[i - 27 * C];
+    __syncthreads();  // input map + dw weights ready; the previous stage's A reads are done
+    const _Float16* X = buf[cur];
+    _Float16* Y = buf[cur ^ 1];
+    const int wn = st.cout_pad >> 5, wm = 8 / wn;  // wave grid: wm (M) x wn (N), 32 channels per wave
+    const int wmi = wid / wn, wni = wid - wmi * wn;
+    const int mtiles = (M + 15) >> 4;
+    const int fm = (mtiles + wm - 1) / wm;  // <= 4 (plan-time check)
+    const int m_base = wmi * fm * 16, n_base = wni * 32;
+    f4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int br = 0; br < 3; ++br) {
+      const int d = br + 1;
+      const float* wb = wsm + br * 9 * C;
+      const float* bb = wsm + 27 * C + br * C;
+      for (int i = tid; i < M * CG; i += kChainThreads) {
+        const int m = i / CG, v = i - m * CG;
+        const int oy = m / OH, ox = m - oy * OH;
+        float t[8];
+        const float4 b0 = *(const float4*)(bb + v * 8), b1 = *(const float4*)(bb + v * 8 + 4);
+        t[0] = b0.x; t[1] = b0.y; t[2] = b0.z; t[3] = b0.w;
+        t[4] = b1.x; t[5] = b1.y; t[6] = b1.z; t[7] = b1.w;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const int y = oy + 1 + (kh - 1) * d, x = ox + 1 + (kw - 1) * d;
+            h8 xv = h8{0, 0, 0, 0, 0, 0, 0, 0};
+            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)H) xv = *(const h8*)(X + (size_t)(y * H + x) * C + v * 8);
+            const float* wp = wb + (kh * 3 + kw) * C + v * 8;
+            const float4 w0 = *(const float4*)wp, w1 = *(const float4*)(wp + 4);
+            t[0] = fmaf(w0.x, (float)xv[0], t[0]);
+            t[1] = fmaf(w0.y, (float)xv[1], t[1]);
+            t[2] = fmaf(w0.z, (float)xv[2], t[2]);
+            t[3] = fmaf(w0.w, (float)xv[3], t[3]);
+            t[4] = fmaf(w1.x, (float)xv[4], t[4]);
+            t[5] = fmaf(w1.y, (float)xv[5], t[5]);
+            t[6] = fmaf(w1.z, (float)xv[6], t[6]);
+            t[7] = fmaf(w1.w, (float)xv[7], t[7]);
+          }
+        h8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (_Float16)t[j];
+        *(h8*)(At + (size_t)m * AS + v * 8) = o;
+      }
+      __syncthreads();
+      // this branch's K slice: k = br*C + [0, C)
+      const _Float16* wrow = st.pw + (size_t)(n_base + fr) * st.kpad + br * C + g * 8;
+      for (int ks = 0; ks < C / 32; ++ks) {
+        const h8 b0 = *(const h8*)(wrow + ks * 32);
+        const h8 b1 = *(const h8*)(wrow + (size_t)16 * st.kpad + ks * 32);
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm) {
+          if (tm < fm && m_base + tm * 16 < M) {
+            const int row = m_base + tm * 16 + fr;
+            const h8 av = *(const h8*)(At + (size_t)(row < M ? row : M - 1) * AS + ks * 32 + g * 8);
+            acc[tm][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b0, acc[tm][0], 0, 0, 0);
+            acc[tm][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b1, acc[tm][1], 0, 0, 0);
+          }
+        }
+      }
+      __syncthreads();  // the A chunk is rewritten by the next branch
+    }
+    // epilogue: bias -> LeakyReLU -> BN affine -> fp16 map Y [M][cout]
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = n_base + j * 16 + fr;
+      if (c >= st.cout) continue;
+      const float bc = st.bias[c];
+      const float sc = st.scale ? st.scale[c] : 1.f;
+      const float sh = st.scale ? st.shift[c] : 0.f;
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm) {
+        if (!(tm < fm)) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m_base + tm * 16 + g * 4 + r;
+          if (m < M) {
+            float x = acc[tm][j][r] + bc;
+            x = x > 0.f ? x : x * a.slope;
+            Y[(size_t)m * st.cout + c] = (_Float16)fmaf(x, sc, sh);
+          }
+        }
+      }
+    }
+    cur ^= 1;
+  }
+  __syncthreads();
+  // ---- tail on the last map: [hw][c], c = last cout ----
+  const int h = a.nst > 0 ? a.st[a.nst - 1].h - 2 : a.st[0].h, hw = h * h;
+  const int c = a.nst > 0 ? a.st[a.nst - 1].cout : a.st[0].cin;
+  const _Float16* X = buf[cur];
+  float* conv = (float*)At;  // [5][hw]
+  for (int p = wid; p < hw; p += kChainThreads / 64) {
+    const _Float16* x = X + (size_t)p * c;
+    float s5[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int ch = lane; ch < c; ch += 64) {
+      const float xv = (float)x[ch];
+#pragma unroll
+      for (int o = 0; o < 5; ++o) s5[o] = fmaf(xv, a.w2[(size_t)o * c + ch], s5[o]);
+    }
+#pragma unroll
+    for (int o = 0; o < 5; ++o) {
+      float v = s5[o];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) conv[o * hw + p] = v;
+    }
+  }
+  __syncthreads();
+  float* feat = conv + 5 * hw;  // [5*ph*pw]
+  const int nf = 5 * a.ph * a.pw;
+  for (int t = tid; t < nf; t += kChainThreads) {
+    const int o = t / (a.ph * a.pw);
+    const int r = t - o * a.ph * a.pw;
+    const int i = r / a.pw, j = r - (r / a.pw) * a.pw;
+    float sum = 0.f;
+    for (int dy = 0; dy < 5; ++dy) {
+      const int y = i - a.pool_pad + dy;
+      if ((unsigned)y >= (unsigned)h) continue;
+      for (int dx = 0; dx < 5; ++dx) {
+        const int x = j - a.pool_pad + dx;
+        if ((unsigned)x >= (unsigned)h) continue;
+        sum += conv[o * hw + y * h + x];
+      }
+    }
+    feat[t] = sum / 25.f;
+  }
+  __syncthreads();
+  float* lg = feat + nf;
+  if (tid < 5) {
+    float s1 = 0.f;
+    for (int q = 0; q < nf; ++q) s1 = fmaf(feat[q], a.fcw[tid * nf + q], s1);
+    s1 += a.fcb[tid];
+    lg[tid] = s1;
+    if (a.logits) a.logits[img * 5 + tid] = s1;
+  }
+  __syncthreads();
+  if (tid < 5 && a.probs) {
+    float mx = lg[0];
+    for (int k = 1; k < 5; ++k) mx = fmaxf(mx, lg[k]);
+    float sum = 0.f;
+    for (int k = 0; k < 5; ++k) sum += expf(lg[k] - mx);
+    a.probs[img * 5 + tid] = expf(lg[tid] - mx) / sum;
+  }
+}
+
+static int g_acff_chain = 1;
+int acff_chain_mode() { return g_acff_chain; }
+void set_acff_chain_mode(int v) { g_acff_chain = v; }
+
+size_t acff_chain_lds(const AcffChainPlan& p) {
+  size_t act = 0, ab = 0;
+  int cmax = 0;
+  for (int i = 0; i < p.nst; ++i) {
+    const int h = p.h[i], oh = h - 2;
+    act = std::max(act, (size_t)h * h * p.cin[i] * 2);
+    act = std::max(act, (size_t)oh * oh * p.cout[i] * 2);
+    ab = std::max(ab, (size_t)oh * oh * (p.cin[i] + 8) * 2);
+    cmax = std::max(cmax, p.cin[i]);
+  }
+  act = (size_t)round_up((int64_t)act, 16);
+  const int oh = p.h[p.nst - 1] - 2;
+  ab = std::max(ab, (size_t)(5 * oh * oh + 5 * 16 + 8) * 4);  // the tail reuses the A chunk
+  ab = (size_t)round_up((int64_t)ab, 16);
+  return 2 * act + ab + (size_t)30 * cmax * 4;
+}
+
+bool acff_chain_ok(const AcffChainPlan& p) {
+  if (p.nst < 1 || p.nst > kChainMaxStages) return false;
+  for (int i = 0; i < p.nst; ++i) {
+    const int oh = p.h[i] - 2, M = oh * oh;
+    if (p.cin[i] % 32 != 0 || p.kpad[i] < 3 * p.cin[i] || oh < 1) return false;
+    const int wn = p.cout_pad[i] / 32;
+    if (p.cout_pad[i] % 32 != 0 || (wn != 1 && wn != 2 && wn != 4 && wn != 8)) return false;
+    const int wm = 8 / wn, mtiles = (M + 15) / 16;
+    if ((mtiles + wm - 1) / wm > 4) return false;
+    if (i > 0 && (p.h[i] != p.h[i - 1] - 2 || p.cin[i] != p.cout[i - 1])) return false;
+  }
+  const int oh = p.h[p.nst - 1] - 2;
+  if (oh * oh > 64 * 16) return false;
+  return acff_chain_lds(p) <= 160 * 1024;
+}
+
+void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in_co, int n, const float* const* dw_wt,
+                       const float* const* dw_b, const void* const* pw, const float* const* bias,
+                       const float* const* scale, const float* const* shift, float slope, const float* w2,
+                       int pool_pad, int ph, int pwid, const float* fcw, const float* fcb, float* logits, float* probs,
+                       hipStream_t s) {
+  RTDM_REQUIRE(acff_chain_ok(p), RTDM_E_INVALID, "acff_chain: unsupported plan");
+  RTDM_REQUIRE((in_cs % 8) == 0 && (in_co % 8) == 0, RTDM_E_INVALID, "acff_chain: input view not 16-byte aligned");
+  RTDM_REQUIRE(ph * pwid <= 16, RTDM_E_UNSUPPORTED, "acff_chain: pooled tail too large");
+  if (n <= 0) return;
+  AcffChainArgs a;
+  a.in = (const _Float16*)in;
+  a.in_cs = in_cs;
+  a.in_co = in_co;
+  a.nst = acff_chain_mode() == 2 ? 0 : p.nst;  // 2: tail only (diagnostics; stages skipped -> wrong)
+  for (int i = 0; i < p.nst; ++i) {
+    AcffChainStage& t = a.st[i];
+    t.dw_wt = dw_wt[i];
+    t.dw_b = dw_b[i];
+    t.pw = (const _Float16*)pw[i];
+    t.bias = bias[i];
+    t.scale = scale[i];
+    t.shift = shift[i];
+    t.cin = p.cin[i];
+    t.cout = p.cout[i];
+    t.cout_pad = p.cout_pad[i];
+    t.kpad = p.kpad[i];
+    t.h = p.h[i];
+  }
+  a.slope = slope;
+  size_t act = 0, ab = 0;
+  for (int i = 0; i < p.nst; ++i) {
+    const int h = p.h[i], oh = h - 2;
+    act = std::max(act, (size_t)h * h * p.cin[i] * 2);
+    act = std::max(act, (size_t)oh * oh * p.cout[i] * 2);
+    ab = std::max(ab, (size_t)oh * oh * (p.cin[i] + 8) * 2);
+  }
+  const int ohl = p.h[p.nst - 1] - 2;
+  ab = std::max(ab, (size_t)(5 * ohl * ohl + 5 * 16 + 8) * 4);
+  a.act_bytes = (int)round_up((int64_t)act, 16);
+  a.a_bytes = (int)round_up((int64_t)ab, 16);
+  a.w2 = w2;
+  a.pool_pad = pool_pad;
+  a.ph = ph;
+  a.pw = pwid;
+  a.fcw = fcw;
+  a.fcb = fcb;
+  a.logits = logits;
+  a.probs = probs;
+  const size_t lds = acff_chain_lds(p);
+  hipLaunchKernelGGL(acff_chain, dim3(n), dim3(kChainThreads), lds, s, a);
   RTDM_HIP(hipGetLastError());
 }
 

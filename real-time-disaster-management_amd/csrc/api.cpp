@@ -33,6 +33,8 @@ rtdm_status rtdm_set_tuning(const char* key, int value) {
       set_two_streams_mode(value);
     else if (!strcmp(key, "acff_persist"))
       set_acff_persist_mode(value);
+    else if (!strcmp(key, "acff_chain"))
+      set_acff_chain_mode(value);
     else if (!strcmp(key, "stem_abl"))
       set_stem_abl(value);
     else if (!strcmp(key, "nms_variant"))

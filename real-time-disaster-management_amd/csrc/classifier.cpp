@@ -53,6 +53,9 @@ struct rtdm_classifier_s {
   std::map<std::pair<int, int>, std::unique_ptr<rtdm::ResizePlan>> resize;
   rtdm::DevBuf resize_tmp;
   size_t resize_tmp_bytes = 0;
+  // stages [chain_start, end) + tail run as one acff_chain launch (-1: none)
+  int chain_start = -1;
+  rtdm::AcffChainPlan chain;
 };
 
 namespace rtdm {
@@ -265,6 +268,32 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
   h.tail_w2 = blob.add(pm.get("conv2.weight", 5 * 256), 5 * 256 * sizeof(float));
   h.tail_fcw = blob.add(pm.get("fc.weight", 5 * nf), (size_t)5 * nf * sizeof(float));
   h.tail_fcb = blob.add(pm.get("fc.bias", 5), 5 * sizeof(float));
+  // ---- small-map suffix: non-pooled, reducer-free acff_fused stages (+ tail) in one launch ----
+  if (f16) {
+    int first = (int)h.stages.size();
+    while (first > 0) {
+      const AcffStage& st = h.stages[first - 1];
+      if (!st.fused || st.persist_cc || st.pool || st.red || !st.affine) break;
+      --first;
+    }
+    const int nst = (int)h.stages.size() - first;
+    if (nst >= 1 && nst <= 4) {
+      AcffChainPlan cp;
+      cp.nst = nst;
+      for (int i = 0; i < nst; ++i) {
+        const AcffStage& st = h.stages[first + i];
+        cp.h[i] = st.h;
+        cp.cin[i] = st.cin;
+        cp.cout[i] = st.cout;
+        cp.cout_pad[i] = st.pw.cout_pad;
+        cp.kpad[i] = st.pw.kpad;
+      }
+      if (acff_chain_ok(cp)) {
+        h.chain_start = first;
+        h.chain = cp;
+      }
+    }
+  }
   h.per_image = off;
   h.blob.upload(blob);
   h.arena.alloc(h.per_image * esize(h.dtype) * h.max_batch);
@@ -332,7 +361,10 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
   launch_conv(a, h.dtype, s);
 
   View cur{buf(h.stem_buf), h.stem_cout, 0};
-  for (const AcffStage& st : h.stages) {
+  const bool chain = h.chain_start >= 0 && acff_chain_mode();
+  for (size_t si = 0; si < h.stages.size(); ++si) {
+    if (chain && (int)si == h.chain_start) break;
+    const AcffStage& st = h.stages[si];
     const int lim = st.pool || st.red_pool ? (st.oh / 2) * 2 : st.oh;
     if (st.fused) {
       const float* sc = st.affine ? h.blob.at<float>(st.pw.s_off) : nullptr;
@@ -472,6 +504,28 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       launch_conv(r, h.dtype, s);
       cur = View{buf(st.red_buf), st.redw.cout, 0};
     }
+  }
+  if (chain) {
+    const int k = h.chain.nst;
+    const float* dw_wt[4];
+    const float* dw_b[4];
+    const void* pw[4];
+    const float* bias[4];
+    const float* sc[4];
+    const float* sh[4];
+    for (int i = 0; i < k; ++i) {
+      const AcffStage& st = h.stages[h.chain_start + i];
+      dw_wt[i] = h.blob.at<float>(st.dw_wt);
+      dw_b[i] = h.blob.at<float>(st.dw_b);
+      pw[i] = h.blob.at<void>(st.pw.w_off);
+      bias[i] = h.blob.at<float>(st.pw.b_off);
+      sc[i] = h.blob.at<float>(st.pw.s_off);
+      sh[i] = h.blob.at<float>(st.pw.t_off);
+    }
+    launch_acff_chain(h.chain, cur.ptr, cur.cs, cur.co, n, dw_wt, dw_b, pw, bias, sc, sh, 0.01f,
+                      h.blob.at<float>(h.tail_w2), h.tail_pool_pad, h.tail_ph, h.tail_pw, h.blob.at<float>(h.tail_fcw),
+                      h.blob.at<float>(h.tail_fcb), logits, probs, s);
+    return;
   }
   launch_cls_tail(cur.ptr, n, h.tail_h, h.tail_h, h.tail_c, h.blob.at<float>(h.tail_w2), h.tail_pool_pad, h.tail_ph,
                   h.tail_pw, h.blob.at<float>(h.tail_fcw), h.blob.at<float>(h.tail_fcb), logits, probs, h.dtype, s);

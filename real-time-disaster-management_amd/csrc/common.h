@@ -229,6 +229,20 @@ void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int
                          const float* dw_wt, const float* dw_b, const void* pwc, int cout, int cout_pad,
                          const float* bias, const float* scale, const float* shift, float slope, void* out, int out_cs,
                          int pool, hipStream_t s);
+// acff.hip: the classifier's non-pooled small-map ACFF suffix + tail in one launch
+struct AcffChainPlan {
+  int nst = 0;
+  int h[4] = {}, cin[4] = {}, cout[4] = {}, cout_pad[4] = {}, kpad[4] = {};
+};
+bool acff_chain_ok(const AcffChainPlan& p);
+size_t acff_chain_lds(const AcffChainPlan& p);
+void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in_co, int n, const float* const* dw_wt,
+                       const float* const* dw_b, const void* const* pw, const float* const* bias,
+                       const float* const* scale, const float* const* shift, float slope, const float* w2,
+                       int pool_pad, int ph, int pwid, const float* fcw, const float* fcb, float* logits, float* probs,
+                       hipStream_t s);
+int acff_chain_mode();  // 1 = use acff_chain when the plan allows (default), 0 = per-stage kernels + tail
+void set_acff_chain_mode(int v);
 int acff_persist_mode();
 void set_acff_persist_mode(int v);
 void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, int stride, int pad, int zero_pad_rb,
