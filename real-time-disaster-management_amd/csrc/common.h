@@ -175,10 +175,21 @@ struct ConvArgs {
   const void* head_w = nullptr;
   int head_cout = 0;
   Epilogue head_e;
+  // int8 path (conv_i8.hip): int8 weights [cout_pad][kpad], per-channel dequant
+  // multipliers deq[c] = s_x * s_w[c], activation quantisation scale 1 / s_x
+  const void* w8 = nullptr;
+  const float* deq = nullptr;
+  float qscale = 0.f;
 };
 
 // Launchers (conv.hip).  dtype = RTDM_F16 / RTDM_F32 (activation + weight type).
 void launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
+// conv_i8.hip: int8 MFMA implicit GEMM (RTDM_I8 detectors) + calibration |x|max
+bool conv_i8_ok(const ConvArgs& a);
+void launch_conv_i8(const ConvArgs& a, hipStream_t s);
+void launch_absmax(View v, int n, int h, int w, int c, unsigned* out, hipStream_t s);
+static constexpr int kCalBins = 2048;  // |x| histogram bins over [0, |x|max]
+void launch_abshist(View v, int n, int h, int w, int c, const unsigned* amax, unsigned* hist, hipStream_t s);
 // conv_pipe.hip: pipelined 256x128 implicit GEMM for Cin % 64 == 0 layers
 bool conv_pipe_ok(const ConvArgs& a);
 void launch_conv_pipe(const ConvArgs& a, hipStream_t s);

@@ -119,6 +119,12 @@ struct Step {
   bool bn = false;  // raw darknet weights (host), packed after planning
   const float *w_beta = nullptr, *w_gamma = nullptr, *w_mean = nullptr, *w_var = nullptr, *w_bias = nullptr,
               *w_W = nullptr;
+  // int8 (RTDM_I8 handles): slot of this conv in the calibration table (-1: fp16 conv),
+  // int8 weights, per-channel weight scales (host) and dequant multipliers (device)
+  int q = -1;
+  size_t w8_off = SIZE_MAX, deq_off = SIZE_MAX;
+  std::vector<float> sw;
+  float qscale = 0.f;
   // two-stream schedule (schedule_streams): stream 0 = the caller's, 1 = the side stream
   int stream = 0;
   std::vector<int> deps;    // earlier steps writing a buffer this step reads
@@ -145,6 +151,13 @@ struct YoloHead {
 struct rtdm_detector_s {
   int img_h = 0, img_w = 0, dtype = 0, max_batch = 0, dev = 0;
   bool planning_only = true;
+  // RTDM_I8: activations fp16 (dtype = RTDM_F16), Cin % 64 == 0 convs on int8 MFMA
+  // once calibrated (rtdm_detector_calibrate); calibrating = forward in fp16 recording
+  // each int8 conv's input |x|max into amax[q]
+  bool int8 = false, calibrated = false;
+  int calibrating = 0;  // 1: |x|max pass, 2: histogram pass
+  int n_q = 0;
+  rtdm::DevBuf amax, hist;  // [n_q] float bits, [n_q][kCalBins] counts
   std::vector<rtdm::CfgBlock> defs;  // without [net]
   std::vector<rtdm::Tensor> tensors;
   std::vector<rtdm::Step> steps;
@@ -344,7 +357,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
           h.layer_tensor[i] = -1;        // the pre-add conv output is never materialised
           h.layer_tensor[i + 1] = full;  // conv output with the residual added
           need_full = !consumers[i + 1].empty();
-        } else if (f16 && fuse_head() && nx.type == "convolutional" && only_next && i + 2 < L && defs[i + 2].type == "yolo" &&
+        } else if (f16 && fuse_head() && !h.int8 && nx.type == "convolutional" && only_next && i + 2 < L && defs[i + 2].type == "yolo" &&
                    consumers[i + 1].size() == 1 && consumers[i + 1][0] == i + 2 && consumers[i + 2].empty() &&
                    nx.i("size", 1) == 1 && nx.i("stride", 1) == 1 && nx.i("groups", 1) == 1 &&
                    nx.i("filters", 0) <= 32 && filters > 64 && filters <= 128 &&
@@ -631,6 +644,34 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         RTDM_REQUIRE(st.hpc.kpad == 128 && st.hpc.cout_pad == 32, RTDM_E_INVALID, "internal: head packing");
       }
       if (stem) st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr);
+      if (h.int8 && use_mfma && !st.head && st.yolo < 0 && st.cin % 64 == 0 && (size == 1 || size == 3) &&
+          st.pc.cout_pad % 128 == 0) {
+        // symmetric per-output-channel int8 of the BN-folded weights, [cout_pad][kpad]
+        const int kp = st.pc.kpad, cp = st.pc.cout_pad;
+        std::vector<int8_t> w8((size_t)cp * kp, 0);
+        st.sw.assign(cp, 0.f);
+        for (int o = 0; o < filters; ++o) {
+          double mx = 0.0;
+          std::vector<double> row((size_t)size * size * st.cin);
+          for (int c = 0; c < st.cin; ++c)
+            for (int kh = 0; kh < size; ++kh)
+              for (int kw = 0; kw < size; ++kw) {
+                double v = st.w_W[(((size_t)o * st.cin + c) * size + kh) * size + kw];
+                if (st.bn) v *= sc[o];
+                row[(size_t)(kh * size + kw) * st.cin + c] = v;
+                mx = std::max(mx, std::fabs(v));
+              }
+          const double sw = mx > 0 ? mx / 127.0 : 1.0;
+          st.sw[o] = (float)sw;
+          for (size_t k = 0; k < row.size(); ++k) {
+            const long q = std::lround(row[k] / sw);
+            w8[(size_t)o * kp + k] = (int8_t)std::max(-127L, std::min(127L, q));
+          }
+        }
+        st.w8_off = blob.add(w8.data(), w8.size());
+        st.deq_off = blob.add(nullptr, (size_t)cp * sizeof(float));
+        st.q = h.n_q++;
+      }
     } else {
       st.pc.cout = filters;
       st.pc.cin = st.cin;
@@ -650,6 +691,12 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     h.arena.alloc(h.per_image * esize_of(h.dtype) * h.max_batch);
     h.zero.alloc(256);
     RTDM_HIP(hipMemset(h.zero.p, 0, 256));
+    if (h.n_q) {
+      h.amax.alloc((size_t)h.n_q * sizeof(unsigned));
+      RTDM_HIP(hipMemset(h.amax.p, 0, (size_t)h.n_q * sizeof(unsigned)));
+      h.hist.alloc((size_t)h.n_q * kCalBins * sizeof(unsigned));
+      RTDM_HIP(hipMemset(h.hist.p, 0, (size_t)h.n_q * kCalBins * sizeof(unsigned)));
+    }
   }
 }
 
@@ -670,6 +717,8 @@ static View tensor_view(const rtdm_detector_s& h, int t) {
 static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, float* io, hipStream_t s,
                          int raw = 0) {
   RTDM_REQUIRE(!h.planning_only, RTDM_E_INVALID, "detect: handle was created without weights");
+  RTDM_REQUIRE(!h.int8 || h.calibrated || h.calibrating != 0 || h.n_q == 0, RTDM_E_INVALID,
+               "detect: int8 detector not calibrated (rtdm_detector_calibrate)");
   RTDM_REQUIRE(n >= 0 && n <= h.max_batch, RTDM_E_CAPACITY,
                "detect: batch " + std::to_string(n) + " exceeds max_batch " + std::to_string(h.max_batch));
   if (n == 0) return;
@@ -765,7 +814,21 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       a.w_f32 = st.pc.mfma ? 0 : 1;
       a.w_stem = h.blob.at<void>(st.pc.stem_off);
       a.zero = h.zero.p;
-      launch_conv(a, h.dtype, s);
+      if (st.q >= 0 && h.calibrating) {
+        if (h.calibrating == 1)
+          launch_absmax(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, h.amax.as<unsigned>() + st.q, s);
+        else
+          launch_abshist(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, h.amax.as<unsigned>() + st.q,
+                         h.hist.as<unsigned>() + (size_t)st.q * kCalBins, s);
+        launch_conv(a, h.dtype, s);
+      } else if (st.q >= 0) {
+        a.w8 = h.blob.at<void>(st.w8_off);
+        a.deq = h.blob.at<float>(st.deq_off);
+        a.qscale = st.qscale;
+        launch_conv_i8(a, s);
+      } else {
+        launch_conv(a, h.dtype, s);
+      }
     } else if (st.kind == ST_MAXPOOL) {
       launch_maxpool(nullptr, tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, st.k, st.s, st.p, st.zero_rb,
                      tensor_view(h, st.out_t), st.oh, st.ow, h.dtype, s);
@@ -832,7 +895,7 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     } else if (st.yolo >= 0) {
       a.e.io = (float*)64;
     }
-    name = conv_kernel_name(a, h.dtype);
+    name = st.q >= 0 ? "conv_i8" : conv_kernel_name(a, h.dtype);
     flop = 2.0 * st.oh * st.ow * (double)st.cout * st.cin * st.ks * st.ks +
            (st.head ? 2.0 * st.oh * st.ow * (double)st.head_cout * st.cout : 0.0);
     double out = 0;
@@ -940,7 +1003,7 @@ static void schedule_streams(rtdm_detector_s& h) {
 
 static std::string describe(const rtdm_detector_s& h) {
   std::ostringstream o;
-  o << "darknet plan: img " << h.img_h << "x" << h.img_w << " dtype " << (h.dtype == RTDM_F16 ? "f16" : "f32")
+  o << "darknet plan: img " << h.img_h << "x" << h.img_w << " dtype " << (h.int8 ? "i8" : h.dtype == RTDM_F16 ? "f16" : "f32")
     << " layers " << h.defs.size() << " steps " << h.steps.size() << " anchors " << h.n_anchors_total << " no " << h.no
     << " GFLOP/img " << h.flop * 1e-9 << " arena/img " << h.per_image << " elems\n";
   auto tn = [&](int t) -> std::string {
@@ -987,12 +1050,14 @@ rtdm_status rtdm_detector_create(const char* cfg_text, int img_h, int img_w, int
     *out = nullptr;
     RTDM_REQUIRE(cfg_text, RTDM_E_INVALID, "detector_create: NULL cfg");
     RTDM_REQUIRE(img_h > 0 && img_w > 0, RTDM_E_INVALID, "detector_create: bad image size");
-    RTDM_REQUIRE(dtype == RTDM_F32 || dtype == RTDM_F16, RTDM_E_INVALID, "detector_create: bad dtype");
+    RTDM_REQUIRE(dtype == RTDM_F32 || dtype == RTDM_F16 || dtype == RTDM_I8, RTDM_E_INVALID,
+                 "detector_create: bad dtype");
     RTDM_REQUIRE(max_batch > 0, RTDM_E_INVALID, "detector_create: max_batch must be > 0");
     auto h = std::make_unique<rtdm_detector_s>();
     h->img_h = img_h;
     h->img_w = img_w;
-    h->dtype = dtype;
+    h->int8 = dtype == RTDM_I8;
+    h->dtype = h->int8 ? RTDM_F16 : dtype;  // int8 handles keep fp16 activations
     h->max_batch = max_batch;
     h->planning_only = weights == nullptr;
     std::vector<CfgBlock> defs = parse_cfg(cfg_text);
@@ -1088,6 +1153,76 @@ rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float
   return guard([&] {
     RTDM_REQUIRE(h, RTDM_E_INVALID, "detect: NULL handle");
     run_detector(*h, x, x_kind, n, io, (hipStream_t)stream);
+  });
+}
+
+rtdm_status rtdm_detector_calibrate(rtdm_detector h, const void* x, int x_kind, int n, int reset, void* stream) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "calibrate: NULL handle");
+    RTDM_REQUIRE(h->int8, RTDM_E_INVALID, "calibrate: handle is not RTDM_I8");
+    if (h->n_q == 0) {
+      h->calibrated = true;
+      return;
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    if (reset) {
+      RTDM_HIP(hipMemsetAsync(h->amax.p, 0, (size_t)h->n_q * sizeof(unsigned), s));
+      RTDM_HIP(hipMemsetAsync(h->hist.p, 0, (size_t)h->n_q * kCalBins * sizeof(unsigned), s));
+    }
+    if (n > 0) {
+      const size_t need = (size_t)h->max_batch * h->n_anchors_total * h->no * sizeof(float);
+      if (h->raw_buf.bytes < need) h->raw_buf.alloc(need);
+      // pass 1: |x|max; pass 2: |x| histograms over [0, |x|max] (bins of earlier calls
+      // keep their own range: a later larger max clamps nothing, it only coarsens)
+      for (int pass = 1; pass <= 2; ++pass) {
+        h->calibrating = pass;
+        try {
+          run_detector(*h, x, x_kind, n, h->raw_buf.as<float>(), s);
+        } catch (...) {
+          h->calibrating = 0;
+          throw;
+        }
+      }
+      h->calibrating = 0;
+    }
+    // scales: the clip c minimising the quantisation MSE of each int8 conv input
+    // (uniform error step^2/12 below c, (|x| - c)^2 above, step = c / 127), over the
+    // histogram; s_x = c / 127; deq[c] = s_x * s_w[c]
+    std::vector<unsigned> am(h->n_q), hc((size_t)h->n_q * kCalBins);
+    RTDM_HIP(hipMemcpyAsync(am.data(), h->amax.p, am.size() * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    RTDM_HIP(hipMemcpyAsync(hc.data(), h->hist.p, hc.size() * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    RTDM_HIP(hipStreamSynchronize(s));
+    for (Step& st : h->steps) {
+      if (st.q < 0) continue;
+      float mx;
+      std::memcpy(&mx, &am[st.q], sizeof(float));
+      RTDM_REQUIRE(std::isfinite(mx), RTDM_E_INVALID, "calibrate: non-finite activations");
+      float clip = mx;
+      if (mx > 0.f) {
+        const unsigned* hh = &hc[(size_t)st.q * kCalBins];
+        const double bw = (double)mx / kCalBins;
+        double best = 1e300;
+        for (int t = kCalBins / 16; t <= kCalBins; ++t) {
+          const double c = t * bw, step = c / 127.0;
+          double e = 0.0;
+          for (int b = 0; b < kCalBins; ++b) {
+            if (!hh[b]) continue;
+            const double xc = (b + 0.5) * bw;
+            e += xc < c ? (double)hh[b] * step * step / 12.0 : (double)hh[b] * (xc - c) * (xc - c);
+          }
+          if (e < best) {
+            best = e;
+            clip = (float)c;
+          }
+        }
+      }
+      const float sx = clip > 0.f ? clip / 127.f : 1.f;
+      st.qscale = 1.f / sx;
+      std::vector<float> dq(st.sw.size());
+      for (size_t c = 0; c < dq.size(); ++c) dq[c] = sx * st.sw[c];
+      RTDM_HIP(hipMemcpy(h->blob.at<float>(st.deq_off), dq.data(), dq.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+    h->calibrated = true;
   });
 }
 

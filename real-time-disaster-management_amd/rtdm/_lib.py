@@ -21,6 +21,7 @@ STATUS_NAMES = {0: "OK", 1: "INVALID", 2: "HIP", 3: "CAPACITY", 4: "UNSUPPORTED"
 # rtdm_dtype
 RTDM_F32 = 0
 RTDM_F16 = 1
+RTDM_I8 = 2
 # rtdm_model_kind
 RTDM_SQUEEZE_ERNET = 0
 RTDM_SQUEEZE_REDCONV = 1
@@ -71,6 +72,7 @@ SIGNATURES = {
     "rtdm_detector_read_timing": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int)]),
     "rtdm_detect": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "rtdm_detect_raw": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "rtdm_detector_calibrate": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "rtdm_detect_trt": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "rtdm_yolo_layer_trt": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_float), c_int, c_int, c_float,
                                     c_int, c_void_p, c_void_p]),

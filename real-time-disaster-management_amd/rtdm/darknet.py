@@ -60,6 +60,7 @@ class Darknet(torch.nn.Module):
             img_size = (img_size, img_size)
         self.img_size = (int(img_size[0]), int(img_size[1]))
         self._stream = None
+        self._calib = None
         self._dtype = L.RTDM_F32
         self._handle = None
         self._handle_key = None
@@ -115,6 +116,29 @@ class Darknet(torch.nn.Module):
         self._release()
         return self
 
+    def int8(self, calib: torch.Tensor):
+        """int8-quantise the detector (README --quant int8; BASELINE config 5): the Cin % 64
+        convs run on int8 MFMA with per-channel weight scales and per-tensor activation
+        scales calibrated on `calib` (uint8 frames [N,H,W,3] or NCHW inputs on the GPU,
+        kept for handles created later)."""
+        if not calib.is_cuda:
+            raise RuntimeError("calibration frames must be on the GPU")
+        self._calib = calib.contiguous()
+        self._dtype = L.RTDM_I8
+        self._release()
+        return self
+
+    def _calibrate(self, h):
+        x = self._calib
+        kind = (L.RTDM_INPUT_FRAME_U8 if x.dtype == torch.uint8 else
+                L.RTDM_INPUT_NCHW_F32 if x.dtype == torch.float32 else L.RTDM_INPUT_NCHW_F16)
+        cap = self._handle_key[1]
+        with torch.cuda.device(x.device):
+            for i in range(0, x.shape[0], cap):
+                c = x[i:i + cap]
+                L.check(L.lib().rtdm_detector_calibrate(h, L.ptr(c), kind, c.shape[0], 1 if i == 0 else 0,
+                                                        L.stream_ptr()))
+
     def fuse(self):  # models.py:397-411 (a no-op in the reference, BN is SyncBatchNorm); BN is always folded here
         return self
 
@@ -145,6 +169,8 @@ class Darknet(torch.nn.Module):
                                              self._stream.size, cap, ctypes.byref(h)))
         self._handle = h
         self._handle_key = (key, cap)
+        if self._dtype == L.RTDM_I8:
+            self._calibrate(h)
         return h
 
     # ---------------------------------------------------------------- forward --
