@@ -25,43 +25,8 @@ import torch  # noqa: E402
 
 from rtdm.cli import list_images, read_image_rgb, select_device  # noqa: E402
 from rtdm.darknet import Darknet, load_darknet_weights  # noqa: E402
+from rtdm.letterbox import letterbox, scale_coords  # noqa: E402
 from rtdm.nms import non_max_suppression  # noqa: E402
-
-
-def letterbox(img: np.ndarray, new_shape: int, color=(128, 128, 128), auto: bool = True):
-    """datasets.py:599-631: r = new/max(h, w); pad the resized image to new_shape (auto=False)
-    or only to the next multiple of 32 (auto=True, the LoadImages default).
-    Returns (img, ratio, (dw, dh))."""
-    from PIL import Image
-    h0, w0 = img.shape[:2]
-    r = new_shape / max(h0, w0)
-    new_unpad = (int(round(w0 * r)), int(round(h0 * r)))
-    dw, dh = new_shape - new_unpad[0], new_shape - new_unpad[1]
-    if auto:
-        dw, dh = dw % 32, dh % 32
-    dw, dh = dw / 2, dh / 2
-    if (w0, h0) != new_unpad:
-        img = np.asarray(Image.fromarray(img).resize(new_unpad, Image.BOX if r < 1 else Image.BILINEAR), np.uint8)
-    top, bottom = int(round(dh - 0.1)), int(round(dh + 0.1))
-    left, right = int(round(dw - 0.1)), int(round(dw + 0.1))
-    out = np.empty((new_unpad[1] + top + bottom, new_unpad[0] + left + right, 3), np.uint8)
-    out[...] = np.asarray(color, np.uint8)
-    out[top:top + new_unpad[1], left:left + new_unpad[0]] = img
-    return out, r, (dw, dh)
-
-
-def scale_coords(img1_shape, coords, img0_shape):
-    """utils.py:123-136 (+ clip_coords :139-142): boxes from the letterboxed frame back to the source."""
-    gain = max(img1_shape) / max(img0_shape)
-    pad = (img1_shape[1] - img0_shape[1] * gain) / 2, (img1_shape[0] - img0_shape[0] * gain) / 2
-    coords[:, [0, 2]] -= pad[0]
-    coords[:, [1, 3]] -= pad[1]
-    coords[:, :4] /= gain
-    coords[:, 0].clamp_(0, img0_shape[1])
-    coords[:, 1].clamp_(0, img0_shape[0])
-    coords[:, 2].clamp_(0, img0_shape[1])
-    coords[:, 3].clamp_(0, img0_shape[0])
-    return coords
 
 
 def load_names(path):

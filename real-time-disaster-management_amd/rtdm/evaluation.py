@@ -1,0 +1,109 @@
+"""mAP@0.5 harness on the HIP runtime: counterpart of victim_localization/yolov3/test.py:11-197.
+
+``test(cfg, data, weights, batch_size, img_size, conf_thres, iou_thres, model, dataloader)``
+keeps the reference signature and return value ``((mp, mr, map, mf1, *loss), maps)``:
+frames → rtdm Darknet → rtdm_nms → per-image matching + ap_per_class (rtdm.metrics).
+The loss terms are 0: the rtdm detector is inference-only (test.py:103-104 only adds them
+when the model carries training hyper-parameters).  Single process, one GPU per process —
+where the reference wraps the model in nn.DataParallel (test.py:42-43), shard the list file
+over ranks and merge DetectionStats instead (rtdm.distributed.gather_results).
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+import torch
+
+from .metrics import DetectionStats
+from .nms import non_max_suppression
+
+
+def parse_data_cfg(path: str) -> dict:
+    """utils/parse_config.py:55-71: key=value lines, '#' comments."""
+    if not os.path.exists(path) and os.path.exists(os.path.join('data', path)):
+        path = os.path.join('data', path)
+    options = {}
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if not line or line.startswith('#'):
+                continue
+            key, val = line.split('=')
+            options[key.strip()] = val.strip()
+    return options
+
+
+def load_classes(path: str):
+    """utils.py:37-41."""
+    with open(path) as f:
+        return [x for x in f.read().split('\n') if x]
+
+
+def _frames_nhwc(imgs: torch.Tensor, device) -> torch.Tensor:
+    """uint8 frames to the detector's NHWC input; NCHW batches (the reference loader's
+    layout) are viewed back to NHWC on the device."""
+    imgs = imgs.to(device, non_blocking=True)
+    if imgs.dtype == torch.uint8 and imgs.dim() == 4 and imgs.shape[1] == 3 and imgs.shape[3] != 3:
+        imgs = imgs.permute(0, 2, 3, 1).contiguous()
+    return imgs
+
+
+def test(cfg, data, weights=None, batch_size=16, img_size=416, conf_thres=0.001, iou_thres=0.6, model=None,
+         dataloader=None, half=False, verbose=None, num_workers=4):
+    from .darknet import Darknet, load_darknet_weights
+    if model is None:
+        if not torch.cuda.is_available():
+            raise RuntimeError("rtdm test.py runs on the HIP runtime: no GPU visible")
+        device = torch.device('cuda:0')
+        verbose = True if verbose is None else verbose
+        model = Darknet(cfg, img_size)
+        if weights.endswith('.pt'):
+            model.load_state_dict(torch.load(weights, map_location='cpu', weights_only=True)['model'])
+        else:
+            load_darknet_weights(model, weights)
+        if half:
+            model.half()
+    else:
+        device = torch.device('cuda', torch.cuda.current_device())
+        verbose = False if verbose is None else verbose
+
+    data = parse_data_cfg(data)
+    nc = int(data['classes'])
+    names = load_classes(data['names']) if os.path.exists(data.get('names', '')) else [str(i) for i in range(nc)]
+
+    if dataloader is None:
+        from .datasets import LoadImagesAndLabels
+        dataset = LoadImagesAndLabels(data['valid'], img_size, batch_size)
+        batch_size = min(batch_size, len(dataset))
+        dataloader = torch.utils.data.DataLoader(dataset, batch_size=batch_size, num_workers=num_workers,
+                                                 pin_memory=True, collate_fn=dataset.collate_fn)
+
+    stats = DetectionStats(nc)
+    t0 = t1 = 0.0
+    for imgs, targets, paths, shapes in dataloader:
+        x = _frames_nhwc(imgs, device)
+        height, width = x.shape[1:3] if x.dtype == torch.uint8 else x.shape[2:4]
+        torch.cuda.synchronize()
+        t = time.time()
+        with torch.no_grad():
+            inf_out, _ = model(x)
+        torch.cuda.synchronize()
+        t0 += time.time() - t
+        t = time.time()
+        output = non_max_suppression(inf_out, conf_thres=conf_thres, iou_thres=iou_thres)
+        t1 += time.time() - t
+        stats.update(output, targets, int(height), int(width))
+
+    r = stats.compute()
+    pf = '%20s' + '%10.3g' * 6
+    print(('%20s' + '%10s' * 6) % ('Class', 'Images', 'Targets', 'P', 'R', 'mAP@0.5', 'F1'))
+    print(pf % ('all', r['seen'], r['nt'].sum(), r['mp'], r['mr'], r['map'], r['mf1']))
+    if verbose and nc > 1 and len(r['ap_class']):
+        for i, c in enumerate(r['ap_class']):
+            print(pf % (names[c], r['seen'], r['nt'][c], r['p'][i], r['r'][i], r['ap'][i], r['f1'][i]))
+    if verbose and r['seen']:
+        ms = tuple(v / r['seen'] * 1e3 for v in (t0, t1, t0 + t1)) + (img_size, img_size, batch_size)
+        print('Speed: %.1f/%.1f/%.1f ms inference/NMS/total per %gx%g image at batch-size %g' % ms)
+    return (r['mp'], r['mr'], r['map'], r['mf1'], 0.0, 0.0, 0.0), np.asarray(r['maps'])

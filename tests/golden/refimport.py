@@ -53,3 +53,21 @@ def import_darknet(nms_impl=None):
         import models
         from utils import utils
     return models, utils
+
+
+def import_yolov3_test(nms_impl=None):
+    """yolov3/test.py as a module (named ref_yolov3_test: the bare name `test` is the
+    stdlib's regression-test package).  Same stubs as import_darknet."""
+    import importlib.util
+    import_darknet(nms_impl)
+    # utils/datasets.py reads cv2 constants as default arguments at import time only
+    # (letterbox/load_image are never called here): plain sentinels suffice
+    cv2 = sys.modules["cv2"]
+    for k in ("INTER_AREA", "INTER_LINEAR", "BORDER_CONSTANT"):
+        if not hasattr(cv2, k):
+            setattr(cv2, k, -1)
+    spec = importlib.util.spec_from_file_location("ref_yolov3_test", os.path.join(DET_DIR, "test.py"))
+    mod = importlib.util.module_from_spec(spec)
+    with _cwd(DET_DIR):
+        spec.loader.exec_module(mod)
+    return mod

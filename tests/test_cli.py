@@ -44,7 +44,7 @@ def test_classification_metrics_match_confusion_definitions():
 def test_letterbox_and_scale_coords():
     det = _load_cli("detect")
     img = np.zeros((300, 500, 3), np.uint8)
-    out, r, (dw, dh) = det.letterbox(img, 416)
+    out, (r, _), (dw, dh) = det.letterbox(img, 416)   # ratio is (w, h) as datasets.py:614
     assert out.shape[1] == 416 and out.shape[0] % 32 == 0 and out.shape[0] >= 250
     sq, _, _ = det.letterbox(img, 416, auto=False)
     assert sq.shape[:2] == (416, 416)
