@@ -235,6 +235,23 @@ rtdm_status rtdm_nms(const float* io, int n, int n_anchors, int no, float conf_t
 rtdm_status rtdm_preprocess_frames(const uint8_t* frames, int n, int in_h, int in_w, int out_size,
                                    float* out, void* stream);
 
+/* ---- detector ingest: letterbox (yolov3/utils/datasets.py:599-631, :508-522) ----
+ * rtdm_letterbox_geometry: the shape arithmetic of letterbox(img, (shape_h, shape_w),
+ * auto, scaleFill, scaleup) for an in_h x in_w image: geom = {new_h, new_w, out_h,
+ * out_w, top, left} (resize target, canvas, placement; Python round() semantics).
+ * rtdm_letterbox: frames [n, in_h, pitch] uint8, 3 channels per pixel (pitch >= 3*in_w)
+ * -> out [n, out_h, out_w, 3] uint8: each frame resized to new_w x new_h with
+ * cv2.INTER_AREA semantics (area averaging when shrinking, INTER_AREA's linear
+ * coefficients when growing) at (left, top), the rest pad_rgb (0x00BBGGRR, output
+ * order).  swap_rb = 1 reads BGR (cv2 frames) and writes RGB.  The output feeds
+ * rtdm_detect with RTDM_INPUT_FRAME_U8.  Replaces cv2.resize + cv2.copyMakeBorder
+ * (datasets.py:626-630) and load_image's shrink (:517-520, new = int(side * r)).  */
+rtdm_status rtdm_letterbox_geometry(int in_h, int in_w, int shape_h, int shape_w, int auto_, int scale_fill,
+                                    int scaleup, int* geom);
+rtdm_status rtdm_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int new_h, int new_w,
+                           int out_h, int out_w, int top, int left, uint32_t pad_rgb, int swap_rb, uint8_t* out,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif

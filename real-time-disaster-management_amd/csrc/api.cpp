@@ -1,4 +1,6 @@
 // Library-level C ABI: errors, version, stand-alone decode / NMS / preprocess.
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 
 #include "common.h"
@@ -132,6 +134,48 @@ rtdm_status rtdm_preprocess_frames(const uint8_t* frames, int n, int in_h, int i
     launch_preprocess(p, frames, n, tmp.as<uint8_t>(), out, 1, RTDM_F32, (hipStream_t)stream);
     // plan + tmp are released on return: finish the work first
     RTDM_HIP(hipStreamSynchronize((hipStream_t)stream));
+  });
+}
+
+rtdm_status rtdm_letterbox_geometry(int in_h, int in_w, int shape_h, int shape_w, int auto_, int scale_fill,
+                                    int scaleup, int* geom) {
+  return guard([&] {
+    RTDM_REQUIRE(geom, RTDM_E_INVALID, "letterbox_geometry: NULL geom");
+    RTDM_REQUIRE(in_h > 0 && in_w > 0 && shape_h > 0 && shape_w > 0, RTDM_E_INVALID, "letterbox_geometry: bad shape");
+    // datasets.py:603-627, with Python's round() (ties to even) as std::nearbyint
+    double r = (double)std::max(shape_h, shape_w) / (double)std::max(in_h, in_w);
+    if (!scaleup) r = std::min(r, 1.0);
+    int new_w = (int)std::nearbyint(in_w * r), new_h = (int)std::nearbyint(in_h * r);
+    double dw = shape_w - new_w, dh = shape_h - new_h;
+    if (auto_) {
+      dw = (double)(((int)dw % 32 + 32) % 32);
+      dh = (double)(((int)dh % 32 + 32) % 32);
+    } else if (scale_fill) {
+      dw = dh = 0.0;
+      new_w = shape_h;  // new_unpad = new_shape (h, w) handed to cv2.resize as (w, h)
+      new_h = shape_w;
+    }
+    dw /= 2;
+    dh /= 2;
+    const int top = (int)std::nearbyint(dh - 0.1), bottom = (int)std::nearbyint(dh + 0.1);
+    const int left = (int)std::nearbyint(dw - 0.1), right = (int)std::nearbyint(dw + 0.1);
+    geom[0] = new_h;
+    geom[1] = new_w;
+    geom[2] = new_h + top + bottom;
+    geom[3] = new_w + left + right;
+    geom[4] = top;
+    geom[5] = left;
+  });
+}
+
+rtdm_status rtdm_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int new_h, int new_w,
+                           int out_h, int out_w, int top, int left, uint32_t pad_rgb, int swap_rb, uint8_t* out,
+                           void* stream) {
+  return guard([&] {
+    if (n == 0) return;
+    RTDM_REQUIRE(frames && out, RTDM_E_INVALID, "letterbox: NULL pointer");
+    launch_letterbox(frames, n, in_h, in_w, pitch, new_h, new_w, out_h, out_w, top, left, pad_rgb, swap_rb, out,
+                     (hipStream_t)stream);
   });
 }
 

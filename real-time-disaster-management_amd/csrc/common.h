@@ -283,6 +283,11 @@ void set_resize_stream_mode(int v);
 void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_t* tmp, void* out,
                        int out_layout /*0: NHWC dtype, 1: NCHW f32*/, int dtype, hipStream_t s);
 
+// Letterbox (datasets.py:599-631): cv2 INTER_AREA resize to new_w x new_h at (left, top)
+// of an out_h x out_w canvas of pad_rgb; uint8 3-channel frames (row pitch in bytes).
+void launch_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int new_h, int new_w, int out_h,
+                      int out_w, int top, int left, uint32_t pad_rgb, int swap_rb, uint8_t* out, hipStream_t s);
+
 void launch_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const float* anchor_vec, float ystride,
                         float* io, int io_rows, int row_off, hipStream_t s);
 

@@ -1,0 +1,284 @@
+// Letterbox ingest on the device: victim_localization/yolov3/utils/datasets.py:599-631
+// (letterbox) and :508-522 (load_image), i.e. cv2.resize(..., INTER_AREA) of a uint8
+// frame to (new_w, new_h), placed at (left, top) of an out_h x out_w canvas filled with
+// the pad colour.  Output is the detector's native input: NHWC uint8 RGB.
+//
+// cv2 is not in this stack, so the resize restates OpenCV's published INTER_AREA
+// algorithm (imgproc resize.cpp, scalar paths) — parity with cv2 itself is UNPINNED;
+// the kernel is bit-exact against the numpy restatement in oracle/letterbox.py:
+//   * both scales >= 1, integral  -> area-fast: integer box sum * (1.f/area), cvRound
+//   * both scales >= 1            -> area: per-axis (src, alpha) tables
+//                                    (computeResizeAreaTab), row sums h = sum S*alpha,
+//                                    v = sum beta*h in fp32 without contraction, cvRound
+//   * otherwise (growing)         -> linear with INTER_AREA's coefficients, 11-bit
+//                                    fixed point (HResizeLinear int + FixedPtCast 22)
+// One thread per output pixel (3 channels); the pad region is a constant store.
+// Frames arrive once per batch and are small next to the detector's traffic (a
+// 640x480 frame is 0.9 MB in, 0.5 MB out at 416), so this is a plain L2-cached
+// gather rather than an LDS-staged pipeline.
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+#include "common.h"
+
+namespace rtdm {
+
+namespace {
+
+constexpr int kLbMaxTaps = 16;
+
+enum LbMode : int { LB_AREA_FAST = 0, LB_AREA = 1, LB_LINEAR = 2 };
+
+struct LbTables {
+  int mode = LB_AREA;
+  int tx = 0, ty = 0;  // taps per destination coordinate (area)
+  int sx = 1, sy = 1;  // integer factors (area-fast)
+  DevBuf buf;          // area: int src[nx*tx] | float w[nx*tx] | int src[ny*ty] | float w[ny*ty]
+                       // linear: int4 x[nx] (i0, i1, c0, c1) | int4 y[ny]
+};
+
+// OpenCV computeResizeAreaTab; scale = 1 / (dsize / ssize) in double, as cv::resize forms it.
+void area_tab(int ssize, int dsize, std::vector<std::vector<std::pair<int, float>>>& tab) {
+  const double scale = 1.0 / ((double)dsize / (double)ssize);
+  tab.assign(dsize, {});
+  for (int d = 0; d < dsize; ++d) {
+    const double f1 = d * scale;
+    const double f2 = f1 + scale;
+    const double cell = std::min(scale, (double)ssize - f1);
+    int s1 = (int)std::ceil(f1), s2 = (int)std::floor(f2);
+    s2 = std::min(s2, ssize - 1);
+    s1 = std::min(s1, s2);
+    auto& t = tab[d];
+    if (s1 - f1 > 1e-3) t.push_back({s1 - 1, (float)((s1 - f1) / cell)});
+    for (int s = s1; s < s2; ++s) t.push_back({s, (float)(1.0 / cell)});
+    if (f2 - s2 > 1e-3) t.push_back({s2, (float)(std::min(std::min(f2 - s2, 1.0), cell) / cell)});
+  }
+}
+
+// INTER_AREA when growing: s = floor(d*scale); f = (d+1) - (s+1)*inv wrapped to [0,1);
+// borders collapse to one tap (f = 0); 11-bit coefficients rounded separately.
+void linear_tab(int ssize, int dsize, std::vector<int>& out) {
+  const double inv = (double)dsize / (double)ssize;
+  const double scale = 1.0 / inv;
+  out.resize(4 * (size_t)dsize);
+  for (int d = 0; d < dsize; ++d) {
+    int s = (int)std::floor(d * scale);
+    float f = (float)((d + 1) - (s + 1) * inv);
+    f = f <= 0 ? 0.f : f - std::floor(f);
+    if (s < 0) {
+      s = 0;
+      f = 0.f;
+    }
+    if (s >= ssize - 1) {
+      s = ssize - 1;
+      f = 0.f;
+    }
+    out[4 * d + 0] = s;
+    out[4 * d + 1] = std::min(s + 1, ssize - 1);
+    out[4 * d + 2] = (int)std::nearbyint((1.f - f) * 2048.f);
+    out[4 * d + 3] = (int)std::nearbyint(f * 2048.f);
+  }
+}
+
+std::mutex g_lb_mu;
+std::map<std::tuple<int, int, int, int, int>, std::unique_ptr<LbTables>> g_lb_cache;
+
+const LbTables& lb_tables(int in_h, int in_w, int new_h, int new_w) {
+  int dev = 0;
+  RTDM_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_lb_mu);
+  auto key = std::make_tuple(dev, in_h, in_w, new_h, new_w);
+  auto it = g_lb_cache.find(key);
+  if (it != g_lb_cache.end()) return *it->second;
+  auto t = std::make_unique<LbTables>();
+  const double scx = 1.0 / ((double)new_w / in_w), scy = 1.0 / ((double)new_h / in_h);
+  std::vector<uint8_t> host;
+  auto append = [&](const void* p, size_t bytes) {
+    const uint8_t* b = (const uint8_t*)p;
+    host.insert(host.end(), b, b + bytes);
+  };
+  if (scx >= 1.0 && scy >= 1.0) {
+    const int isx = (int)std::lround(scx), isy = (int)std::lround(scy);
+    if (std::fabs(scx - isx) < 2.220446049250313e-16 && std::fabs(scy - isy) < 2.220446049250313e-16) {
+      RTDM_REQUIRE(isx * isy <= 65536, RTDM_E_INVALID, "letterbox: shrink factor too large");
+      t->mode = LB_AREA_FAST;
+      t->sx = isx;
+      t->sy = isy;
+    } else {
+      t->mode = LB_AREA;
+      std::vector<std::vector<std::pair<int, float>>> xt, yt;
+      area_tab(in_w, new_w, xt);
+      area_tab(in_h, new_h, yt);
+      for (auto& v : xt) t->tx = std::max<int>(t->tx, (int)v.size());
+      for (auto& v : yt) t->ty = std::max<int>(t->ty, (int)v.size());
+      RTDM_REQUIRE(t->tx <= kLbMaxTaps && t->ty <= kLbMaxTaps, RTDM_E_INVALID,
+                   "letterbox: shrink factors above 14 are not supported");
+      auto pack = [&](const std::vector<std::vector<std::pair<int, float>>>& tab, int taps) {
+        std::vector<int> src(tab.size() * taps);
+        std::vector<float> w(tab.size() * taps);
+        for (size_t d = 0; d < tab.size(); ++d)
+          for (int k = 0; k < taps; ++k) {
+            // padding taps: weight 0 on the last real source (an exact +0 in fp32)
+            const bool real = k < (int)tab[d].size();
+            src[d * taps + k] = real ? tab[d][k].first : tab[d].back().first;
+            w[d * taps + k] = real ? tab[d][k].second : 0.f;
+          }
+        append(src.data(), src.size() * 4);
+        append(w.data(), w.size() * 4);
+      };
+      pack(xt, t->tx);
+      pack(yt, t->ty);
+    }
+  } else {
+    t->mode = LB_LINEAR;
+    std::vector<int> xt, yt;
+    linear_tab(in_w, new_w, xt);
+    linear_tab(in_h, new_h, yt);
+    append(xt.data(), xt.size() * 4);
+    append(yt.data(), yt.size() * 4);
+  }
+  if (!host.empty()) {
+    t->buf.alloc(host.size());
+    RTDM_HIP(hipMemcpy(t->buf.p, host.data(), host.size(), hipMemcpyHostToDevice));
+  }
+  auto& ref = *t;
+  g_lb_cache.emplace(key, std::move(t));
+  return ref;
+}
+
+struct LbArgs {
+  const uint8_t* src;
+  int64_t frame_bytes;  // source frame stride
+  int pitch;            // source row stride (bytes)
+  int new_h, new_w, out_h, out_w, top, left;
+  uint32_t pad;  // 0x00BBGGRR in output channel order
+  int swap_rb;
+  int mode, tx, ty, sx, sy;
+  float inv_area;
+  const void* tab;
+  uint8_t* out;
+};
+
+__device__ __forceinline__ uint8_t sat_round(float v) {
+  const int i = (int)rintf(v);  // cvRound: nearest, ties to even
+  return (uint8_t)min(255, max(0, i));
+}
+
+__global__ void __launch_bounds__(256) letterbox_kernel(LbArgs a) {
+  const int64_t npx = (int64_t)a.out_h * a.out_w;
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npx) return;
+  const int img = blockIdx.y;
+  const int oy = (int)(p / a.out_w), ox = (int)(p - (int64_t)oy * a.out_w);
+  uint8_t* o = a.out + ((int64_t)img * npx + p) * 3;
+  const int dy = oy - a.top, dx = ox - a.left;
+  if (dy < 0 || dy >= a.new_h || dx < 0 || dx >= a.new_w) {
+    o[0] = (uint8_t)(a.pad & 0xff);
+    o[1] = (uint8_t)((a.pad >> 8) & 0xff);
+    o[2] = (uint8_t)((a.pad >> 16) & 0xff);
+    return;
+  }
+  const uint8_t* f = a.src + (int64_t)img * a.frame_bytes;
+  uint8_t r[3];
+  if (a.mode == LB_AREA_FAST) {
+    int s0 = 0, s1 = 0, s2 = 0;
+    const uint8_t* row = f + (int64_t)dy * a.sy * a.pitch + (int64_t)dx * a.sx * 3;
+    for (int j = 0; j < a.sy; ++j, row += a.pitch)
+      for (int k = 0; k < a.sx; ++k) {
+        s0 += row[3 * k];
+        s1 += row[3 * k + 1];
+        s2 += row[3 * k + 2];
+      }
+    r[0] = sat_round(__fmul_rn((float)s0, a.inv_area));
+    r[1] = sat_round(__fmul_rn((float)s1, a.inv_area));
+    r[2] = sat_round(__fmul_rn((float)s2, a.inv_area));
+  } else if (a.mode == LB_AREA) {
+    const int* xs = (const int*)a.tab;
+    const float* xw = (const float*)(xs + (int64_t)a.new_w * a.tx);
+    const int* ys = (const int*)(xw + (int64_t)a.new_w * a.tx);
+    const float* yw = (const float*)(ys + (int64_t)a.new_h * a.ty);
+    xs += dx * a.tx;
+    xw += dx * a.tx;
+    ys += dy * a.ty;
+    yw += dy * a.ty;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    for (int j = 0; j < a.ty; ++j) {
+      const uint8_t* row = f + (int64_t)ys[j] * a.pitch;
+      float h0 = 0.f, h1 = 0.f, h2 = 0.f;
+      for (int k = 0; k < a.tx; ++k) {
+        const uint8_t* s = row + xs[k] * 3;
+        const float w = xw[k];
+        h0 = __fadd_rn(h0, __fmul_rn((float)s[0], w));
+        h1 = __fadd_rn(h1, __fmul_rn((float)s[1], w));
+        h2 = __fadd_rn(h2, __fmul_rn((float)s[2], w));
+      }
+      const float b = yw[j];
+      if (j == 0) {
+        v0 = __fmul_rn(b, h0);
+        v1 = __fmul_rn(b, h1);
+        v2 = __fmul_rn(b, h2);
+      } else {
+        v0 = __fadd_rn(v0, __fmul_rn(b, h0));
+        v1 = __fadd_rn(v1, __fmul_rn(b, h1));
+        v2 = __fadd_rn(v2, __fmul_rn(b, h2));
+      }
+    }
+    r[0] = sat_round(v0);
+    r[1] = sat_round(v1);
+    r[2] = sat_round(v2);
+  } else {
+    const int4 xt = ((const int4*)a.tab)[dx];
+    const int4 yt = ((const int4*)a.tab)[a.new_w + dy];
+    const uint8_t* r0 = f + (int64_t)yt.x * a.pitch;
+    const uint8_t* r1 = f + (int64_t)yt.y * a.pitch;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int h0 = r0[xt.x * 3 + c] * xt.z + r0[xt.y * 3 + c] * xt.w;
+      const int h1 = r1[xt.x * 3 + c] * xt.z + r1[xt.y * 3 + c] * xt.w;
+      const int v = (yt.z * h0 + yt.w * h1 + (1 << 21)) >> 22;
+      r[c] = (uint8_t)min(255, max(0, v));
+    }
+  }
+  o[0] = a.swap_rb ? r[2] : r[0];
+  o[1] = r[1];
+  o[2] = a.swap_rb ? r[0] : r[2];
+}
+
+}  // namespace
+
+void launch_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int new_h, int new_w, int out_h,
+                      int out_w, int top, int left, uint32_t pad_rgb, int swap_rb, uint8_t* out, hipStream_t s) {
+  RTDM_REQUIRE(n > 0 && n <= 65535, RTDM_E_INVALID, "letterbox: n must be in [1, 65535]");
+  RTDM_REQUIRE(in_h > 0 && in_w > 0 && new_h > 0 && new_w > 0, RTDM_E_INVALID, "letterbox: bad shape");
+  RTDM_REQUIRE(pitch >= in_w * 3, RTDM_E_INVALID, "letterbox: pitch < 3 * in_w");
+  RTDM_REQUIRE(top >= 0 && left >= 0 && top + new_h <= out_h && left + new_w <= out_w, RTDM_E_INVALID,
+               "letterbox: resized frame does not fit the canvas");
+  const LbTables& t = lb_tables(in_h, in_w, new_h, new_w);
+  LbArgs a;
+  a.src = frames;
+  a.frame_bytes = (int64_t)pitch * in_h;
+  a.pitch = pitch;
+  a.new_h = new_h;
+  a.new_w = new_w;
+  a.out_h = out_h;
+  a.out_w = out_w;
+  a.top = top;
+  a.left = left;
+  a.pad = pad_rgb;
+  a.swap_rb = swap_rb;
+  a.mode = t.mode;
+  a.tx = t.tx;
+  a.ty = t.ty;
+  a.sx = t.sx;
+  a.sy = t.sy;
+  a.inv_area = 1.f / (float)(t.sx * t.sy);
+  a.tab = t.buf.p;
+  a.out = out;
+  const int64_t npx = (int64_t)out_h * out_w;
+  hipLaunchKernelGGL(letterbox_kernel, dim3((unsigned)((npx + 255) / 256), n), dim3(256), 0, s, a);
+  RTDM_HIP(hipGetLastError());
+}
+
+}  // namespace rtdm

@@ -5,10 +5,10 @@ Same flags (:159-174) and outputs: per image "%gx%g <counts per class> Done. (ti
 ``--save-txt`` rows "x1 y1 x2 y2 cls conf" (:118-121), annotated images in --output.
 Darknet(cfg, img_size) + load_darknet_weights / torch.load(...)['model'] (:21-28) →
 model(img)[0] (:87) → non_max_suppression(conf, iou, classes, agnostic) (:91) →
-scale_coords back to the source image (:108).  Frames are letterboxed on the host like
+scale_coords back to the source image (:108).  Frames are letterboxed on the GPU like
 LoadImages → letterbox (utils/datasets.py:599-631, auto=True: longer side → img_size,
-the shorter padded to a multiple of 32 with (128,128,128)); cv2.INTER_AREA is replaced
-by Pillow's BOX filter (shrinking) / BILINEAR (growing).  Each distinct letterboxed
+the shorter padded to a multiple of 32 with (128,128,128)) by rtdm_letterbox, whose
+resize restates cv2.INTER_AREA (rtdm.letterbox).  Each distinct letterboxed
 shape gets its own planned detector handle (the reference rebuilds grids per shape,
 models.py:228-230).
 """
@@ -25,7 +25,7 @@ import torch  # noqa: E402
 
 from rtdm.cli import list_images, read_image_rgb, select_device  # noqa: E402
 from rtdm.darknet import Darknet, load_darknet_weights  # noqa: E402
-from rtdm.letterbox import letterbox, scale_coords  # noqa: E402
+from rtdm.letterbox import geometry, letterbox, letterbox_frames, scale_coords  # noqa: E402,F401
 from rtdm.nms import non_max_suppression  # noqa: E402
 
 
@@ -65,21 +65,23 @@ def detect(opt):
     results = {}
     for path in list_images(opt.source):
         im0 = read_image_rgb(path)
-        img, _, _ = letterbox(im0, opt.img_size)
-        x = torch.from_numpy(img[None]).to(device)  # uint8 NHWC; the /255 is fused on device
+        # source frame up at its own size; letterbox (INTER_AREA resize + pad) on the device
+        g = geometry(im0.shape[0], im0.shape[1], opt.img_size, auto=True)
+        x = letterbox_frames(torch.from_numpy(im0[None]).to(device), g)  # uint8 NHWC; /255 fused in the stem
+        img_shape = (g[2], g[3])
         torch.cuda.synchronize()
         t1 = time.time()
-        pred, _ = model_for(tuple(img.shape[:2]))(x)
+        pred, _ = model_for(img_shape)(x)
         det = non_max_suppression(pred, opt.conf_thres, opt.iou_thres, classes=opt.classes,
                                   agnostic=opt.agnostic_nms)[0]
         torch.cuda.synchronize()
         t2 = time.time()
-        s = '%gx%g ' % img.shape[:2]
+        s = '%gx%g ' % img_shape
         save_path = os.path.join(out, os.path.basename(path))
         rows = []
         if det is not None and len(det):
             det = det.cpu()
-            det[:, :4] = scale_coords(img.shape[:2], det[:, :4], im0.shape).round()
+            det[:, :4] = scale_coords(img_shape, det[:, :4], im0.shape).round()
             for c in det[:, -1].unique():
                 n = int((det[:, -1] == c).sum())
                 s += '%g %ss, ' % (n, names[int(c)])

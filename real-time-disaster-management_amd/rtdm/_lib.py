@@ -9,8 +9,8 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import (POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_uint8,
-                    c_void_p)
+from ctypes import (POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_size_t, c_uint32, c_uint64,
+                    c_uint8, c_void_p)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RTDM_LIB", os.path.join(_HERE, "librtdm.so"))
@@ -84,6 +84,9 @@ SIGNATURES = {
     "rtdm_nms": (c_int, [c_void_p, c_int, c_int, c_int, c_float, c_double, c_int, c_int, c_uint64, c_int, c_void_p,
                          c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rtdm_preprocess_frames": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "rtdm_letterbox_geometry": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, POINTER(c_int)]),
+    "rtdm_letterbox": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                               c_uint32, c_int, c_void_p, c_void_p]),
 }
 
 _lib = None

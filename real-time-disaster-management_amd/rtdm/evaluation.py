@@ -41,9 +41,11 @@ def load_classes(path: str):
         return [x for x in f.read().split('\n') if x]
 
 
-def _frames_nhwc(imgs: torch.Tensor, device) -> torch.Tensor:
-    """uint8 frames to the detector's NHWC input; NCHW batches (the reference loader's
-    layout) are viewed back to NHWC on the device."""
+def _frames_nhwc(imgs, device) -> torch.Tensor:
+    """uint8 frames to the detector's NHWC input: RawFrames batches are letterboxed on the
+    device; NCHW batches (the reference loader's layout) are viewed back to NHWC there."""
+    if hasattr(imgs, "to_device"):
+        return imgs.to_device(device)
     imgs = imgs.to(device, non_blocking=True)
     if imgs.dtype == torch.uint8 and imgs.dim() == 4 and imgs.shape[1] == 3 and imgs.shape[3] != 3:
         imgs = imgs.permute(0, 2, 3, 1).contiguous()
@@ -78,7 +80,7 @@ def test(cfg, data, weights=None, batch_size=16, img_size=416, conf_thres=0.001,
         dataset = LoadImagesAndLabels(data['valid'], img_size, batch_size)
         batch_size = min(batch_size, len(dataset))
         dataloader = torch.utils.data.DataLoader(dataset, batch_size=batch_size, num_workers=num_workers,
-                                                 pin_memory=True, collate_fn=dataset.collate_fn)
+                                                 pin_memory=False, collate_fn=dataset.collate_fn)
 
     stats = DetectionStats(nc)
     t0 = t1 = 0.0

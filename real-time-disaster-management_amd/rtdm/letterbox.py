@@ -1,65 +1,97 @@
-"""Host-side frame ingest for the detector CLIs: letterbox + box rescaling
-(victim_localization/yolov3/utils/datasets.py:508-522, 599-631; utils/utils.py:123-142).
+"""Detector frame ingest: letterbox + box rescaling on the HIP runtime
+(victim_localization/yolov3/utils/datasets.py:508-522 load_image, :599-631 letterbox;
+utils/utils.py:123-142 scale_coords / clip_coords).
 
-The reference decodes with cv2 and resizes with cv2.INTER_AREA; cv2 is not part of
-this stack, so shrinking uses Pillow's BOX filter and growing BILINEAR (pixel parity
-with cv2 is unpinned: cv2 is absent here).  Geometry — the scale ratio, the unpadded
-size, the split of the padding, the label/box transforms — follows the reference
+The resize runs on the device (``rtdm_letterbox``): cv2.INTER_AREA semantics — area
+averaging when shrinking, INTER_AREA's linear coefficients when growing — restated from
+OpenCV's published algorithm because cv2 is not part of this stack (pixel parity with
+cv2 is unpinned; the kernel is bit-exact against oracle/letterbox.py).  JPEG decoding
+stays on the host (Pillow): there is no rocJPEG in this ROCm image.  The geometry —
+scale ratio, unpadded size, padding split, label transforms — follows the reference
 exactly, so boxes map back to the same source coordinates.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
+import torch
+
+from . import _lib as L
 
 
-def resize(img: np.ndarray, size_wh) -> np.ndarray:
-    from PIL import Image
-    w, h = int(size_wh[0]), int(size_wh[1])
-    if (img.shape[1], img.shape[0]) == (w, h):
-        return img
-    shrink = w < img.shape[1] or h < img.shape[0]
-    return np.asarray(Image.fromarray(img).resize((w, h), Image.BOX if shrink else Image.BILINEAR), np.uint8)
+def geometry(in_h: int, in_w: int, new_shape=416, auto: bool = True, scale_fill: bool = False,
+             scaleup: bool = True):
+    """letterbox() shape arithmetic (datasets.py:603-627) ->
+    (new_h, new_w, out_h, out_w, top, left), computed by rtdm_letterbox_geometry."""
+    if isinstance(new_shape, int):
+        new_shape = (new_shape, new_shape)
+    g = (ctypes.c_int * 6)()
+    L.check(L.lib().rtdm_letterbox_geometry(int(in_h), int(in_w), int(new_shape[0]), int(new_shape[1]), int(auto),
+                                            int(scale_fill), int(scaleup), g))
+    return tuple(g)
 
 
-def load_image(img: np.ndarray, img_size: int, augment: bool = False):
-    """datasets.py:508-522: shrink so the longer side is img_size (never grow at test time).
-    Returns (img, (h0, w0), (h, w))."""
-    h0, w0 = img.shape[:2]
+def ratio_pad(in_h: int, in_w: int, new_shape=416, auto: bool = True, scaleup: bool = True):
+    """The (ratio, (dw, dh)) pair letterbox() returns (datasets.py:631)."""
+    if isinstance(new_shape, int):
+        new_shape = (new_shape, new_shape)
+    r = max(new_shape) / max(in_h, in_w)
+    if not scaleup:
+        r = min(r, 1.0)
+    nw, nh = int(round(in_w * r)), int(round(in_h * r))
+    dw, dh = new_shape[1] - nw, new_shape[0] - nh
+    if auto:
+        dw, dh = dw % 32, dh % 32
+    return (r, r), (dw / 2, dh / 2)
+
+
+def dataset_geometry(h0: int, w0: int, img_size: int):
+    """LoadImagesAndLabels evaluation path: load_image shrinks to (int(w0*r), int(h0*r))
+    (datasets.py:515-520, never grows), then letterbox(auto=False, scaleup=False) pads to
+    img_size² without a second resize.  Returns (geom, (h, w), ratio, pad)."""
     r = img_size / max(h0, w0)
-    if r < 1 or (augment and r != 1):
-        img = resize(img, (int(w0 * r), int(h0 * r)))
-    return img, (h0, w0), img.shape[:2]
+    h, w = (int(h0 * r), int(w0 * r)) if r < 1 else (h0, w0)
+    g = geometry(h, w, img_size, auto=False, scaleup=False)
+    ratio, pad = ratio_pad(h, w, img_size, auto=False, scaleup=False)
+    # the second letterbox never resizes (ratio 1): the device resize goes h0 x w0 -> g's new size
+    return g, (h, w), ratio, pad
+
+
+def letterbox_frames(frames: torch.Tensor, geom, color=(128, 128, 128), bgr: bool = False,
+                     out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """frames: uint8 [N, H, W, 3] on the GPU (rows may be pitched: stride(1) >= 3*W, unit
+    channel/pixel strides) -> [N, out_h, out_w, 3] uint8 RGB letterboxed frames, the
+    detector's RTDM_INPUT_FRAME_U8 input.  bgr=True reads cv2-order frames."""
+    if not frames.is_cuda or frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3:
+        raise ValueError("letterbox_frames: frames must be uint8 [N,H,W,3] on the GPU")
+    if frames.stride(3) != 1 or frames.stride(2) != 3 or frames.stride(0) != frames.stride(1) * frames.shape[1]:
+        frames = frames.contiguous()
+    n, h, w, _ = frames.shape
+    new_h, new_w, out_h, out_w, top, left = geom
+    if out is None:
+        out = torch.empty((n, out_h, out_w, 3), dtype=torch.uint8, device=frames.device)
+    if tuple(out.shape) != (n, out_h, out_w, 3) or not out.is_contiguous():
+        raise ValueError("letterbox_frames: out must be a contiguous [N, out_h, out_w, 3] uint8 tensor")
+    pad = int(color[0]) | (int(color[1]) << 8) | (int(color[2]) << 16)
+    with torch.cuda.device(frames.device):
+        L.check(L.lib().rtdm_letterbox(L.ptr(frames), n, h, w, frames.stride(1), new_h, new_w, out_h, out_w, top,
+                                       left, pad, int(bgr), L.ptr(out), L.stream_ptr(stream)))
+    return out
 
 
 def letterbox(img: np.ndarray, new_shape=416, color=(128, 128, 128), auto: bool = True, scaleFill: bool = False,
-              scaleup: bool = True):
-    """datasets.py:599-631.  Returns (img, (ratio_w, ratio_h), (dw, dh)) with dw/dh the
-    per-side padding before rounding (float, as the reference returns it)."""
-    shape = img.shape[:2]
-    if isinstance(new_shape, int):
-        new_shape = (new_shape, new_shape)
-    r = max(new_shape) / max(shape)
-    if not scaleup:
-        r = min(r, 1.0)
-    ratio = r, r
-    new_unpad = int(round(shape[1] * r)), int(round(shape[0] * r))
-    dw, dh = new_shape[1] - new_unpad[0], new_shape[0] - new_unpad[1]
-    if auto:
-        dw, dh = np.mod(dw, 32), np.mod(dh, 32)
-    elif scaleFill:
-        dw, dh = 0.0, 0.0
-        new_unpad = new_shape
-        ratio = new_shape[0] / shape[1], new_shape[1] / shape[0]
-    dw /= 2
-    dh /= 2
-    if shape[::-1] != tuple(new_unpad):
-        img = resize(img, new_unpad)
-    top, bottom = int(round(dh - 0.1)), int(round(dh + 0.1))
-    left, right = int(round(dw - 0.1)), int(round(dw + 0.1))
-    out = np.empty((img.shape[0] + top + bottom, img.shape[1] + left + right, 3), np.uint8)
-    out[...] = np.asarray(color, np.uint8)
-    out[top:top + img.shape[0], left:left + img.shape[1]] = img
-    return out, ratio, (dw, dh)
+              scaleup: bool = True, device=None):
+    """datasets.py:599-631 for one host image, resized on the GPU.  Returns
+    (img [h, w, 3] uint8 numpy, (ratio_w, ratio_h), (dw, dh)) like the reference."""
+    g = geometry(img.shape[0], img.shape[1], new_shape, auto, scaleFill, scaleup)
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    x = torch.from_numpy(np.ascontiguousarray(img))[None].to(dev)
+    out = letterbox_frames(x, g, color)
+    ratio, pad = ratio_pad(img.shape[0], img.shape[1], new_shape, auto, scaleup)
+    if scaleFill:
+        ratio, pad = (g[1] / img.shape[1], g[0] / img.shape[0]), (0.0, 0.0)
+    return out[0].cpu().numpy(), ratio, pad
 
 
 def scale_coords(img1_shape, coords, img0_shape, ratio_pad=None):

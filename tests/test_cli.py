@@ -42,18 +42,20 @@ def test_classification_metrics_match_confusion_definitions():
 
 
 def test_letterbox_and_scale_coords():
+    """detect.py's letterbox geometry (rtdm_letterbox_geometry, no GPU needed) and
+    scale_coords mapping a letterboxed box back to the source."""
     det = _load_cli("detect")
-    img = np.zeros((300, 500, 3), np.uint8)
-    out, (r, _), (dw, dh) = det.letterbox(img, 416)   # ratio is (w, h) as datasets.py:614
-    assert out.shape[1] == 416 and out.shape[0] % 32 == 0 and out.shape[0] >= 250
-    sq, _, _ = det.letterbox(img, 416, auto=False)
-    assert sq.shape[:2] == (416, 416)
+    g = det.geometry(300, 500, 416)                     # auto=True (LoadImages)
+    assert g[3] == 416 and g[2] % 32 == 0 and g[2] >= 250
+    assert det.geometry(300, 500, 416, auto=False)[2:4] == (416, 416)
+    from rtdm.letterbox import ratio_pad
+    (r, _), (dw, dh) = ratio_pad(300, 500, 416)          # ratio is (w, h) as datasets.py:614
     # a box in source coordinates -> letterboxed -> scale_coords back
     box = np.array([[50.0, 40.0, 200.0, 260.0]])
     lb = box * r
     lb[:, [0, 2]] += dw
     lb[:, [1, 3]] += dh
-    back = det.scale_coords(out.shape[:2], torch.tensor(lb), img.shape)
+    back = det.scale_coords((g[2], g[3]), torch.tensor(lb), (300, 500, 3))
     assert np.allclose(back.numpy(), box, atol=0.6)
 
 

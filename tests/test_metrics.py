@@ -114,29 +114,51 @@ def test_detection_stats_empty():
 
 
 def test_letterbox_geometry():
-    """datasets.py:599-631 geometry (ratio, unpadded size, padding split) and
-    utils.py:123-136 scale_coords inverting it; labels re-normalised like
-    datasets.py:441-482."""
-    from rtdm.letterbox import labels_to_letterbox, letterbox, load_image, scale_coords
-    img0 = np.random.default_rng(0).integers(0, 255, (300, 500, 3), dtype=np.uint8)
-    img, (h0, w0), (h, w) = load_image(img0, 416)
-    assert (h0, w0) == (300, 500) and (h, w) == (int(300 * 416 / 500), 416)
-    out, ratio, pad = letterbox(img, 416, auto=False, scaleup=False)
-    assert out.shape == (416, 416, 3) and ratio == (1.0, 1.0)
-    assert pad == (0.0, (416 - h) / 2)
-    assert (out[0] == 128).all() and (out[-1] == 128).all()
-    out_auto, _, pad_a = letterbox(img0, 416)           # LoadImages (detect.py) form
-    assert out_auto.shape[1] == 416 and out_auto.shape[0] % 32 == 0
+    """datasets.py:599-631 geometry (ratio, unpadded size, padding split; rtdm_letterbox_geometry
+    against the oracle restatement over many shapes and flags), the LoadImagesAndLabels
+    composition (load_image shrink + square pad), and utils.py:123-136 scale_coords
+    inverting it; labels re-normalised like datasets.py:441-482."""
+    from oracle import letterbox as OL
+    from rtdm.letterbox import dataset_geometry, geometry, labels_to_letterbox, scale_coords
+    rng = np.random.default_rng(5)
+    shapes = [(300, 500), (480, 640), (416, 416), (1080, 1920), (200, 100), (833, 411), (5, 7)]
+    shapes += [tuple(int(v) for v in rng.integers(1, 2000, 2)) for _ in range(40)]
+    for (h, w) in shapes:
+        for new in (416, 608, (320, 416)):
+            for auto in (True, False):
+                for up in (True, False):
+                    assert geometry(h, w, new, auto, False, up) == OL.geometry(h, w, new, auto, False, up), \
+                        (h, w, new, auto, up)
+    g, (h, w), ratio, pad = dataset_geometry(300, 500, 416)
+    assert (h, w) == (int(300 * 416 / 500), 416) and ratio == (1.0, 1.0)
+    assert g == (h, w, 416, 416, int(round(pad[1] - 0.1)), 0) and pad == (0.0, (416 - h) / 2)
+    assert dataset_geometry(200, 300, 416)[0][:2] == (200, 300)     # never grows
     lab = np.array([[1, 0.5, 0.5, 0.2, 0.4]], np.float32)
     ll = labels_to_letterbox(lab, ratio, pad, h, w, 416, 416)
     assert np.allclose(ll[0], [1, 0.5, 0.5, 0.2, 0.4 * h / 416], atol=1e-6)
-    g = 416 / 500
-    py = (416 - 300 * g) / 2     # scale_coords' own padding (from the source shape, not load_image's int())
+    gn = 416 / 500
+    py = (416 - 300 * gn) / 2    # scale_coords' own padding (from the source shape, not load_image's int())
     box = torch.tensor([[100.0, 50.0 + py, 200.0, 150.0 + py]])
     back = scale_coords((416, 416), box.clone(), (300, 500))
-    assert torch.allclose(back, torch.tensor([[100 / g, 50 / g, 200 / g, 150 / g]]), atol=1e-3)
+    assert torch.allclose(back, torch.tensor([[100 / gn, 50 / gn, 200 / gn, 150 / gn]]), atol=1e-3)
     far = scale_coords((416, 416), torch.tensor([[-50.0, -50.0, 900.0, 900.0]]), (300, 500))
     assert far[0, 0] < 0 and far[0, 2] > 500    # reference clip_coords is a no-op
+
+
+def test_oracle_letterbox_resize_properties():
+    """Known answers for the INTER_AREA restatement: integral shrink = rounded box mean;
+    constant frames stay constant in all three modes; pad colour outside the frame."""
+    from oracle import letterbox as OL
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (64, 96, 3), dtype=np.uint8)
+    fast = OL.resize_area(img, 48, 32)
+    mean = img.reshape(32, 2, 48, 2, 3).astype(np.float64).mean(axis=(1, 3))
+    assert np.abs(fast.astype(np.float64) - mean).max() <= 0.5
+    for (nw, nh) in ((48, 32), (37, 29), (150, 100), (80, 100)):
+        c = np.full((64, 96, 3), 77, np.uint8)
+        assert (OL.resize_area(c, nw, nh) == 77).all(), (nw, nh)
+    out = OL.letterbox(img, OL.geometry(64, 96, 128, auto=False), color=(1, 2, 3))
+    assert out.shape == (128, 128, 3) and (out[0, 0] == [1, 2, 3]).all()
 
 
 def test_classification_metrics_known_answer():
