@@ -167,6 +167,8 @@ __device__ __forceinline__ uint8_t sat_round(float v) {
 }
 
 __global__ void __launch_bounds__(256) letterbox_kernel(LbArgs a) {
+  // the restated float sums round every product and sum: no FMA contraction here
+#pragma clang fp contract(off)
   const int64_t npx = (int64_t)a.out_h * a.out_w;
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npx) return;
@@ -191,9 +193,9 @@ __global__ void __launch_bounds__(256) letterbox_kernel(LbArgs a) {
         s1 += row[3 * k + 1];
         s2 += row[3 * k + 2];
       }
-    r[0] = sat_round(__fmul_rn((float)s0, a.inv_area));
-    r[1] = sat_round(__fmul_rn((float)s1, a.inv_area));
-    r[2] = sat_round(__fmul_rn((float)s2, a.inv_area));
+    r[0] = sat_round((float)s0 * a.inv_area);
+    r[1] = sat_round((float)s1 * a.inv_area);
+    r[2] = sat_round((float)s2 * a.inv_area);
   } else if (a.mode == LB_AREA) {
     const int* xs = (const int*)a.tab;
     const float* xw = (const float*)(xs + (int64_t)a.new_w * a.tx);
@@ -210,19 +212,19 @@ __global__ void __launch_bounds__(256) letterbox_kernel(LbArgs a) {
       for (int k = 0; k < a.tx; ++k) {
         const uint8_t* s = row + xs[k] * 3;
         const float w = xw[k];
-        h0 = __fadd_rn(h0, __fmul_rn((float)s[0], w));
-        h1 = __fadd_rn(h1, __fmul_rn((float)s[1], w));
-        h2 = __fadd_rn(h2, __fmul_rn((float)s[2], w));
+        h0 = h0 + (float)s[0] * w;
+        h1 = h1 + (float)s[1] * w;
+        h2 = h2 + (float)s[2] * w;
       }
       const float b = yw[j];
       if (j == 0) {
-        v0 = __fmul_rn(b, h0);
-        v1 = __fmul_rn(b, h1);
-        v2 = __fmul_rn(b, h2);
+        v0 = b * h0;
+        v1 = b * h1;
+        v2 = b * h2;
       } else {
-        v0 = __fadd_rn(v0, __fmul_rn(b, h0));
-        v1 = __fadd_rn(v1, __fmul_rn(b, h1));
-        v2 = __fadd_rn(v2, __fmul_rn(b, h2));
+        v0 = v0 + b * h0;
+        v1 = v1 + b * h1;
+        v2 = v2 + b * h2;
       }
     }
     r[0] = sat_round(v0);
