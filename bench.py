@@ -142,7 +142,7 @@ def pmc_traffic(kernel):
     FETCH_SIZE doubled per the gfx950 correction).  None when no pass covers it."""
     import glob
     base = kernel.split("<")[0]
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))  # tags sort by round
     for path in reversed(files):
         try:
             d = json.load(open(path))
