@@ -56,6 +56,8 @@ def parse():
                     help="1: classifier on a side stream beside the detector; 0: both stages serial")
     ap.add_argument("--priority", type=int, default=0,
                     help="1: detector + NMS on a high-priority stream, classifier on a low-priority one")
+    ap.add_argument("--step-events", type=int, default=1,
+                    help="0: no per-step hipEvents in the timed region (roofline fields then null)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU oracle leg")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="CPU oracle leg: time chunks of 16 frames until this much CPU time has passed")
@@ -204,7 +206,8 @@ def main():
     torch.cuda.synchronize()
     h, steps = step_table(det, b)
     from rtdm import _lib as L
-    L.check(L.lib().rtdm_detector_enable_timing(h, args.steps))
+    if args.step_events:
+        L.check(L.lib().rtdm_detector_enable_timing(h, args.steps))
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -222,8 +225,9 @@ def main():
         elapsed = float(t.item())
     ms = (ctypes.c_double * len(steps))()
     calls = ctypes.c_int()
-    L.check(L.lib().rtdm_detector_read_timing(h, ms, ctypes.byref(calls)))
-    L.check(L.lib().rtdm_detector_enable_timing(h, 0))
+    if args.step_events:
+        L.check(L.lib().rtdm_detector_read_timing(h, ms, ctypes.byref(calls)))
+        L.check(L.lib().rtdm_detector_enable_timing(h, 0))
     # roofline: kernel symbol with the largest summed device time
     agg = {}
     for (name, layer, flop, byt), t in zip(steps, ms):
@@ -235,8 +239,8 @@ def main():
     dom = max(agg, key=lambda k: agg[k][0])
     t_ms, flop, byt, launches = agg[dom]
     det_ms = sum(ms) / max(1, calls.value)
-    avg_ms = t_ms / launches
-    achieved_tflops = (flop / launches) / (avg_ms * 1e-3) / 1e12
+    avg_ms = t_ms / launches if launches else 0.0
+    achieved_tflops = (flop / launches) / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     tr = pmc_traffic(dom)
     traffic = round(tr["bytes_per_launch"]) if tr else None
     frames_total = world * b * args.steps
@@ -259,7 +263,7 @@ def main():
                      "frac": round(achieved_tflops / MFMA_F16_DENSE_PEAK_TFLOPS, 4), "traffic": traffic,
                      "avg_launch_ms": round(avg_ms, 4), "launches": launches,
                      "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tr["source"] if tr else None,
-                     "algorithmic_bytes_per_launch": round(byt / launches)},
+                     "algorithmic_bytes_per_launch": round(byt / launches) if launches else None},
         "pipeline": {"flop_per_frame": pipe_flop,
                      "pipeline_tflops": round(pipe_flop * value / world / 1e12, 2),
                      "pipeline_frac": round(pipe_flop * value / world / 1e12 / MFMA_F16_DENSE_PEAK_TFLOPS, 4),

@@ -247,6 +247,66 @@ __device__ __forceinline__ void epi_vec8(const ConvArgs& a, int m0, int c0, cons
   }
 }
 
+// Lean variant of epi_vec8 for the common Darknet conv (bias -> leaky/linear ->
+// optional scale/shift -> full / 2x2-pool / x2-upsample outputs), with every view
+// 8-channel aligned and 8 valid channels (checked on the host by epi_lean_ok).  No
+// residual, swish or YOLO decode paths: the generic epilogue compiles to ~7k
+// instructions, and fetching them cold at every tile's end cost ~10 us per tile
+// round in the MFMA-bound convs (tools/ab_conv.py modes 8-10).
+__device__ __forceinline__ void epi_vec8_lean(const ConvArgs& a, int m0, int c0, const float (&v)[4][8],
+                                              const float (&bias)[8], const float (&sc)[8], const float (&sh)[8]) {
+  const Epilogue& e = a.e;
+  float pmax[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pmax[j] = -INFINITY;
+  int pn, poy, pox;
+  row_to_pix(a, m0, pn, poy, pox);
+  const bool leaky = e.act == ACT_LEAKY;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + r;
+    if (m >= a.M) continue;
+    int n, oy, ox;
+    row_pix4(a, m0, r, pn, poy, pox, n, oy, ox);
+    const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
+    h8v hv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = v[r][j] + bias[j];
+      t = leaky ? (t > 0.f ? t : t * e.slope) : t;
+      t = t * sc[j] + sh[j];
+      hv[j] = (_Float16)t;
+      pmax[j] = fmaxf(pmax[j], t);
+    }
+    if (e.full.ptr) *(h8v*)((_Float16*)e.full.ptr + pix * e.full.cs + e.full.co + c0) = hv;
+    if (e.up.ptr) {
+      const int uw = a.ow * 2;
+      const size_t u0 = ((size_t)n * a.oh * 2 + 2 * oy) * uw + 2 * ox;
+      _Float16* up = (_Float16*)e.up.ptr + e.up.co + c0;
+      *(h8v*)(up + u0 * e.up.cs) = hv;
+      *(h8v*)(up + (u0 + 1) * e.up.cs) = hv;
+      *(h8v*)(up + (u0 + uw) * e.up.cs) = hv;
+      *(h8v*)(up + (u0 + uw + 1) * e.up.cs) = hv;
+    }
+  }
+  if (e.pool.ptr && a.quad && m0 < a.M) {
+    const size_t pp = ((size_t)pn * a.qh + (poy >> 1)) * a.qw + (pox >> 1);
+    h8v pv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pv[j] = (_Float16)pmax[j];
+    *(h8v*)((_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0) = pv;
+  }
+}
+
+inline bool epi_lean_ok(const ConvArgs& a) {
+  const Epilogue& e = a.e;
+  if (e.res.ptr || e.io || (e.act != ACT_LEAKY && e.act != ACT_LINEAR) || a.cout % 8 != 0) return false;
+  if (!e.bias || (e.scale && !e.shift)) return false;
+  for (const View* v : {&e.full, &e.pool, &e.up})
+    if (v->ptr && ((v->cs | v->co) & 7) != 0) return false;
+  return !e.pool.ptr || a.quad;
+}
+
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 

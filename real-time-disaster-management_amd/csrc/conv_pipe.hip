@@ -76,7 +76,9 @@ __device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v
 
 // ABL: ablation bits for diagnostic builds only (outputs are wrong when non-zero):
 // 1 = no buffer->LDS loads in the K-loop, 2 = no fragment ds_reads in the K-loop,
-// 4 = no wait + barrier in the K-loop.  Bit 8 (not an ablation): fused YOLO head.
+// 4 = no wait + barrier in the K-loop, 16 = no epilogue (one guarded store keeps the
+// MFMAs live), 32 = no K-loop (prologue + epilogue only).  Bit 8 (not an ablation):
+// fused YOLO head; bit 128 (not an ablation): lean epilogue (epi_vec8_lean).
 template <int ABL>
 __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
   constexpr int WM = 4, WN = 2;
@@ -276,9 +278,11 @@ __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  for (int kb = 0; kb + 2 < nk; ++kb) body(T_{}, T_{});
-  if (nk >= 2) body(F_{}, T_{});
-  body(F_{}, F_{});
+  if constexpr (!(ABL & 32)) {
+    for (int kb = 0; kb + 2 < nk; ++kb) body(T_{}, T_{});
+    if (nk >= 2) body(F_{}, T_{});
+    body(F_{}, F_{});
+  }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -339,7 +343,30 @@ __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
     return;
   }
 
+  if constexpr ((ABL & 16) != 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < FN; ++tn) t += acc[tm][tn][0] + acc[tm][tn][1] + acc[tm][tn][2] + acc[tm][tn][3];
+    if (t == 1234.5f) ((float*)a.e.full.ptr)[tid] = t;
+    return;
+  }
   // ---- epilogue: accumulators -> LDS C tile (fp32) -> 4 rows x 8 channels per thread ----
+  // lean epilogue: this thread's 8 channels are the same in both of its units
+  // (NT % CG == 0), so bias/scale/shift are loaded once, before the C-tile pass
+  constexpr int CG = BN / 8;
+  float lb[8], ls[8], lh[8];
+  if constexpr ((ABL & 128) != 0) {
+    const int c0 = n_base + (tid % CG) * 8;
+    const bool cv = c0 < a.cout;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lb[j] = cv ? a.e.bias[c0 + j] : 0.f;
+      ls[j] = cv && a.e.scale ? a.e.scale[c0 + j] : 1.f;
+      lh[j] = cv && a.e.scale ? a.e.shift[c0 + j] : 0.f;
+    }
+  }
   float* Cs = reinterpret_cast<float*>(smem_raw);
   const int rq = g * 4;
 #pragma unroll
@@ -352,10 +379,14 @@ __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
       for (int j = 0; j < 4; ++j) Cs[(row + j) * kPCstr + col] = acc[tm][tn][j];
     }
   __syncthreads();
-  constexpr int CG = BN / 8;
   constexpr int UNITS = (BM / 4) * CG;
+  static_assert(NT % CG == 0, "channel group per thread");
   for (int u = tid; u < UNITS; u += NT) {
     const int q = u / CG, gg = u - (u / CG) * CG;
+    if constexpr ((ABL & 64) != 0) {
+      if (Cs[(q * 4) * kPCstr + gg * 8] == 1234.5f) ((float*)a.e.full.ptr)[tid] = 0.f;
+      continue;
+    }
     const int m0 = m_base + q * 4, c0 = n_base + gg * 8;
     if (m0 >= a.M || c0 >= a.cout) continue;
     float v[4][8];
@@ -363,7 +394,10 @@ __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[r][j] = Cs[(q * 4 + r) * kPCstr + gg * 8 + j];
-    epi_vec8(a, m0, c0, v);
+    if constexpr ((ABL & 128) != 0)
+      epi_vec8_lean(a, m0, c0, v, lb, ls, lh);
+    else
+      epi_vec8(a, m0, c0, v);
   }
 }
 
@@ -383,7 +417,9 @@ bool conv_pipe_ok(const ConvArgs& a) {
 
 // mode (conv_pipe_mode): 1 = the kernel; 2..5 = ablation builds for diagnostics
 // (tools/ab_conv.py; outputs wrong): 2 no loads, 3 no ds_reads, 4 neither, 5 no
-// barrier.
+// barrier, 6 no epilogue, 7 bare MFMA loop (no loads, reads or epilogue), 8 no K-loop,
+// 9 neither K-loop nor epilogue, 10 no K-loop and no global epilogue stores (bit 64),
+// 11 the generic epilogue where the lean one applies (correct outputs).
 void launch_conv_pipe(const ConvArgs& a, hipStream_t s) {
   const int64_t nblk = (int64_t)((a.M + kPBM - 1) / kPBM) * (a.cout_pad / kPBN);
   RTDM_REQUIRE(nblk < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
@@ -397,7 +433,18 @@ void launch_conv_pipe(const ConvArgs& a, hipStream_t s) {
     case 3: hipLaunchKernelGGL((conv_pipe_f16<2>), grid, dim3(512), 0, s, a); break;
     case 4: hipLaunchKernelGGL((conv_pipe_f16<3>), grid, dim3(512), 0, s, a); break;
     case 5: hipLaunchKernelGGL((conv_pipe_f16<4>), grid, dim3(512), 0, s, a); break;
-    default: hipLaunchKernelGGL((conv_pipe_f16<0>), grid, dim3(512), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((conv_pipe_f16<16>), grid, dim3(512), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((conv_pipe_f16<19>), grid, dim3(512), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((conv_pipe_f16<32>), grid, dim3(512), 0, s, a); break;
+    case 9: hipLaunchKernelGGL((conv_pipe_f16<48>), grid, dim3(512), 0, s, a); break;
+    case 10: hipLaunchKernelGGL((conv_pipe_f16<96>), grid, dim3(512), 0, s, a); break;
+    case 11: hipLaunchKernelGGL((conv_pipe_f16<0>), grid, dim3(512), 0, s, a); break;
+    default:
+      if (epi_lean_ok(a))
+        hipLaunchKernelGGL((conv_pipe_f16<128>), grid, dim3(512), 0, s, a);
+      else
+        hipLaunchKernelGGL((conv_pipe_f16<0>), grid, dim3(512), 0, s, a);
+      break;
   }
 }
 
