@@ -35,7 +35,8 @@ namespace rtdm {
 // Blocks are remapped so that consecutive tiles of one M row-panel (sharing the
 // A rows) run on the same XCD (blocks b, b+8, ... share an XCD's L2).
 // --------------------------------------------------------------------------
-template <int BM, int BN, int BK, int WM, int WN>
+// EK: epilogue instantiation — 0 generic epi_vec8, 1 epi_vec8_lean, 2 epi_vec8_io
+template <int BM, int BN, int BK, int WM, int WN, int EK = 0>
 __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_f16(ConvArgs a) {
   constexpr int NT = 64 * WM * WN;
   constexpr int KV = BK / 8;          // 16-byte vectors per row of a K-block
@@ -174,6 +175,18 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_f16(ConvArgs a) {
   __syncthreads();
   constexpr int CG = BN / 8;
   constexpr int UNITS = (BM / 4) * CG;
+  float lb[8], ls[8], lh[8];
+  if constexpr (EK == 1) {
+    static_assert(NT % CG == 0, "channel group per thread");
+    const int c0 = n_base + (tid % CG) * 8;
+    const bool cv = c0 < a.cout;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lb[j] = cv ? a.e.bias[c0 + j] : 0.f;
+      ls[j] = cv && a.e.scale ? a.e.scale[c0 + j] : 1.f;
+      lh[j] = cv && a.e.scale ? a.e.shift[c0 + j] : 0.f;
+    }
+  }
   for (int u = tid; u < UNITS; u += NT) {
     const int q = u / CG, g = u - (u / CG) * CG;
     const int m0 = m_base + q * 4, c0 = n_base + g * 8;
@@ -183,7 +196,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_f16(ConvArgs a) {
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[r][j] = Cs[(q * 4 + r) * CSTR + g * 8 + j];
-    epi_vec8(a, m0, c0, v);
+    if constexpr (EK == 1)
+      epi_vec8_lean(a, m0, c0, v, lb, ls, lh);
+    else if constexpr (EK == 2)
+      epi_vec8_io(a, m0, c0, v);
+    else
+      epi_vec8(a, m0, c0, v);
   }
 }
 
@@ -1206,7 +1224,13 @@ static void launch_mfma(const ConvArgs& a, hipStream_t s) {
   RTDM_REQUIRE(a.kpad % BK == 0, RTDM_E_INVALID, "conv: kpad not a multiple of BK");
   const int64_t nblk = (int64_t)((a.M + BM - 1) / BM) * (a.cout_pad / BN);
   RTDM_REQUIRE(nblk < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
-  hipLaunchKernelGGL((conv_mfma_f16<BM, BN, BK, WM, WN>), dim3((unsigned)nblk), dim3(64 * WM * WN), 0, s, a);
+  const dim3 grid((unsigned)nblk), block(64 * WM * WN);
+  if (epi_lean_ok(a))
+    hipLaunchKernelGGL((conv_mfma_f16<BM, BN, BK, WM, WN, 1>), grid, block, 0, s, a);
+  else if (epi_io_ok(a))
+    hipLaunchKernelGGL((conv_mfma_f16<BM, BN, BK, WM, WN, 2>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_mfma_f16<BM, BN, BK, WM, WN, 0>), grid, block, 0, s, a);
 }
 
 static bool mfma_ok(const ConvArgs& a) {

@@ -298,6 +298,63 @@ __device__ __forceinline__ void epi_vec8_lean(const ConvArgs& a, int m0, int c0,
   }
 }
 
+// YOLO-head variant of epi_vec8: bias -> activation -> optional scale/shift -> decode
+// (or raw) into io, the only output.  Same operations, in the same order, as the io
+// branch of epi_vec8 (bit-identical), without the code of the other branches.
+__device__ __forceinline__ void epi_vec8_io(const ConvArgs& a, int m0, int c0, const float (&v)[4][8]) {
+  const Epilogue& e = a.e;
+  const int nc = a.cout - c0 < 8 ? a.cout - c0 : 8;
+  float bias[8], sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool cv = j < nc;
+    bias[j] = (e.bias && cv) ? e.bias[c0 + j] : 0.f;
+    sc[j] = (e.scale && cv) ? e.scale[c0 + j] : 1.f;
+    sh[j] = (e.scale && cv) ? e.shift[c0 + j] : 0.f;
+  }
+  int pn, poy, pox;
+  row_to_pix(a, m0, pn, poy, pox);
+  const size_t plane = (size_t)a.oh * a.ow;
+  const int ai0 = c0 / e.no, k0 = c0 - ai0 * e.no;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + r;
+    if (m >= a.M) continue;
+    int n, oy, ox;
+    row_pix4(a, m0, r, pn, poy, pox, n, oy, ox);
+    const size_t pix_io = (size_t)n * e.io_rows + e.io_off + (size_t)oy * a.ow + ox;
+    int ai = ai0, k = k0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (j < nc) {
+        float t = v[r][j] + bias[j];
+        if (e.act == ACT_LEAKY) t = t > 0.f ? t : t * e.slope;
+        const float x = t * sc[j] + sh[j];
+        float o;
+        if (e.raw)
+          o = x;
+        else if (k < 2)
+          o = (__frcp_rn(1.f + __expf(-x)) + (float)(k == 0 ? ox : oy)) * e.ystride;
+        else if (k < 4)
+          o = (__expf(x) * e.anchor_vec[2 * ai + (k - 2)]) * e.ystride;
+        else
+          o = __frcp_rn(1.f + __expf(-x));
+        e.io[(pix_io + (size_t)ai * plane) * e.no + k] = o;
+      }
+      if (++k == e.no) {
+        k = 0;
+        ++ai;
+      }
+    }
+  }
+}
+
+inline bool epi_io_ok(const ConvArgs& a) {
+  const Epilogue& e = a.e;
+  return e.io && !e.res.ptr && !e.full.ptr && !e.pool.ptr && !e.up.ptr &&
+         (e.act == ACT_LEAKY || e.act == ACT_LINEAR) && (!e.scale || e.shift);
+}
+
 inline bool epi_lean_ok(const ConvArgs& a) {
   const Epilogue& e = a.e;
   if (e.res.ptr || e.io || (e.act != ACT_LEAKY && e.act != ACT_LINEAR) || a.cout % 8 != 0) return false;
