@@ -79,8 +79,9 @@ __device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v
 // 4 = no wait + barrier in the K-loop, 16 = no epilogue (one guarded store keeps the
 // MFMAs live), 32 = no K-loop (prologue + epilogue only).  Bit 8 (not an ablation):
 // fused YOLO head; bit 128 (not an ablation): lean epilogue (epi_vec8_lean).
+// One 256 x 128 output tile (logical tile index bid, M-major over N tiles).
 template <int ABL>
-__global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
+__device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem_raw, int bid) {
   constexpr int WM = 4, WN = 2;
   constexpr int BM = kPBM, BN = kPBN, BK = kPBK;
   constexpr int WAVES = WM * WN, NT = 64 * WAVES;
@@ -89,18 +90,12 @@ __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
   constexpr int NB = BN * BK * 2 / (NT * 16);          // B ops
   constexpr int VM = NA + NB;
   static_assert(VM == 6 || VM == 12, "wait literal");
-  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kPSmem];
   _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int ntn = a.cout_pad / BN;
-  int bid = blockIdx.x;
-  {  // bijective XCD remap: each XCD runs a contiguous run of tiles (shared A panels in its L2)
-    const int nblk = gridDim.x, xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
   const int mt = bid / ntn;
   const int m_base = mt * BM, n_base = (bid - mt * ntn) * BN;
 
@@ -401,6 +396,25 @@ __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a) {
   }
 }
 
+// Persistent over tiles: one workgroup per CU walks a contiguous run of tiles of its
+// XCD (A panels shared in that XCD's L2), so a tile's epilogue stores drain while the
+// next tile's first K-blocks load, instead of every CU storing, then loading, in
+// lockstep rounds.  Between tiles only LDS is fenced (lgkmcnt): the stores stay in flight.
+template <int ABL>
+__global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a, int ntiles) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kPSmem];
+  const int nb = gridDim.x, xcd = blockIdx.x & 7, l = blockIdx.x >> 3;
+  const int q = ntiles >> 3, r = ntiles & 7;
+  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int hi = lo + q + (xcd < r ? 1 : 0);
+  const int bx = (nb - xcd + 7) >> 3;  // workgroups on this XCD (>= 1: this one)
+  for (int t = lo + l; t < hi; t += bx) {
+    pipe_tile<ABL>(a, smem_raw, t);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
 
 bool conv_pipe_ok(const ConvArgs& a) {
   if (!a.zero || a.in_kind != IN_NHWC || a.w_f32 || (a.in_cs | a.in_co) % 8 != 0) return false;
@@ -420,30 +434,43 @@ bool conv_pipe_ok(const ConvArgs& a) {
 // barrier, 6 no epilogue, 7 bare MFMA loop (no loads, reads or epilogue), 8 no K-loop,
 // 9 neither K-loop nor epilogue, 10 no K-loop and no global epilogue stores (bit 64),
 // 11 the generic epilogue where the lean one applies (correct outputs).
+static int pipe_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
 void launch_conv_pipe(const ConvArgs& a, hipStream_t s) {
-  const int64_t nblk = (int64_t)((a.M + kPBM - 1) / kPBM) * (a.cout_pad / kPBN);
-  RTDM_REQUIRE(nblk < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
-  const dim3 grid((unsigned)nblk);
+  const int64_t nt = (int64_t)((a.M + kPBM - 1) / kPBM) * (a.cout_pad / kPBN);
+  RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
+  const int ntiles = (int)nt;
+  // mode 13: one workgroup per tile (non-persistent), for A/B runs
+  const int cap = conv_pipe_mode() == 13 ? ntiles : pipe_cus();
+  const dim3 grid((unsigned)(ntiles < cap ? ntiles : cap));
   if (a.head_w) {
-    hipLaunchKernelGGL((conv_pipe_f16<8>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv_pipe_f16<8>), grid, dim3(512), 0, s, a, ntiles);
     return;
   }
   switch (conv_pipe_mode()) {
-    case 2: hipLaunchKernelGGL((conv_pipe_f16<1>), grid, dim3(512), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((conv_pipe_f16<2>), grid, dim3(512), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((conv_pipe_f16<3>), grid, dim3(512), 0, s, a); break;
-    case 5: hipLaunchKernelGGL((conv_pipe_f16<4>), grid, dim3(512), 0, s, a); break;
-    case 6: hipLaunchKernelGGL((conv_pipe_f16<16>), grid, dim3(512), 0, s, a); break;
-    case 7: hipLaunchKernelGGL((conv_pipe_f16<19>), grid, dim3(512), 0, s, a); break;
-    case 8: hipLaunchKernelGGL((conv_pipe_f16<32>), grid, dim3(512), 0, s, a); break;
-    case 9: hipLaunchKernelGGL((conv_pipe_f16<48>), grid, dim3(512), 0, s, a); break;
-    case 10: hipLaunchKernelGGL((conv_pipe_f16<96>), grid, dim3(512), 0, s, a); break;
-    case 11: hipLaunchKernelGGL((conv_pipe_f16<0>), grid, dim3(512), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((conv_pipe_f16<1>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 3: hipLaunchKernelGGL((conv_pipe_f16<2>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 4: hipLaunchKernelGGL((conv_pipe_f16<3>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 5: hipLaunchKernelGGL((conv_pipe_f16<4>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 6: hipLaunchKernelGGL((conv_pipe_f16<16>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 7: hipLaunchKernelGGL((conv_pipe_f16<19>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 8: hipLaunchKernelGGL((conv_pipe_f16<32>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 9: hipLaunchKernelGGL((conv_pipe_f16<48>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 10: hipLaunchKernelGGL((conv_pipe_f16<96>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 11: hipLaunchKernelGGL((conv_pipe_f16<0>), grid, dim3(512), 0, s, a, ntiles); break;
     default:
       if (epi_lean_ok(a))
-        hipLaunchKernelGGL((conv_pipe_f16<128>), grid, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((conv_pipe_f16<128>), grid, dim3(512), 0, s, a, ntiles);
       else
-        hipLaunchKernelGGL((conv_pipe_f16<0>), grid, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((conv_pipe_f16<0>), grid, dim3(512), 0, s, a, ntiles);
       break;
   }
 }
