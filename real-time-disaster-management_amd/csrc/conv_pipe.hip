@@ -301,7 +301,10 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
         for (int j = 0; j < 4; ++j) {
           const int row = wm * (BM / WM) + tm * 16 + g * 4 + j;
           float x = acc[tm][tn][j] + bias;
-          if (e.act == ACT_LEAKY) x = x > 0.f ? x : x * e.slope;
+          if (e.act == ACT_LEAKY)
+            x = x > 0.f ? x : x * e.slope;
+          else if (e.act == ACT_SWISH)  // yolov4-tiny-swish.cfg (models.py:43-44)
+            x = x * sigmoidf_(x);
           x = cv ? x * sc + sh : 0.f;
           Hs[row * BN + 8 * ((col >> 3) ^ (row & 15)) + (col & 7)] = (_Float16)x;
         }

@@ -52,6 +52,8 @@ DET_CASES = [  # (cfg, size, n_frames, full_io)
     ("yolov3-aider-416", 416, 1, False),
     ("yolov3-spp-aider", 608, 1, False),
     ("yolov3-tiny-aider-416", 416, 1, False),
+    ("yolov4-tiny-swish", 416, 1, False),
+    ("yolov4-tiny-3l-512x512", 512, 1, False),
 ]
 NMS_SETTINGS = [(0.3, 0.4), (0.01, 0.6)]
 IO_STRIDE = 53
@@ -174,6 +176,10 @@ REF_VL = os.path.join(os.path.dirname(CLS_DIR), "victim_localization")
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    shapes_golden()
-    classifier_goldens()
-    det_goldens()
+    only = sys.argv[1:]  # e.g. "det" to regenerate only det_golden.npz
+    if not only or "shapes" in only:
+        shapes_golden()
+    if not only or "cls" in only:
+        classifier_goldens()
+    if not only or "det" in only:
+        det_goldens()

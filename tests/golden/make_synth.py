@@ -24,7 +24,8 @@ sys.path.insert(0, HERE)
 from rtdm import synth  # noqa: E402
 from refimport import DET_DIR, import_darknet  # noqa: E402
 
-CFGS = ["yolov4-tiny-aider-416", "yolov3-aider-416", "yolov3-spp-aider", "yolov3-tiny-aider-416"]
+CFGS = ["yolov4-tiny-aider-416", "yolov3-aider-416", "yolov3-spp-aider", "yolov3-tiny-aider-416",
+        "yolov4-tiny-swish", "yolov4-tiny-3l-512x512"]
 
 
 def calibrate(name: str, size: int = 416):

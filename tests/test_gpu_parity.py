@@ -207,7 +207,8 @@ def test_detector_golden_small(dev, det_golden, half):
 
 
 @pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416", "yolov3-spp-aider@608",
-                                  "yolov3-tiny-aider-416@416"])
+                                  "yolov3-tiny-aider-416@416", "yolov4-tiny-swish@416",
+                                  "yolov4-tiny-3l-512x512@512"])
 @pytest.mark.parametrize("half", [False, True])
 def test_detector_golden_full(dev, det_golden, case, half):
     from rtdm.synth import BASE_SEED, synth_frames
@@ -237,8 +238,9 @@ def test_detector_golden_full(dev, det_golden, case, half):
         assert matched / len(ref) >= (0.9 if half else 0.99), (case, matched, len(ref))
 
 
-@pytest.mark.parametrize("size", [608, 256])
-def test_detector_fused_head_matches_unfused(dev, size):
+@pytest.mark.parametrize("cfg,size", [("yolov4-tiny-aider-416", 608), ("yolov4-tiny-aider-416", 256),
+                                      ("yolov4-tiny-swish", 256)])
+def test_detector_fused_head_matches_unfused(dev, cfg, size):
     """conv -> 1x1 head -> [yolo] fused into one conv_pipe_f16 launch gives the same
     io bits as the separate head conv (same fp16 activations, same MFMA K order)."""
     from rtdm import _lib as L
@@ -248,7 +250,7 @@ def test_detector_fused_head_matches_unfused(dev, size):
     try:
         for fuse in (0, 1):
             L.check(L.lib().rtdm_set_tuning(b"fuse_head", fuse))
-            m, _, _ = _darknet("yolov4-tiny-aider-416", size, True)
+            m, _, _ = _darknet(cfg, size, True)
             io, _ = m(x)
             assert ("head1x1" in m.describe()) == bool(fuse)
             outs[fuse] = io.cpu()

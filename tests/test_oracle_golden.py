@@ -49,7 +49,8 @@ def test_darknet_oracle_matches_reference_goldens(det_golden):
     from oracle.darknet import DarknetRef
     from rtdm.synth import BASE_SEED, load_calibration, synth_darknet_weights, synth_frames
     import hashlib
-    for case in ("yolov4-tiny-aider-416@256", "yolov4-tiny-aider-416@608", "yolov3-tiny-aider-416@416"):
+    for case in ("yolov4-tiny-aider-416@256", "yolov4-tiny-aider-416@608", "yolov3-tiny-aider-416@416",
+                 "yolov4-tiny-swish@416", "yolov4-tiny-3l-512x512@512"):
         cfg, size = case.split("@")
         size = int(size)
         text = cfg_text(cfg)
