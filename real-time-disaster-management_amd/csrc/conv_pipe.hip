@@ -99,6 +99,33 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   const int mt = bid / ntn;
   const int m_base = mt * BM, n_base = (bid - mt * ntn) * BN;
 
+  // Epilogue channel constants, loaded at the tile's start so their latency hides under
+  // the K-loop.  Lean epilogue: this thread's 8 channels are the same in both of its
+  // units (NT % CG == 0).  Fused head: the FN columns of this lane's accumulators.
+  constexpr int CG = BN / 8;
+  float lb[8], ls[8], lh[8];
+  if constexpr ((ABL & 128) != 0) {
+    const int c0 = n_base + (tid % CG) * 8;
+    const bool cv = c0 < a.cout;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lb[j] = cv ? a.e.bias[c0 + j] : 0.f;
+      ls[j] = cv && a.e.scale ? a.e.scale[c0 + j] : 1.f;
+      lh[j] = cv && a.e.scale ? a.e.shift[c0 + j] : 0.f;
+    }
+  }
+  float hb[FN], hs[FN], hh[FN];
+  if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+    for (int tn = 0; tn < FN; ++tn) {
+      const int col = wn * (BN / WN) + tn * 16 + (lane & 15);
+      const bool cv = col < a.cout;
+      hb[tn] = cv ? a.e.bias[col] : 0.f;
+      hs[tn] = (cv && a.e.scale) ? a.e.scale[col] : 1.f;
+      hh[tn] = (cv && a.e.scale) ? a.e.shift[col] : 0.f;
+    }
+  }
+
   // ---- per-lane staging state.  A op j of wave w fills tile rows 8(NA w + j) + lane/8,
   //      B op j rows 8(NB w + j) + lane/8; LDS slot lane%8 of a row holds k-vector
   //      slot ^ ((row >> 1) & 7) (the read side applies the same involution). ----
@@ -292,9 +319,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     for (int tn = 0; tn < FN; ++tn) {
       const int col = wn * (BN / WN) + tn * 16 + fr;
       const bool cv = col < a.cout;
-      const float bias = cv ? e.bias[col] : 0.f;
-      const float sc = (cv && e.scale) ? e.scale[col] : 1.f;
-      const float sh = (cv && e.scale) ? e.shift[col] : 0.f;
+      const float bias = hb[tn], sc = hs[tn], sh = hh[tn];
 #pragma unroll
       for (int tm = 0; tm < FM; ++tm)
 #pragma unroll
@@ -351,20 +376,6 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     return;
   }
   // ---- epilogue: accumulators -> LDS C tile (fp32) -> 4 rows x 8 channels per thread ----
-  // lean epilogue: this thread's 8 channels are the same in both of its units
-  // (NT % CG == 0), so bias/scale/shift are loaded once, before the C-tile pass
-  constexpr int CG = BN / 8;
-  float lb[8], ls[8], lh[8];
-  if constexpr ((ABL & 128) != 0) {
-    const int c0 = n_base + (tid % CG) * 8;
-    const bool cv = c0 < a.cout;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      lb[j] = cv ? a.e.bias[c0 + j] : 0.f;
-      ls[j] = cv && a.e.scale ? a.e.scale[c0 + j] : 1.f;
-      lh[j] = cv && a.e.scale ? a.e.shift[c0 + j] : 0.f;
-    }
-  }
   float* Cs = reinterpret_cast<float*>(smem_raw);
   const int rq = g * 4;
 #pragma unroll
