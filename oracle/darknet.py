@@ -4,7 +4,11 @@ Restates yolov3/utils/parse_config.py:6-52 (cfg parse), models.py:9-123
 (create_modules: conv(bias=!bn) + BN(eps 1e-4) + LeakyReLU(0.1)/Swish; maxpool
 with ZeroPad2d for size 2 / stride 1; nearest upsample; route concat; shortcut
 add), models.py:449-486 (weight stream order), models.py:332-395 (forward) and
-models.py:204-258 + 422-436 (YOLOLayer inference decode, create_grids).
+models.py:204-258 + 422-436 (YOLOLayer inference decode, create_grids), and the
+[acff] block (models.py:46-55 -> ACFF.forward :296-315: three dilated depthwise 3x3
+branches d1p0 / d2p1 / d3p2 with bias, ADDED, then 1x1 conv + bias, LeakyReLU(0.01),
+BatchNorm2d(eps 1e-5, eval), Dropout(eval) -- its parameters come from a state dict, not
+the .weights stream).
 """
 from __future__ import annotations
 
@@ -39,7 +43,8 @@ def parse_cfg(text: str):
 
 
 class DarknetRef:
-    def __init__(self, cfg_text: str, stream: np.ndarray):
+    def __init__(self, cfg_text: str, stream: np.ndarray, acff: dict | None = None):
+        """acff: {layer index: {ACFF state-dict key (conv1.weight, ...): array}}."""
         self.mdefs = parse_cfg(cfg_text)
         self.net = self.mdefs.pop(0)
         self.params = {}
@@ -62,6 +67,10 @@ class DarknetRef:
                 p["w"] = torch.from_numpy(stream[ptr:ptr + nw].copy()).view(f, cin[-1], k, k)
                 ptr += nw
                 self.params[i] = p
+            elif t == "acff":
+                f = int(m["filters"])
+                assert acff is not None and i in acff, f"[acff] layer {i} needs its parameters"
+                self.params[i] = {k: torch.from_numpy(np.asarray(v, np.float32).copy()) for k, v in acff[i].items()}
             elif t == "route":
                 f = sum(cin[l + 1 if l > 0 else l] for l in m["layers"])
                 self.routs.update(i + l if l < 0 else l for l in m["layers"])
@@ -94,6 +103,15 @@ class DarknetRef:
                     x = F.leaky_relu(x, 0.1)
                 elif m["activation"] == "swish":
                     x = x * torch.sigmoid(x)
+            elif t == "acff":
+                p = self.params[i]
+                c = x.shape[1]
+                y = (F.conv2d(x, p["conv1.weight"], p["conv1.bias"], 1, 0, 1, c)
+                     + F.conv2d(x, p["conv2.weight"], p["conv2.bias"], 1, 1, 2, c)
+                     + F.conv2d(x, p["conv3.weight"], p["conv3.bias"], 1, 2, 3, c))
+                y = F.leaky_relu(F.conv2d(y, p["fused_conv.weight"], p["fused_conv.bias"]), 0.01)
+                x = F.batch_norm(y, p["batch_norm.running_mean"], p["batch_norm.running_var"],
+                                 p["batch_norm.weight"], p["batch_norm.bias"], False, 0.1, 1e-5)
             elif t == "maxpool":
                 k, s = int(m["size"]), int(m["stride"])
                 if k == 2 and s == 1:
@@ -104,9 +122,28 @@ class DarknetRef:
                 x = F.interpolate(x, scale_factor=int(m["stride"]), mode="nearest")
             elif t == "route":
                 ls = m["layers"]
-                x = out[ls[0]] if len(ls) == 1 else torch.cat([out[l] for l in ls], 1)
+                if len(ls) == 1:
+                    x = out[ls[0]]
+                else:
+                    ws = [out[l].shape[-1] for l in ls]
+                    if len(ls) == 2 and ws[0] != ws[1]:
+                        # models.py:364-375: on a size mismatch the narrower of the two maps
+                        # is nearest-resized to the wider one's width, in place in `out`
+                        big = 0 if (ws[0], 0) > (ws[1], 1) else 1
+                        small = ls[1 - big]
+                        out[small] = F.interpolate(out[small], size=max(ws))
+                    x = torch.cat([out[l] for l in ls], 1)
             elif t == "shortcut":
-                x = x + out[m["from"][0]]
+                # weightedFeatureFusion.forward (models.py:135-155), unweighted
+                a = out[m["from"][0]]
+                nc, ac = x.shape[1], a.shape[1]
+                if nc > ac:
+                    x = x.clone()
+                    x[:, :ac] = x[:, :ac] + a
+                elif nc < ac:
+                    x = x + a[:, :nc]
+                else:
+                    x = x + a
             elif t == "yolo":
                 self.heads.append({"na": len(m["mask"]), "ny": x.shape[2], "nx": x.shape[3],
                                    "anchors": [tuple(m["anchors"][a]) for a in m["mask"]],

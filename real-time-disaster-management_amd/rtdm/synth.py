@@ -98,10 +98,64 @@ def conv_layers(cfg_text: str):
             f = sum(filters_out[l + 1 if l > 0 else l] for l in m["layers"])
         elif t in ("shortcut", "maxpool", "upsample", "yolo"):
             f = filters_out[-1]
+        elif t == "acff":
+            f = int(m["filters"])
         else:
             raise ValueError(f"unsupported layer type {t}")
         filters_out.append(f)
     return convs
+
+
+def acff_layers(cfg_text: str):
+    """[(layer_idx, cin, cout)] of the [acff] blocks (models.py:46-55 -> ACFF :265-315)."""
+    mdefs = parse_cfg_text(cfg_text)
+    net = mdefs.pop(0)
+    filters_out = [int(net.get("channels", 3))]
+    out = []
+    for i, m in enumerate(mdefs):
+        t = m["type"]
+        if t in ("convolutional", "acff"):
+            f = int(m["filters"])
+            if t == "acff":
+                out.append((i, filters_out[-1], f))
+        elif t == "route":
+            f = sum(filters_out[l + 1 if l > 0 else l] for l in m["layers"])
+        else:
+            f = filters_out[-1]
+        filters_out.append(f)
+    return out
+
+
+ACFF_KEYS = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "conv3.weight", "conv3.bias",
+             "fused_conv.weight", "fused_conv.bias", "batch_norm.weight", "batch_norm.bias",
+             "batch_norm.running_mean", "batch_norm.running_var")
+
+
+def synth_acff_params(cfg_text: str, seed: int = 9, calib: dict | None = None) -> dict:
+    """{layer: {ACFF state-dict key: array}} for a Darknet cfg's [acff] blocks.  These are
+    not in a .weights stream (load_darknet_weights, models.py:457-486, loads only
+    [convolutional]); the reference gets them from a .pt state dict.  Depthwise branches
+    He-scaled over their 9 taps and down-weighted by 1/sqrt(3) (three are summed), the 1x1
+    He-scaled, BN gamma 1 / beta 0 with running stats from `calib` (acffmean<i>/acffvar<i>)."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    for (i, c, f) in acff_layers(cfg_text):
+        p = {}
+        for b in (1, 2, 3):
+            p[f"conv{b}.weight"] = (rng.standard_normal((c, 1, 3, 3), dtype=np.float32)
+                                    * np.float32(np.sqrt(2.0 / 9.0 / 3.0)))
+            p[f"conv{b}.bias"] = (rng.standard_normal(c, dtype=np.float32) * np.float32(0.05))
+        p["fused_conv.weight"] = rng.standard_normal((f, c, 1, 1), dtype=np.float32) * np.float32(np.sqrt(2.0 / c))
+        p["fused_conv.bias"] = rng.standard_normal(f, dtype=np.float32) * np.float32(0.05)
+        p["batch_norm.weight"] = np.ones(f, np.float32)
+        p["batch_norm.bias"] = np.zeros(f, np.float32)
+        if calib is not None and f"acffobj{i}" in calib:  # head ACFF: objectness shift
+            p["batch_norm.bias"] = calib[f"acffobj{i}"].astype(np.float32)
+        has = calib is not None and f"acffmean{i}" in calib
+        p["batch_norm.running_mean"] = calib[f"acffmean{i}"].astype(np.float32) if has else np.zeros(f, np.float32)
+        p["batch_norm.running_var"] = calib[f"acffvar{i}"].astype(np.float32) if has else np.ones(f, np.float32)
+        out[i] = p
+    return out
 
 
 def cfg_name(cfg_path_or_name: str) -> str:

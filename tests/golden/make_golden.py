@@ -54,6 +54,7 @@ DET_CASES = [  # (cfg, size, n_frames, full_io)
     ("yolov3-tiny-aider-416", 416, 1, False),
     ("yolov4-tiny-swish", 416, 1, False),
     ("yolov4-tiny-3l-512x512", 512, 1, False),
+    ("yolov3-acffx", 416, 1, False),
 ]
 NMS_SETTINGS = [(0.3, 0.4), (0.01, 0.6)]
 IO_STRIDE = 53
@@ -128,6 +129,11 @@ def det_goldens():
         with tempfile.NamedTemporaryFile(suffix=".weights") as f:
             synth.write_darknet_weights(f.name, stream)
             models.load_darknet_weights(model, f.name)
+        acff = synth.synth_acff_params(text, calib=synth.load_calibration(cfg))
+        for i, p in acff.items():  # [acff] blocks: state-dict parameters (not in .weights)
+            sd = {k: torch.from_numpy(v) for k, v in p.items()}
+            sd["batch_norm.num_batches_tracked"] = torch.tensor(0)
+            model.module_list[i][0].load_state_dict(sd)
         model.eval()
         frames = synth.synth_frames(nf, size, size, seed=synth.BASE_SEED + 700)
         x = torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0

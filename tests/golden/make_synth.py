@@ -25,7 +25,7 @@ from rtdm import synth  # noqa: E402
 from refimport import DET_DIR, import_darknet  # noqa: E402
 
 CFGS = ["yolov4-tiny-aider-416", "yolov3-aider-416", "yolov3-spp-aider", "yolov3-tiny-aider-416",
-        "yolov4-tiny-swish", "yolov4-tiny-3l-512x512"]
+        "yolov4-tiny-swish", "yolov4-tiny-3l-512x512", "yolov3-acffx"]
 
 
 def calibrate(name: str, size: int = 416):
@@ -37,10 +37,41 @@ def calibrate(name: str, size: int = 416):
     with tempfile.NamedTemporaryFile(suffix=".weights") as f:
         synth.write_darknet_weights(f.name, stream)
         models.load_darknet_weights(model, f.name)
+    acff = synth.synth_acff_params(text)  # ACFF blocks (yolov3-acffx.cfg): not in .weights
+    for i, p in acff.items():
+        mod = model.module_list[i][0]
+        sd = {k: torch.from_numpy(v) for k, v in p.items()}
+        sd["batch_norm.num_batches_tracked"] = torch.tensor(0)
+        mod.load_state_dict(sd)
     model.eval()
     calib = {}
     heads = {}
     mdefs = model.module_defs
+    logit03 = float(np.log(0.3 / 0.7))
+    for i in acff:
+        mod = model.module_list[i][0]
+
+        def bn_pre(m, inp, i=i):
+            x = inp[0].detach().double()
+            mean = x.mean(dim=(0, 2, 3))
+            var = x.var(dim=(0, 2, 3), unbiased=False) + 1e-6
+            m.running_mean.copy_(mean.float())
+            m.running_var.copy_(var.float())
+            calib[f"acffmean{i}"] = mean.float().numpy()
+            calib[f"acffvar{i}"] = var.float().numpy()
+        mod.batch_norm.register_forward_pre_hook(bn_pre)
+        if i + 1 < len(mdefs) and mdefs[i + 1]["type"] == "yolo":
+            def ahook(m, inp, out, i=i):
+                no = int(mdefs[i + 1]["classes"]) + 5
+                na = out.shape[1] // no
+                obj = out.detach().view(out.shape[0], na, no, *out.shape[2:])[:, :, 4]
+                q = float(np.quantile(obj.numpy().reshape(-1), 0.98))
+                shift = np.zeros(out.shape[1], np.float32)
+                shift[[a * no + 4 for a in range(na)]] = logit03 - q
+                calib[f"acffobj{i}"] = shift
+                m.batch_norm.bias.add_(torch.from_numpy(shift))
+                out += torch.from_numpy(shift).view(1, -1, 1, 1)
+            mod.register_forward_hook(ahook)
     for i, (mdef, mod) in enumerate(zip(mdefs, model.module_list)):
         if mdef["type"] != "convolutional":
             continue
@@ -65,7 +96,6 @@ def calibrate(name: str, size: int = 416):
     x = torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0
     with torch.no_grad():
         model(x)
-    logit03 = float(np.log(0.3 / 0.7))
     for i, p in heads.items():
         no = int(mdefs[i + 1]["classes"]) + 5
         na = p.shape[1] // no

@@ -49,8 +49,9 @@ def test_darknet_oracle_matches_reference_goldens(det_golden):
     from oracle.darknet import DarknetRef
     from rtdm.synth import BASE_SEED, load_calibration, synth_darknet_weights, synth_frames
     import hashlib
+    from rtdm.synth import synth_acff_params
     for case in ("yolov4-tiny-aider-416@256", "yolov4-tiny-aider-416@608", "yolov3-tiny-aider-416@416",
-                 "yolov4-tiny-swish@416", "yolov4-tiny-3l-512x512@512"):
+                 "yolov4-tiny-swish@416", "yolov4-tiny-3l-512x512@512", "yolov3-acffx@416"):
         cfg, size = case.split("@")
         size = int(size)
         text = cfg_text(cfg)
@@ -59,7 +60,9 @@ def test_darknet_oracle_matches_reference_goldens(det_golden):
         n = int(det_golden[f"{case}/io_shape"][0])
         frames = synth_frames(n, size, size, seed=BASE_SEED + 700)
         assert hashlib.sha256(frames.tobytes()).hexdigest() == str(det_golden[f"{case}/frames_sha"])
-        io = DarknetRef(text, stream).forward(torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0).numpy()
+        acff = synth_acff_params(text, calib=load_calibration(cfg))  # YOLO-ACFF blocks, if any
+        io = DarknetRef(text, stream, acff).forward(
+            torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0).numpy()
         assert np.array_equal(io[:, ::53], det_golden[f"{case}/io_rows"]), case
         if f"{case}/io" in det_golden:
             assert np.array_equal(io, det_golden[f"{case}/io"])
