@@ -85,7 +85,12 @@ static std::vector<CfgBlock> parse_cfg(const std::string& text) {
   return defs;
 }
 
-enum StepKind { ST_CONV = 0, ST_MAXPOOL = 1, ST_UPSAMPLE = 2, ST_COPY = 3 };
+// ST_DW3: an [acff] block's three dilated depthwise branches into a [3C] scratch map
+// (its 1x1 fusion is the ST_CONV after it); ST_RESIZE: the route's nearest resize of the
+// narrower of two maps (models.py:364-375)
+// ST_ADD: a [shortcut] that cannot ride the previous conv's epilogue (that conv's pre-add
+// output is also routed elsewhere): out = in + res
+enum StepKind { ST_CONV = 0, ST_MAXPOOL = 1, ST_UPSAMPLE = 2, ST_COPY = 3, ST_DW3 = 4, ST_RESIZE = 5, ST_ADD = 6 };
 
 struct Tensor {
   int c = 0, h = 0, w = 0;
@@ -108,6 +113,15 @@ struct Step {
   int full_t = -1, pool_t = -1, up_t = -1, res_t = -1;
   int yolo = -1;  // index into yolo heads
   bool quad = false;
+  float slope = 0.1f;  // LeakyReLU slope: 0.1 Darknet conv (models.py:40), 0.01 ACFF (:291)
+  // [acff] (models.py:46-55, ACFF :265-315): this ST_CONV is the 1x1 fusion over the
+  // ST_DW3 map [b1|b2|b3] with the weights repeated 3x along K (= W (b1+b2+b3)); BN is
+  // the post-activation affine a_bn = [gamma | beta | mean | var], eps 1e-5
+  bool acff = false;
+  std::vector<float> a_W;
+  const float* a_bn = nullptr;
+  const float* a_dw = nullptr;  // ST_DW3: [w1 C*9 | b1 C | w2 | b2 | w3 | b3]
+  size_t dw_w_off = SIZE_MAX, dw_b_off = SIZE_MAX;
   // fused 1x1 head conv (layer + 1) feeding a [yolo] (layer + 2): conv_pipe_f16 head
   // epilogue; this conv's own output is not materialised
   bool head = false;
@@ -202,7 +216,7 @@ void set_fuse_head(int v) { g_fuse_head = v ? 1 : 0; }
 static size_t esize_of(int dtype) { return dtype == RTDM_F16 ? 2 : 4; }
 
 static bool implicit_input(const std::string& t) {
-  return t == "convolutional" || t == "maxpool" || t == "upsample" || t == "shortcut" || t == "yolo";
+  return t == "convolutional" || t == "acff" || t == "maxpool" || t == "upsample" || t == "shortcut" || t == "yolo";
 }
 
 static int resolve_ref(int layer, int l) { return l < 0 ? layer + l : l; }
@@ -263,20 +277,47 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       out_w[i] = cur_w;
       continue;
     }
-    if (t == "convolutional") {
-      const int bn = d.i("batch_normalize", 0);
+    if (t == "convolutional" || t == "acff") {
+      const bool is_acff = t == "acff";
+      const int bn = is_acff ? 0 : d.i("batch_normalize", 0);
       const int filters = d.i("filters", 0);
-      const int size = d.i("size", 1);
-      RTDM_REQUIRE(d.has("stride"), RTDM_E_UNSUPPORTED, "cfg: conv without stride (stride_x/stride_y) unsupported");
-      const int stride = d.i("stride", 1);
-      const int pad = d.i("pad", 0) ? (size - 1) / 2 : 0;
+      const int size = is_acff ? 1 : d.i("size", 1);
+      RTDM_REQUIRE(is_acff || d.has("stride"), RTDM_E_UNSUPPORTED, "cfg: conv without stride (stride_x/stride_y) unsupported");
+      const int stride = is_acff ? 1 : d.i("stride", 1);
+      const int pad = is_acff ? 0 : d.i("pad", 0) ? (size - 1) / 2 : 0;
       RTDM_REQUIRE(d.i("groups", 1) == 1, RTDM_E_UNSUPPORTED, "cfg: grouped conv unsupported");
-      const std::string actn = d.str("activation", "linear");
+      const std::string actn = is_acff ? "leaky" : d.str("activation", "linear");
       int act = ACT_LINEAR;
       if (actn == "leaky")
         act = ACT_LEAKY;
       else if (actn == "swish")
         act = ACT_SWISH;
+      const int acff_c = cur_c;
+      if (is_acff) {
+        // three dilated depthwise branches d1p0 / d2p1 / d3p2, each [C, H-2, W-2] (+bias),
+        // written side by side as one [3C] map for the 1x1 fusion conv below
+        RTDM_REQUIRE(d.i("size", 3) == 3, RTDM_E_UNSUPPORTED, "cfg: acff size must be 3");
+        RTDM_REQUIRE(cur_h > 2 && cur_w > 2 && cur_t >= 0, RTDM_E_UNSUPPORTED, "cfg: acff input too small");
+        Step dw;
+        dw.kind = ST_DW3;
+        dw.layer = i;
+        dw.in_t = cur_t;
+        dw.cin = cur_c;
+        dw.ih = cur_h;
+        dw.iw = cur_w;
+        dw.oh = cur_h - 2;
+        dw.ow = cur_w - 2;
+        dw.a_dw = take_w(3 * ((int64_t)cur_c * 9 + cur_c));
+        h.tensors[cur_t].materialised = true;
+        dw.out_t = new_tensor(3 * cur_c, dw.oh, dw.ow, "acffdw" + std::to_string(i));
+        h.tensors[dw.out_t].materialised = true;
+        h.flop += 2.0 * dw.oh * dw.ow * 3.0 * cur_c * 9;
+        h.steps.push_back(dw);
+        cur_t = dw.out_t;
+        cur_c = 3 * cur_c;
+        cur_h -= 2;
+        cur_w -= 2;
+      }
       // create_modules adds no module for any other activation (models.py:40-44): identity
       Step s;
       s.kind = ST_CONV;
@@ -293,7 +334,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       s.oh = (cur_h + 2 * pad - size) / stride + 1;
       s.ow = (cur_w + 2 * pad - size) / stride + 1;
       RTDM_REQUIRE(s.oh > 0 && s.ow > 0, RTDM_E_UNSUPPORTED, "cfg: conv output empty at layer " + std::to_string(i));
-      h.flop += 2.0 * s.oh * s.ow * (double)filters * cur_c * size * size;
+      h.flop += 2.0 * s.oh * s.ow * (double)filters * (is_acff ? acff_c : cur_c) * size * size;
       // weights: [bn: beta gamma mean var | bias] then W
       const float *beta = nullptr, *gamma = nullptr, *mean = nullptr, *var = nullptr, *bias = nullptr;
       if (bn) {
@@ -301,10 +342,25 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         gamma = take_w(filters);
         mean = take_w(filters);
         var = take_w(filters);
-      } else {
+      } else if (!is_acff) {
         bias = take_w(filters);
       }
-      const float* W = take_w((int64_t)filters * cur_c * size * size);
+      const float* W = nullptr;
+      if (is_acff) {  // fused_conv weight [F][C], bias [F], then BN gamma/beta/mean/var
+        const float* w1 = take_w((int64_t)filters * acff_c);
+        bias = take_w(filters);
+        s.a_bn = take_w(4 * (int64_t)filters);
+        if (w1) {
+          s.a_W.resize((size_t)filters * cur_c);
+          for (int o = 0; o < filters; ++o)
+            for (int r = 0; r < 3; ++r)
+              for (int c = 0; c < acff_c; ++c) s.a_W[((size_t)o * 3 + r) * acff_c + c] = w1[(size_t)o * acff_c + c];
+        }
+        s.acff = true;
+        s.slope = 0.01f;
+      } else {
+        W = take_w((int64_t)filters * cur_c * size * size);
+      }
       s.bn = bn != 0;
       s.w_beta = beta;
       s.w_gamma = gamma;
@@ -357,7 +413,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
           h.layer_tensor[i] = -1;        // the pre-add conv output is never materialised
           h.layer_tensor[i + 1] = full;  // conv output with the residual added
           need_full = !consumers[i + 1].empty();
-        } else if (f16 && fuse_head() && !h.int8 && nx.type == "convolutional" && only_next && i + 2 < L && defs[i + 2].type == "yolo" &&
+        } else if (f16 && fuse_head() && !h.int8 && !is_acff && nx.type == "convolutional" && only_next && i + 2 < L && defs[i + 2].type == "yolo" &&
                    consumers[i + 1].size() == 1 && consumers[i + 1][0] == i + 2 && consumers[i + 2].empty() &&
                    nx.i("size", 1) == 1 && nx.i("stride", 1) == 1 && nx.i("groups", 1) == 1 &&
                    nx.i("filters", 0) <= 32 && filters > 64 && filters <= 128 &&
@@ -529,6 +585,31 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         cur_h = h.tensors[tt].h;
         cur_w = h.tensors[tt].w;
       } else {
+        if (ls.size() == 2) {
+          // models.py:364-375: maps of different widths -> the narrower one is nearest-resized
+          // to size (W, W) of the wider one, replacing that layer's stored output
+          const int s0 = resolve_ref(i, ls[0]), s1 = resolve_ref(i, ls[1]);
+          const int t0 = h.layer_tensor[s0], t1 = h.layer_tensor[s1];
+          RTDM_REQUIRE(t0 >= 0 && t1 >= 0, RTDM_E_UNSUPPORTED, "cfg: route to a layer without output");
+          const int w0 = h.tensors[t0].w, w1 = h.tensors[t1].w;
+          if (w0 != w1) {
+            const bool big0 = w0 > w1;  // max((w, num)): ties cannot happen here
+            const int src = big0 ? s1 : s0, st_ = big0 ? t1 : t0, sz = big0 ? w0 : w1;
+            Step rz;
+            rz.kind = ST_RESIZE;
+            rz.layer = i;
+            rz.in_t = st_;
+            rz.cin = h.tensors[st_].c;
+            rz.ih = h.tensors[st_].h;
+            rz.iw = h.tensors[st_].w;
+            rz.oh = sz;
+            rz.ow = sz;
+            h.tensors[st_].materialised = true;
+            rz.out_t = new_tensor(rz.cin, sz, sz, "resize" + std::to_string(src));
+            h.layer_tensor[src] = rz.out_t;
+            h.steps.push_back(rz);
+          }
+        }
         int csum = 0, hh = -1, ww = -1;
         for (int l : ls) {
           const int tt = h.layer_tensor[resolve_ref(i, l)];
@@ -574,7 +655,27 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         cur_w = ww;
       }
     } else if (t == "shortcut") {
-      throw Error{RTDM_E_UNSUPPORTED, "cfg: shortcut not preceded by a fusable conv (layer " + std::to_string(i) + ")"};
+      // unfused weightedFeatureFusion (models.py:135-155), unweighted, same shapes
+      RTDM_REQUIRE(!d.has("weights_type") && d.ints("from").size() == 1 && cur_t >= 0, RTDM_E_UNSUPPORTED,
+                   "cfg: unsupported shortcut at layer " + std::to_string(i));
+      const int rt = h.layer_tensor[resolve_ref(i, d.ints("from")[0])];
+      RTDM_REQUIRE(rt >= 0 && h.tensors[rt].c == cur_c && h.tensors[rt].h == cur_h && h.tensors[rt].w == cur_w,
+                   RTDM_E_UNSUPPORTED, "cfg: shortcut with channel/shape mismatch unsupported (layer " + std::to_string(i) + ")");
+      Step ad;
+      ad.kind = ST_ADD;
+      ad.layer = i;
+      ad.in_t = cur_t;
+      ad.res_t = rt;
+      ad.cin = cur_c;
+      ad.ih = ad.oh = cur_h;
+      ad.iw = ad.ow = cur_w;
+      h.tensors[cur_t].materialised = true;
+      h.tensors[rt].materialised = true;
+      ad.out_t = new_tensor(cur_c, cur_h, cur_w, "add" + std::to_string(i));
+      h.tensors[ad.out_t].materialised = true;
+      h.layer_tensor[i] = ad.out_t;
+      cur_t = ad.out_t;
+      h.steps.push_back(ad);
     } else if (t == "yolo") {
       throw Error{RTDM_E_UNSUPPORTED, "cfg: yolo not preceded by a fusable head conv (layer " + std::to_string(i) + ")"};
     } else {
@@ -604,6 +705,18 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
   h.per_image = off;
   // ---- pack conv weights: MFMA layout iff the input view is 16-byte aligned NHWC ----
   for (Step& st : h.steps) {
+    if (st.kind == ST_DW3 && weights) {  // [3][C][9] taps, [3][C] biases (launch_dw3_acff)
+      const int c = st.cin;
+      std::vector<float> w((size_t)3 * c * 9), b((size_t)3 * c);
+      for (int r = 0; r < 3; ++r) {
+        const float* src = st.a_dw + (size_t)r * (c * 9 + c);
+        std::copy(src, src + (size_t)c * 9, w.begin() + (size_t)r * c * 9);
+        std::copy(src + (size_t)c * 9, src + (size_t)c * 10, b.begin() + (size_t)r * c);
+      }
+      st.dw_w_off = blob.add_f32(w);
+      st.dw_b_off = blob.add_f32(b);
+      st.a_dw = nullptr;
+    }
     if (st.kind != ST_CONV) continue;
     bool use_mfma = f16 && st.in_t >= 0 && st.cin % 8 == 0;
     if (use_mfma) {
@@ -625,8 +738,24 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
           b[o] = st.w_bias[o];
         }
       }
-      st.pc = pack_conv(blob, st.w_W, filters, st.cin, size, st.bn ? sc.data() : nullptr, use_mfma);
+      st.pc = pack_conv(blob, st.acff ? st.a_W.data() : st.w_W, filters, st.cin, size, st.bn ? sc.data() : nullptr,
+                        use_mfma);
       st.pc.b_off = blob.add_f32(b);
+      if (st.acff) {  // BatchNorm2d after the LeakyReLU (acff.py order), eps 1e-5
+        std::vector<float> as(filters), at(filters);
+        for (int o = 0; o < filters; ++o) {
+          const double g = st.a_bn[o], be = st.a_bn[filters + o], mu = st.a_bn[2 * filters + o],
+                       var = st.a_bn[3 * filters + o];
+          const double k = g / std::sqrt(var + 1e-5);
+          as[o] = (float)k;
+          at[o] = (float)(be - mu * k);
+        }
+        st.pc.s_off = blob.add_f32(as);
+        st.pc.t_off = blob.add_f32(at);
+        st.a_W.clear();
+        st.a_W.shrink_to_fit();
+        st.a_bn = nullptr;
+      }
       if (st.head) {
         std::vector<double> hsc(st.head_cout, 1.0);
         std::vector<float> hb(st.head_cout);
@@ -644,7 +773,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         RTDM_REQUIRE(st.hpc.kpad == 128 && st.hpc.cout_pad == 32, RTDM_E_INVALID, "internal: head packing");
       }
       if (stem) st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr);
-      if (h.int8 && use_mfma && !st.head && st.yolo < 0 && st.cin % 64 == 0 && (size == 1 || size == 3) &&
+      if (h.int8 && use_mfma && !st.head && !st.acff && st.yolo < 0 && st.cin % 64 == 0 && (size == 1 || size == 3) &&
           st.pc.cout_pad % 128 == 0) {
         // symmetric per-output-channel int8 of the BN-folded weights, [cout_pad][kpad]
         const int kp = st.pc.kpad, cp = st.pc.cout_pad;
@@ -779,7 +908,11 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       a.cout_pad = st.pc.cout_pad;
       a.e.bias = h.blob.at<float>(st.pc.b_off);
       a.e.act = st.act;
-      a.e.slope = 0.1f;
+      a.e.slope = st.slope;
+      if (st.pc.s_off != SIZE_MAX) {
+        a.e.scale = h.blob.at<float>(st.pc.s_off);
+        a.e.shift = h.blob.at<float>(st.pc.t_off);
+      }
       a.e.full = tensor_view(h, st.full_t);
       a.e.pool = tensor_view(h, st.pool_t);
       a.e.up = tensor_view(h, st.up_t);
@@ -838,6 +971,17 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       View o = tensor_view(h, st.out_t);
       o.co += st.k;
       launch_copy_slice(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, o, h.dtype, s);
+    } else if (st.kind == ST_DW3) {
+      const View iv = tensor_view(h, st.in_t), ov = tensor_view(h, st.out_t);
+      RTDM_REQUIRE(ov.cs == 3 * st.cin && ov.co == 0, RTDM_E_INVALID, "internal: acff branch map view");
+      launch_dw3_acff(iv.ptr, iv.cs, iv.co, n, st.ih, st.iw, st.cin, st.oh, st.ow, h.blob.at<float>(st.dw_w_off),
+                      h.blob.at<float>(st.dw_b_off), ov.ptr, h.dtype, s);
+    } else if (st.kind == ST_ADD) {
+      launch_add(tensor_view(h, st.in_t), tensor_view(h, st.res_t), n, st.ih, st.iw, st.cin, tensor_view(h, st.out_t),
+                 h.dtype, s);
+    } else if (st.kind == ST_RESIZE) {
+      launch_resize_nearest(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, tensor_view(h, st.out_t), st.oh, st.ow,
+                            h.dtype, s);
     }
     if (ev) RTDM_HIP(hipEventRecord(ev[2 * si + 1], s));
     if (two && st.signal) RTDM_HIP(hipEventRecord(h.step_ev[si], s));
@@ -909,6 +1053,18 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     name = "maxpool_kernel";
     flop = 0;
     bytes = ((double)st.ih * st.iw + (double)st.oh * st.ow) * st.cin * es;
+  } else if (st.kind == ST_DW3) {
+    name = "dw3_acff_kernel";
+    flop = 2.0 * st.oh * st.ow * 3.0 * st.cin * 9;
+    bytes = ((double)st.ih * st.iw + 3.0 * st.oh * st.ow) * st.cin * es;
+  } else if (st.kind == ST_ADD) {
+    name = "add_kernel";
+    flop = 0;
+    bytes = 3.0 * st.ih * st.iw * st.cin * es;
+  } else if (st.kind == ST_RESIZE) {
+    name = "resize_nearest_kernel";
+    flop = 0;
+    bytes = ((double)st.ih * st.iw + (double)st.oh * st.ow) * st.cin * es;
   } else {
     name = "upsample_kernel";
     flop = 0;
@@ -941,6 +1097,7 @@ static void schedule_streams(rtdm_detector_s& h) {
       if (t >= 0 && h.tensors[t].materialised) writes[i].push_back(buf_of(t));
     };
     rd(st.in_t);
+    if (st.kind == ST_ADD) rd(st.res_t);
     if (st.kind == ST_CONV) {
       rd(st.res_t);
       wr(st.full_t);
@@ -1029,6 +1186,12 @@ static std::string describe(const rtdm_detector_s& h) {
         << tn(st.out_t);
     } else if (st.kind == ST_UPSAMPLE) {
       o << "upsample x" << st.f << " " << tn(st.in_t) << " -> " << tn(st.out_t);
+    } else if (st.kind == ST_DW3) {
+      o << "acff dw3x3 d1/d2/d3 " << tn(st.in_t) << " -> " << tn(st.out_t);
+    } else if (st.kind == ST_ADD) {
+      o << "shortcut add " << tn(st.in_t) << " + " << tn(st.res_t) << " -> " << tn(st.out_t);
+    } else if (st.kind == ST_RESIZE) {
+      o << "resize nearest " << tn(st.in_t) << " -> " << tn(st.out_t);
     } else {
       o << "copy " << tn(st.in_t) << " -> " << tn(st.out_t) << "+" << st.k;
     }

@@ -279,6 +279,68 @@ void launch_upsample(View iv, int n, int h, int w, int c, int f, View ov, int dt
   RTDM_HIP(hipGetLastError());
 }
 
+// Unfused [shortcut] (weightedFeatureFusion.forward, models.py:135-155, same shapes).
+template <typename T>
+__global__ __launch_bounds__(256) void add_kernel(const T* __restrict__ a, int a_cs, int a_co, const T* __restrict__ b,
+                                                  int b_cs, int b_co, int64_t pix, int c, T* __restrict__ out,
+                                                  int o_cs, int o_co) {
+  const int64_t total = pix * c;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(idx % c);
+    const int64_t p = idx / c;
+    out[p * o_cs + o_co + ch] = (T)((float)a[p * a_cs + a_co + ch] + (float)b[p * b_cs + b_co + ch]);
+  }
+}
+
+void launch_add(View a, View b, int n, int h, int w, int c, View ov, int dtype, hipStream_t s) {
+  const int64_t pix = (int64_t)n * h * w;
+  if (pix * c <= 0) return;
+  const int g = grid_for(pix * c, 256);
+  if (dtype == RTDM_F16)
+    hipLaunchKernelGGL(add_kernel<_Float16>, dim3(g), dim3(256), 0, s, (const _Float16*)a.ptr, a.cs, a.co,
+                       (const _Float16*)b.ptr, b.cs, b.co, pix, c, (_Float16*)ov.ptr, ov.cs, ov.co);
+  else
+    hipLaunchKernelGGL(add_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)a.ptr, a.cs, a.co,
+                       (const float*)b.ptr, b.cs, b.co, pix, c, (float*)ov.ptr, ov.cs, ov.co);
+  RTDM_HIP(hipGetLastError());
+}
+
+// Route resize of YOLO-ACFF (models.py:364-375 -> F.interpolate nearest, given size):
+// PyTorch's nearest source index, scale = in / out in fp32.
+template <typename T>
+__global__ __launch_bounds__(256) void resize_nearest_kernel(const T* __restrict__ in, int in_cs, int in_co, int n,
+                                                             int h, int w, int c, T* __restrict__ out, int out_cs,
+                                                             int out_co, int oh, int ow) {
+  const float sy = (float)h / (float)oh, sx = (float)w / (float)ow;
+  const int64_t total = (int64_t)n * oh * ow * c;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(idx % c);
+    int64_t p = idx / c;
+    const int ox = (int)(p % ow);
+    p /= ow;
+    const int oy = (int)(p % oh);
+    const int b = (int)(p / oh);
+    const int iy = min((int)floorf((float)oy * sy), h - 1), ix = min((int)floorf((float)ox * sx), w - 1);
+    out[(((size_t)b * oh + oy) * ow + ox) * out_cs + out_co + ch] =
+        in[(((size_t)b * h + iy) * w + ix) * in_cs + in_co + ch];
+  }
+}
+
+void launch_resize_nearest(View iv, int n, int h, int w, int c, View ov, int oh, int ow, int dtype, hipStream_t s) {
+  const int64_t total = (int64_t)n * oh * ow * c;
+  if (total <= 0) return;
+  const int g = grid_for(total, 256);
+  if (dtype == RTDM_F16)
+    hipLaunchKernelGGL(resize_nearest_kernel<_Float16>, dim3(g), dim3(256), 0, s, (const _Float16*)iv.ptr, iv.cs,
+                       iv.co, n, h, w, c, (_Float16*)ov.ptr, ov.cs, ov.co, oh, ow);
+  else
+    hipLaunchKernelGGL(resize_nearest_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)iv.ptr, iv.cs, iv.co, n,
+                       h, w, c, (float*)ov.ptr, ov.cs, ov.co, oh, ow);
+  RTDM_HIP(hipGetLastError());
+}
+
 void launch_copy_slice(View iv, int n, int h, int w, int c, View ov, int dtype, hipStream_t s) {
   launch_upsample(iv, n, h, w, c, 1, ov, dtype, s);
 }

@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
-from .synth import conv_layers, read_darknet_weights
+from .synth import ACFF_KEYS, acff_layers, conv_layers, read_darknet_weights
 
 
 def read_cfg(cfg: str) -> str:
@@ -39,14 +39,19 @@ def state_dict_to_stream(cfg_text: str, sd: dict) -> np.ndarray:
             v = v.detach().cpu().float().numpy()
         return np.asarray(v, np.float32).reshape(-1)
 
-    for (i, cin, cout, k, bn, head) in conv_layers(cfg_text):
+    convs = {i: bn for (i, cin, cout, k, bn, head) in conv_layers(cfg_text)}
+    acffs = {i for (i, c, f) in acff_layers(cfg_text)}
+    for i in sorted(set(convs) | acffs):
         p = f"module_list.{i}."
-        if bn:
+        if i in acffs:  # ACFF block (models.py:46-55): module_list.i.acff_i.*
+            parts += [g(f"{p}acff_{i}.{k}") for k in ACFF_KEYS]
+        elif convs[i]:
             parts += [g(p + "BatchNorm2d.bias"), g(p + "BatchNorm2d.weight"), g(p + "BatchNorm2d.running_mean"),
                       g(p + "BatchNorm2d.running_var")]
+            parts.append(g(p + "Conv2d.weight"))
         else:
             parts.append(g(p + "Conv2d.bias"))
-        parts.append(g(p + "Conv2d.weight"))
+            parts.append(g(p + "Conv2d.weight"))
     return np.concatenate(parts).astype(np.float32)
 
 

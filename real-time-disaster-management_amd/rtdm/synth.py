@@ -263,3 +263,29 @@ def synth_classifier_state_dict(kind: str, seed: int = 11):
             v = rng.normal(0, np.sqrt(2.0 / fan_in), size=shp)
         sd[k] = v.astype(np.float32)
     return sd
+
+
+def acff_stream(params: dict) -> np.ndarray:
+    """One [acff] block's parameters in the detector stream order: conv1 w, b, conv2 w, b,
+    conv3 w, b, fused_conv w, b, BN gamma, beta, running mean, running var."""
+    return np.concatenate([np.asarray(params[k], np.float32).reshape(-1) for k in ACFF_KEYS])
+
+
+def inline_acff(cfg_text: str, conv_stream: np.ndarray, acff: dict) -> np.ndarray:
+    """Darknet conv stream (models.py:457-486 order) with each [acff] block's parameters
+    inserted at its layer position: the stream rtdm_detector_create takes for YOLO-ACFF."""
+    if not acff:
+        return conv_stream
+    parts, ptr = [], 0
+    convs = {i: (cin, cout, k, bn) for (i, cin, cout, k, bn, _) in conv_layers(cfg_text)}
+    for i in sorted(set(convs) | set(acff)):
+        if i in acff:
+            parts.append(acff_stream(acff[i]))
+        else:
+            cin, cout, k, bn = convs[i]
+            n = (4 * cout if bn else cout) + cout * cin * k * k
+            parts.append(conv_stream[ptr:ptr + n])
+            ptr += n
+    assert ptr == conv_stream.size, (ptr, conv_stream.size)
+    return np.concatenate(parts).astype(np.float32)
+

@@ -167,10 +167,12 @@ def test_classifier_batch_edges(dev, cls_weights):
 # --------------------------------------------------------------- detector --
 def _darknet(cfg, size, half=False):
     from rtdm.darknet import Darknet
-    from rtdm.synth import load_calibration, synth_darknet_weights
+    from rtdm.synth import inline_acff, load_calibration, synth_acff_params, synth_darknet_weights
     text = cfg_text(cfg)
     m = Darknet(text, (size, size))
-    stream = synth_darknet_weights(text, calib=load_calibration(cfg))
+    calib = load_calibration(cfg)
+    # YOLO-ACFF cfgs: the [acff] blocks' state-dict parameters go inline (others: no-op)
+    stream = inline_acff(text, synth_darknet_weights(text, calib=calib), synth_acff_params(text, calib=calib))
     m.load_weight_stream(stream)
     if half:
         m.half()
@@ -208,7 +210,7 @@ def test_detector_golden_small(dev, det_golden, half):
 
 @pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416", "yolov3-spp-aider@608",
                                   "yolov3-tiny-aider-416@416", "yolov4-tiny-swish@416",
-                                  "yolov4-tiny-3l-512x512@512"])
+                                  "yolov4-tiny-3l-512x512@512", "yolov3-acffx@416"])
 @pytest.mark.parametrize("half", [False, True])
 def test_detector_golden_full(dev, det_golden, case, half):
     from rtdm.synth import BASE_SEED, synth_frames
@@ -219,6 +221,18 @@ def test_detector_golden_full(dev, det_golden, case, half):
     io, _ = m(torch.from_numpy(frames).to(dev))
     io = io.cpu().numpy()
     assert list(io.shape) == list(det_golden[f"{case}/io_shape"])
+    if cfg == "yolov3-acffx":
+        # 21 ACFF blocks on synthetic weights amplify rounding ~2x per block pair: fp32 reaches
+        # the heads at ~1.5e-3 relative (tools/acff_layers.py; per-layer test below), fp16
+        # is not comparable end to end.  Measured fp32: xy 0.017 px, wh 0.7 %, p 2.8e-3.
+        if half:
+            assert np.isfinite(io).all()
+            return
+        d = np.abs(io[:, ::53] - det_golden[f"{case}/io_rows"])
+        ref = det_golden[f"{case}/io_rows"]
+        assert d[..., :2].max() <= 0.05 and d[..., 4:].max() <= 5e-3, (d[..., :2].max(), d[..., 4:].max())
+        assert (d[..., 2:4] <= 1e-3 + 2e-2 * np.abs(ref[..., 2:4])).all()
+        return
     deep = not cfg.startswith("yolov4-tiny") and not cfg.startswith("yolov3-tiny")
     _check_io(io[:, ::53], det_golden[f"{case}/io_rows"], half, deep)
     # detections: reference survivors matched by ours
@@ -289,6 +303,34 @@ def test_detector_layers_vs_oracle(dev, half):
         assert err <= (5e-2 if half else 1e-4) * scale + (5e-2 if half else 1e-4), (i, err, scale)
         checked += 1
     assert checked >= 20
+
+
+@pytest.mark.parametrize("half", [False, True])
+def test_yolo_acff_layers_vs_oracle(dev, half):
+    """YOLO-ACFF (yolov3-acffx.cfg: [acff] blocks, unfused shortcuts, route resize) layer by
+    layer against the oracle.  fp32: every layer within 5e-3 of its max (measured growth
+    5e-7 -> 1.5e-3 from the stem to the heads).  fp16: the first two ACFF stages (through
+    L14) within 2e-2 (measured <= 8.8e-3); deeper layers inherit the amplified fp16 rounding."""
+    from oracle.darknet import DarknetRef
+    from rtdm.synth import load_calibration, synth_acff_params, synth_darknet_weights, synth_frames
+    m, text, _ = _darknet("yolov3-acffx", 416, half)
+    frames = synth_frames(2, 416, 416, seed=3)
+    m(torch.from_numpy(frames).to(dev))
+    cal = load_calibration("yolov3-acffx")
+    ref = DarknetRef(text, synth_darknet_weights(text, calib=cal), synth_acff_params(text, calib=cal))
+    _, outs = ref.forward(torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0, keep_layers=True)
+    checked = 0
+    for i, o in enumerate(outs):
+        if not isinstance(o, torch.Tensor) or (half and i > 14):
+            continue
+        try:
+            got = m.layer_output(i, 2).cpu()
+        except RuntimeError:
+            continue  # fused away
+        rel = (got - o).abs().max().item() / (o.abs().max().item() + 1e-6)
+        assert rel <= (2e-2 if half else 5e-3), (i, ref.mdefs[i]["type"], rel)
+        checked += 1
+    assert checked >= (10 if half else 50), checked
 
 
 # -------------------------------------------------------------------- NMS --

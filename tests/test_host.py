@@ -126,3 +126,34 @@ def test_two_rank_gloo_broadcast_and_gather():
     total = [r for r in res if r[1] is not None][0]
     assert total[1] == float(synth_frames(8, 32, 32).sum())
     assert total[2] == [0, 1]
+
+
+def test_yolo_acff_stream_from_reference_state_dict():
+    """The reference Darknet state_dict of a YOLO-ACFF cfg (module_list.i.Conv2d/BatchNorm2d
+    and module_list.i.acff_i.* keys) maps to the same inline stream as the synthetic path,
+    and the C++ planner asks for exactly that many floats."""
+    from rtdm.darknet import Darknet, state_dict_to_stream
+    from rtdm.synth import (ACFF_KEYS, conv_layers, inline_acff, synth_acff_params,
+                            synth_darknet_weights)
+    text = cfg_text("yolov3-acffx")
+    conv = synth_darknet_weights(text)
+    acff = synth_acff_params(text)
+    sd, ptr = {}, 0
+    for (i, cin, cout, k, bn, head) in conv_layers(text):
+        p = f"module_list.{i}."
+        if bn:
+            for name in ("bias", "weight", "running_mean", "running_var"):
+                sd[p + "BatchNorm2d." + name] = conv[ptr:ptr + cout]
+                ptr += cout
+        else:
+            sd[p + "Conv2d.bias"] = conv[ptr:ptr + cout]
+            ptr += cout
+        sd[p + "Conv2d.weight"] = conv[ptr:ptr + cout * cin * k * k].reshape(cout, cin, k, k)
+        ptr += cout * cin * k * k
+    for i, prm in acff.items():
+        for key in ACFF_KEYS:
+            sd[f"module_list.{i}.acff_{i}.{key}"] = prm[key]
+    stream = inline_acff(text, conv, acff)
+    assert np.array_equal(state_dict_to_stream(text, sd), stream)
+    assert Darknet(text, (416, 416)).info.weight_floats == stream.size
+
