@@ -333,6 +333,101 @@ def test_yolo_acff_layers_vs_oracle(dev, half):
     assert checked >= (10 if half else 50), checked
 
 
+_ACFF_MINI = """[net]
+width=64
+height=64
+channels=3
+
+[convolutional]
+batch_normalize=1
+filters=8
+size=3
+stride=1
+pad=1
+activation=leaky
+
+[acff]
+filters=16
+size=3
+
+[route]
+layers=-1,-2
+
+[convolutional]
+batch_normalize=1
+filters=24
+size=1
+stride=1
+pad=1
+activation=leaky
+
+[convolutional]
+batch_normalize=1
+filters=24
+size=3
+stride=1
+pad=1
+activation=leaky
+
+[shortcut]
+from=-3
+activation=linear
+
+[convolutional]
+size=1
+stride=1
+pad=1
+filters=14
+activation=linear
+
+[yolo]
+mask=0,1
+anchors=10,14, 23,27
+classes=2
+num=2
+
+[route]
+layers=-4
+
+[convolutional]
+size=1
+stride=1
+pad=1
+filters=14
+activation=linear
+
+[yolo]
+mask=0,1
+anchors=10,14, 23,27
+classes=2
+num=2
+"""
+
+
+@pytest.mark.parametrize("half", [False, True])
+def test_acff_route_resize_shortcut_small(dev, half):
+    """A 64x64 net with one [acff] block (62x62 output), a route of mismatched widths (the
+    ACFF map nearest-resized to 64, models.py:364-375) and a shortcut whose pre-add conv
+    output is routed again (unfused ST_ADD), against the oracle: shallow, so the fp32/fp16
+    bars of the tiny detectors apply."""
+    from oracle.darknet import DarknetRef
+    from rtdm.darknet import Darknet
+    from rtdm.synth import inline_acff, synth_acff_params, synth_darknet_weights, synth_frames
+    conv = synth_darknet_weights(_ACFF_MINI, seed=5)
+    acff = synth_acff_params(_ACFF_MINI, seed=6)
+    m = Darknet(_ACFF_MINI, (64, 64))
+    m.load_weight_stream(inline_acff(_ACFF_MINI, conv, acff))
+    if half:
+        m.half()
+    desc = m.describe()
+    assert "resize nearest" in desc and "shortcut add" in desc and "acff dw3x3" in desc, desc
+    frames = synth_frames(3, 64, 64, seed=21)
+    io, _ = m(torch.from_numpy(frames).to(dev))
+    ref = DarknetRef(_ACFF_MINI, conv, acff).forward(torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0)
+    assert io.shape == ref.shape
+    _check_io(io.cpu().numpy(), ref.numpy(), half)
+
+
 # -------------------------------------------------------------------- NMS --
 def _nms_compare(io, conf, iou, multi_label=True, agnostic=False, classes=None):
     from oracle import nms as ON
