@@ -1,23 +1,35 @@
 #!/usr/bin/env python3
 """Two-stage aerial-frame inference benchmark (BASELINE.json metric).
 
-One step = one batch of synthetic 608x608 uint8 frames through the whole hot
-path on the GPU: classifier CLI transform + ACFF classifier (ErNET by default),
-Darknet detector of record (yolov4-tiny-aider-416.cfg run at 608x608; /255
-fused), YOLO decode (fused into the head convs) and per-image NMS (conf 0.3,
-IoU 0.4, detect.py defaults).  Frames are resident in HBM before timing.
+One step = one GLOBAL batch of synthetic 608x608 uint8 frames (default 64) through
+the whole hot path on the GPU(s): classifier CLI transform + ACFF classifier (ErNET,
+the reference's trained weights), Darknet detector of record (yolov4-tiny-aider-416.cfg
+run at 608x608; /255 fused), YOLO decode (fused into the head convs) and per-image NMS
+(conf 0.3, IoU 0.4, detect.py defaults).  Frames are resident in HBM before timing.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-       (one rank per GPU; each rank processes its own shard of frames —
-       batch 64 per GPU, weak scaling; weights broadcast once over RCCL).
+       one rank per GPU; the global batch is frame-sharded (rank r processes frames
+       [r*B/N, (r+1)*B/N), SURVEY.md §8e: 8 frames per GPU at N=8), weights are
+       broadcast once over RCCL and every step ends with a gather of all ranks'
+       results (logits, probs, detections, indices, counts) to rank 0 over RCCL.
+       --per-gpu-batch b instead fixes the frames per GPU (weak scaling).
+
+Each rank replays the step as one hipGraph per input buffer (TwoStagePipeline
+graphs=True); the steps cycle over --rotate distinct frame batches so no step
+re-reads the previous step's frames from the 256 MB Infinity Cache.
 
 Prints ONE JSON line on rank 0 (value = frames/s over all ranks), with
-  roofline:     the dominant kernel (largest summed device time in the timed
-                region, measured with hipEvents on the launch stream) against
-                the dense fp16 MFMA peak
-  cpu_baseline: the CPU oracle (torch-CPU restatement of the reference path,
-                incl. NMS) timed on a bounded sample on this host, rank 0 only.
+  roofline:     the dominant kernel (largest summed device time), its algorithmic FLOP
+                per launch / its average launch time from hipEvents recorded on its
+                launch stream around every detector launch, over --roofline-steps eager
+                steps run right after the timed region (events cannot sit inside the
+                replayed graphs), against the dense fp16 MFMA peak; traffic from the
+                committed rocprofv3 PMC passes (profiles/*_traffic.json)
+  cpu_baseline: the CPU oracle (torch-CPU restatement of the reference path, incl. NMS)
+                timed on a bounded sample on this host, rank 0 at N=1 only
+  h2d:          the same step with the frames uploaded from pinned host memory inside
+                the timed step (PCIe-inclusive rate; never `value`)
 """
 from __future__ import annotations
 
@@ -25,6 +37,7 @@ import argparse
 import ctypes
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -35,16 +48,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "real-time-disaster-management_amd"))
 
 MFMA_F16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/fp16
-HBM_PEAK_GBS = 8000.0
 CLASSIFIER_FLOP = {"squeeze-ernet": 90953544.0, "squeeze-redconv": 77593080.0, "ernet": 319307650.0}
+METRIC = "frames/sec two-stage (ErNET→YOLOv4) 608×608 b64 @1/2/4/8 GPU; top-1/mAP parity"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="frames per GPU per step")
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=64, help="global frames per step (sharded over the ranks)")
+    ap.add_argument("--per-gpu-batch", type=int, default=0,
+                    help="> 0: frames per GPU per step instead (weak scaling; global = this * N)")
     ap.add_argument("--img", type=int, default=608)
     ap.add_argument("--cfg", default="yolov4-tiny-aider-416")
     ap.add_argument("--classifier", default="ernet", choices=["ernet", "squeeze-ernet", "squeeze-redconv"])
@@ -56,15 +71,18 @@ def parse():
                     help="1: classifier on a side stream beside the detector; 0: both stages serial")
     ap.add_argument("--priority", type=int, default=0,
                     help="1: detector + NMS on a high-priority stream, classifier on a low-priority one")
-    ap.add_argument("--step-events", type=int, default=1,
-                    help="0: no per-step hipEvents in the timed region (roofline fields then null)")
+    ap.add_argument("--graphs", type=int, default=1, help="1: replay each step as a hipGraph; 0: eager launches")
+    ap.add_argument("--rotate", type=int, default=4, help="distinct frame batches the steps cycle over")
+    ap.add_argument("--roofline-steps", type=int, default=20,
+                    help="eager steps with per-launch hipEvents after the timed region (0: no roofline)")
+    ap.add_argument("--h2d-steps", type=int, default=20, help="PCIe-inclusive steps (0: skip)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU oracle leg")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="CPU oracle leg: time chunks of 16 frames until this much CPU time has passed")
     return ap.parse_args()
 
 
-def dist_setup(args):
+def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -78,52 +96,44 @@ def dist_setup(args):
     return world, rank, local
 
 
+def trained_classifier(name):
+    """The reference's trained state dict (weights/<name>-state_dict.pt, copied into
+    tests/golden/classifier_weights.npz by tests/golden/make_golden.py)."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "classifier_weights.npz"), allow_pickle=False)
+    return {k.split("/", 1)[1]: z[k] for k in z.files if k.split("/", 1)[0] == name}
+
+
 def build(args, world, rank):
     from rtdm.classifier import build_model
     from rtdm.darknet import Darknet
     from rtdm.pipeline import TwoStagePipeline
-    from rtdm.synth import (inline_acff, load_calibration, synth_acff_params, synth_classifier_state_dict,
-                            synth_darknet_weights)
+    from rtdm.synth import classifier_param_shapes, inline_acff, load_calibration, synth_acff_params, \
+        synth_darknet_weights
 
     cfg_path = os.path.join(ROOT, "real-time-disaster-management_amd", "rtdm", "cfg", args.cfg + ".cfg")
     text = open(cfg_path).read()
     det = Darknet(text, (args.img, args.img))
     cls = build_model(args.classifier)
-    # rank 0 makes the weights; RCCL broadcast to the other ranks (once, untimed)
+    # rank 0 makes / loads the weights; RCCL broadcast to the other ranks (once, untimed)
     if rank == 0:
         calib = load_calibration(args.cfg)
         conv, acff = synth_darknet_weights(text, calib=calib), synth_acff_params(text, calib=calib)
         stream = inline_acff(text, conv, acff)  # YOLO-ACFF cfgs: [acff] params inline
         args.ref_weights = (conv, acff)         # the CPU oracle takes them apart
-        sd = synth_classifier_state_dict(args.classifier)
+        sd = trained_classifier(args.classifier)
     else:
         stream, sd = None, None
     if world > 1:
-        import torch.distributed as dist
-        n = torch.tensor([det.info.weight_floats], device="cuda")
-        t = torch.from_numpy(stream).cuda() if rank == 0 else torch.empty(int(n.item()), device="cuda")
-        dist.broadcast(t, 0)
-        stream = t.cpu().numpy()
-        keys = sorted(synth_classifier_state_dict(args.classifier).keys())
-        flat = torch.cat([torch.from_numpy(sd[k]).reshape(-1) for k in keys]).cuda() if rank == 0 else None
-        shapes = {k: v.shape for k, v in synth_classifier_state_dict(args.classifier).items()}
-        total = sum(int(np.prod(shapes[k])) for k in keys)
-        if rank != 0:
-            flat = torch.empty(total, device="cuda")
-        dist.broadcast(flat, 0)
-        flat = flat.cpu().numpy()
-        sd, o = {}, 0
-        for k in keys:
-            c = int(np.prod(shapes[k]))
-            sd[k] = flat[o:o + c].reshape(shapes[k])
-            o += c
+        from rtdm.distributed import broadcast_array, broadcast_state_dict
+        stream = broadcast_array(stream)
+        sd = broadcast_state_dict(sd, classifier_param_shapes(args.classifier))
     det.load_weight_stream(stream)
     cls.load_state_dict(sd)
     if args.dtype == "f16":
         det.half()
         cls.half()
     pipe = TwoStagePipeline(cls, det, args.conf, args.iou, args.max_det, overlap=bool(args.overlap),
-                            priority=bool(args.priority))
+                            priority=bool(args.priority), graphs=bool(args.graphs))
     return pipe, det, cls, text, stream, sd
 
 
@@ -141,10 +151,10 @@ def step_table(det, n):
     return h, rows
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/*_traffic.json, written by tools/prof_summary.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command;
+def pmc_traffic(kernel, per_gpu_batch):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary that was
+    measured at this per-GPU batch (profiles/*_traffic.json, written by tools/prof_summary.py
+    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench command;
     FETCH_SIZE doubled per the gfx950 correction).  None when no pass covers it."""
     import glob
     base = kernel.split("<")[0]
@@ -154,10 +164,24 @@ def pmc_traffic(kernel):
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
+        if d.get("_per_gpu_batch", 64) != per_gpu_batch:
+            continue
         for k, t in d.items():
+            if k.startswith("_") or not isinstance(t, dict):
+                continue
             if k.split("<")[0] == base and "fetch_size_bytes_avg" in t and "write_size_bytes_avg" in t:
                 return {"bytes_per_launch": t["hbm_bytes_avg"], "source": os.path.relpath(path, ROOT)}
     return None
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(args, text, stream, sd):
@@ -193,33 +217,62 @@ def cpu_baseline(args, text, stream, sd):
         dt += time.perf_counter() - t0
         done += chunk
     return {"value": round(done / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"first {done} frames of the same synthetic {args.img}x{args.img} workload in chunks of {chunk}, "
                       f"fp32 torch-CPU oracle ({args.classifier} + {args.cfg} + decode + NMS), {dt:.1f} s"}
 
 
+def make_frames(args, first, count, dev):
+    """`--rotate` distinct frame batches of this rank's shard: the seeded synthetic frames
+    (frame i depends only on the seed and its global index) and, for
+    rotation j > 0, the same frames cyclically shifted by (37j, 53j) pixels on the device."""
+    from rtdm.synth import synth_frames
+    base = torch.from_numpy(synth_frames(count, args.img, args.img, first=first)).to(dev)
+    out = [base]
+    for j in range(1, max(1, args.rotate)):
+        out.append(torch.roll(base, shifts=(37 * j, 53 * j), dims=(1, 2)).contiguous())
+    return out
+
+
 def main():
     args = parse()
-    world, rank, local = dist_setup(args)
-    from rtdm.synth import synth_frames
-    dev = torch.device("cuda", torch.cuda.current_device())
-    pipe, det, cls, text, stream, sd = build(args, world, rank)
-    b = args.batch
-    frames = torch.from_numpy(synth_frames(b, args.img, args.img, first=rank * b)).to(dev)
-    torch.cuda.synchronize()
-    for _ in range(args.warmup):
-        pipe(frames)
-    torch.cuda.synchronize()
-    h, steps = step_table(det, b)
-    from rtdm import _lib as L
-    if args.step_events:
-        L.check(L.lib().rtdm_detector_enable_timing(h, args.steps))
+    world, rank, local = dist_setup()
+    dist = None
     if world > 1:
         import torch.distributed as dist
+    from rtdm.distributed import gather_records, shard_range
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if args.per_gpu_batch > 0:
+        global_batch, scaling = args.per_gpu_batch * world, "weak"
+    else:
+        global_batch, scaling = args.batch, "strong"
+    if global_batch % world:
+        raise SystemExit(f"global batch {global_batch} does not shard evenly over {world} ranks")
+    first, b = shard_range(global_batch, world, rank)
+    pipe, det, cls, text, stream, sd = build(args, world, rank)
+    frames = make_frames(args, first, b, dev)
+    rec_len = pipe.record_layout(b)[1]
+    gathered = torch.empty((world, rec_len), device=dev, dtype=torch.float32) if world > 1 and rank == 0 else None
+    torch.cuda.synchronize()
+
+    def step(k):
+        out = pipe(frames[k % len(frames)])
+        if world > 1:
+            gather_records(out["record"], gathered if rank == 0 else None)
+        return out
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pipe(frames)
+    for k in range(args.steps):
+        evs[k][0].record()
+        out = step(k)
+        evs[k][1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -228,62 +281,109 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ms = (ctypes.c_double * len(steps))()
-    calls = ctypes.c_int()
-    if args.step_events:
+    step_ms = [s.elapsed_time(e) for s, e in evs]
+    counts = out["count"].cpu()
+    if world > 1 and rank == 0:  # every rank's shard arrived: counts of the whole global batch
+        from rtdm.pipeline import unpack_record
+        counts = torch.cat([unpack_record(gathered[r], pipe, b)["count"].cpu() for r in range(world)])
+
+    # ---- roofline: per-launch hipEvents on the detector's launch streams, eager steps ----
+    from rtdm import _lib as L
+    h, steps = step_table(det, b)
+    rl = None
+    if args.roofline_steps > 0:
+        L.check(L.lib().rtdm_detector_enable_timing(h, args.roofline_steps))
+        for k in range(args.roofline_steps):
+            pipe._launch(frames[k % len(frames)])
+        torch.cuda.synchronize()
+        ms = (ctypes.c_double * len(steps))()
+        calls = ctypes.c_int()
         L.check(L.lib().rtdm_detector_read_timing(h, ms, ctypes.byref(calls)))
         L.check(L.lib().rtdm_detector_enable_timing(h, 0))
-    # roofline: kernel symbol with the largest summed device time
-    agg = {}
-    for (name, layer, flop, byt), t in zip(steps, ms):
-        a = agg.setdefault(name, [0.0, 0.0, 0.0, 0])
-        a[0] += t
-        a[1] += flop * calls.value
-        a[2] += byt * calls.value
-        a[3] += calls.value
-    dom = max(agg, key=lambda k: agg[k][0])
-    t_ms, flop, byt, launches = agg[dom]
-    det_ms = sum(ms) / max(1, calls.value)
-    avg_ms = t_ms / launches if launches else 0.0
-    achieved_tflops = (flop / launches) / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-    tr = pmc_traffic(dom)
-    traffic = round(tr["bytes_per_launch"]) if tr else None
-    frames_total = world * b * args.steps
-    value = frames_total / elapsed
+        agg = {}
+        for (name, layer, flop, byt), t in zip(steps, ms):
+            a = agg.setdefault(name, [0.0, 0.0, 0.0, 0])
+            a[0] += t
+            a[1] += flop * calls.value
+            a[2] += byt * calls.value
+            a[3] += calls.value
+        dom = max(agg, key=lambda k: agg[k][0])
+        t_ms, flop, byt, launches = agg[dom]
+        avg_ms = t_ms / launches
+        achieved = (flop / launches) / (avg_ms * 1e-3) / 1e12
+        tr = pmc_traffic(dom, b)
+        rl = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": MFMA_F16_DENSE_PEAK_TFLOPS,
+              "unit": "TFLOP/s", "frac": round(achieved / MFMA_F16_DENSE_PEAK_TFLOPS, 4),
+              "traffic": round(tr["bytes_per_launch"]) if tr else None,
+              "avg_launch_ms": round(avg_ms, 4), "launches": launches,
+              "algorithmic_flop_per_launch": round(flop / launches),
+              "algorithmic_bytes_per_launch": round(byt / launches),
+              "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tr["source"] if tr else None,
+              "timing": f"hipEvents around each detector launch on its launch stream, {calls.value} eager steps "
+                        f"after the timed region"}
+        if rank == 0:
+            per_step = {f"L{layer}:{name}": round(t / max(1, calls.value), 4)
+                        for (name, layer, flop, byt), t in zip(steps, ms)}
+            outdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else ROOT
+            with open(os.path.join(outdir, "bench_steps.json"), "w") as f:
+                json.dump(per_step, f, indent=1)
+
+    # ---- PCIe-inclusive variant: frames uploaded from pinned host memory each step ----
+    h2d = None
+    if args.h2d_steps > 0:
+        host = [f.cpu().pin_memory() for f in frames]
+        dst = torch.empty_like(frames[0])
+        for k in range(2):
+            dst.copy_(host[k % len(host)], non_blocking=True)
+            pipe(dst)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for k in range(args.h2d_steps):
+            dst.copy_(host[k % len(host)], non_blocking=True)
+            o2 = pipe(dst)
+            if world > 1:
+                gather_records(o2["record"], gathered if rank == 0 else None)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e2 = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([e2], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e2 = float(t.item())
+        h2d = {"value": round(global_batch * args.h2d_steps / e2, 2), "unit": "frames/s",
+               "bytes_per_frame": args.img * args.img * 3, "steps": args.h2d_steps,
+               "note": "uint8 frames copied host(pinned)->HBM on the step's stream before each step"}
+
+    value = global_batch * args.steps / elapsed
     pipe_flop = det.flop_per_image + CLASSIFIER_FLOP[args.classifier]
-    counts = pipe._bufs[(b, str(dev))]["count"].cpu()
     rec = {
-        "metric": "frames/sec two-stage (ErNET→YOLOv4) 608×608 b64 @1/2/4/8 GPU; top-1/mAP parity",
+        "metric": METRIC,
         "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f16" if args.dtype == "f16" else "f32",
-        "data": "synthetic 608x608 uint8 frames (seeded), synthetic calibrated detector weights, "
-                "random-init classifier weights",
+        "scaling": scaling, "vs_baseline": None, "dtype": "f16" if args.dtype == "f16" else "f32",
+        "data": f"synthetic {args.img}x{args.img} uint8 frames (seeded, {len(frames)} rotations), synthetic "
+                f"calibrated detector weights, the reference's trained {args.classifier} weights",
         "config": {"workload": f"two-stage {args.classifier} -> {args.cfg}@{args.img} + decode + NMS "
                                f"(conf {args.conf}, iou {args.iou})",
-                   "global_batch": b * world, "per_gpu_batch": b, "img": args.img,
-                   "parallelism": f"dp{world} (frame shards, no data-path collective)"},
-        "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved_tflops, 2),
-                     "peak": MFMA_F16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved_tflops / MFMA_F16_DENSE_PEAK_TFLOPS, 4), "traffic": traffic,
-                     "avg_launch_ms": round(avg_ms, 4), "launches": launches,
-                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tr["source"] if tr else None,
-                     "algorithmic_bytes_per_launch": round(byt / launches) if launches else None},
+                   "global_batch": global_batch, "per_gpu_batch": b, "img": args.img,
+                   "parallelism": f"dp{world}: frame-sharded global batch"
+                                  + (", per-step RCCL gather of every rank's results to rank 0" if world > 1 else ""),
+                   "graphs": bool(args.graphs)},
+        "step_ms_median": round(statistics.median(step_ms), 4),
+        "step_ms_p90": round(sorted(step_ms)[int(0.9 * (len(step_ms) - 1))], 4),
+        "roofline": rl,
         "pipeline": {"flop_per_frame": pipe_flop,
                      "pipeline_tflops": round(pipe_flop * value / world / 1e12, 2),
                      "pipeline_frac": round(pipe_flop * value / world / 1e12 / MFMA_F16_DENSE_PEAK_TFLOPS, 4),
-                     "detector_kernel_ms_per_step": round(det_ms, 4),
                      "detections_per_frame": round(float(counts.float().mean()), 2)},
+        "h2d": h2d,
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(args, text, stream, sd)
     if rank == 0:
-        step_ms = {}
-        for (name, layer, flop, byt), t in zip(steps, ms):
-            step_ms[f"L{layer}:{name}"] = round(t / max(1, calls.value), 4)
-        with open(os.path.join(ROOT, "gpurun_out" if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else ".",
-                               "bench_steps.json"), "w") as f:
-            json.dump(step_ms, f, indent=1)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

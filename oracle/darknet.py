@@ -83,10 +83,19 @@ class DarknetRef:
         assert ptr == stream.size, (ptr, stream.size)
 
     @torch.no_grad()
-    def forward(self, x: torch.Tensor, keep_layers=False, raw=False):
+    def forward(self, x: torch.Tensor, keep_layers=False, raw=False, f16_storage=False):
         """x: [N,3,H,W] fp32 in [0,1] -> io [N, sum(A*ny*nx), 5+nc] (and per-layer outputs).
-        raw=True: the undecoded p rows instead (YOLOLayer training branch, models.py:240-250)."""
+        raw=True: the undecoded p rows instead (YOLOLayer training branch, models.py:240-250).
+
+        f16_storage=True: NOT the reference -- a model of what an fp16 inference engine
+        does to it (the reference's own --half path, detect.py:58-60, stores every
+        activation in fp16 too): BN folded into the conv weights (eps 1e-4), weights and the
+        input rounded to fp16, fp32 arithmetic, every layer output rounded to fp16 except the
+        raw head maps (decoded in fp32).  The fp16 parity tests bound the HIP fp16 io's
+        deviation from the fp32 oracle by a small multiple of this mode's own deviation."""
+        h16 = (lambda t: t.half().float()) if f16_storage else (lambda t: t)
         img_size = x.shape[-2:]
+        x = h16(x)
         out, io_list = [], []
         self.heads = []  # per [yolo]: grid and masked anchors (the TRT plugin's fields)
         for i, m in enumerate(self.mdefs):
@@ -96,9 +105,17 @@ class DarknetRef:
                 k = int(m["size"])
                 s = int(m["stride"])
                 pad = (k - 1) // 2 if m["pad"] else 0
-                x = F.conv2d(x, p["w"], p.get("bias"), s, pad)
-                if "gamma" in p:
-                    x = F.batch_norm(x, p["mean"], p["var"], p["gamma"], p["beta"], False, 0.003, 1e-4)
+                if f16_storage:
+                    w, b = p["w"].double(), p.get("bias")
+                    if "gamma" in p:
+                        sc = p["gamma"].double() / torch.sqrt(p["var"].double() + 1e-4)
+                        w = w * sc.view(-1, 1, 1, 1)
+                        b = (p["beta"].double() - p["mean"].double() * sc).float()
+                    x = F.conv2d(x, h16(w.float()), b, s, pad)
+                else:
+                    x = F.conv2d(x, p["w"], p.get("bias"), s, pad)
+                    if "gamma" in p:
+                        x = F.batch_norm(x, p["mean"], p["var"], p["gamma"], p["beta"], False, 0.003, 1e-4)
                 if m["activation"] == "leaky":
                     x = F.leaky_relu(x, 0.1)
                 elif m["activation"] == "swish":
@@ -109,7 +126,7 @@ class DarknetRef:
                 y = (F.conv2d(x, p["conv1.weight"], p["conv1.bias"], 1, 0, 1, c)
                      + F.conv2d(x, p["conv2.weight"], p["conv2.bias"], 1, 1, 2, c)
                      + F.conv2d(x, p["conv3.weight"], p["conv3.bias"], 1, 2, 3, c))
-                y = F.leaky_relu(F.conv2d(y, p["fused_conv.weight"], p["fused_conv.bias"]), 0.01)
+                y = F.leaky_relu(F.conv2d(h16(y), h16(p["fused_conv.weight"]), p["fused_conv.bias"]), 0.01)
                 x = F.batch_norm(y, p["batch_norm.running_mean"], p["batch_norm.running_var"],
                                  p["batch_norm.weight"], p["batch_norm.bias"], False, 0.1, 1e-5)
             elif t == "maxpool":
@@ -152,6 +169,9 @@ class DarknetRef:
                 io_list.append(self._raw(m, x) if raw else self._yolo(m, x, img_size))
             else:
                 raise ValueError(t)
+            nxt = self.mdefs[i + 1]["type"] if i + 1 < len(self.mdefs) else ""
+            if t != "yolo" and nxt != "yolo":
+                x = h16(x)
             out.append(x if (keep_layers or i in self.routs) else [])
         io = torch.cat(io_list, 1)
         return (io, out) if keep_layers else io

@@ -1,7 +1,11 @@
 // Library-level C ABI: errors, version, stand-alone decode / NMS / preprocess.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 
 #include "common.h"
 
@@ -57,16 +61,10 @@ rtdm_status rtdm_yolo_decode(const float* p, int n, int na, int no, int ny, int 
                  "yolo_decode: rows out of range");
     // create_grids (models.py:422-436): stride = max(img) / max(ng); anchor_vec = anchors / stride
     const double ystride = (double)std::max(img_h, img_w) / (double)std::max(ny, nx);
-    // anchor_vec is tiny: stage it through a device buffer owned by the stream's lifetime
-    static thread_local DevBuf av;
-    float host[16];
-    for (int i = 0; i < 2 * na; ++i) host[i] = anchors[i] / (float)ystride;
-    if (!av.p) av.alloc(sizeof(host));
-    RTDM_HIP(hipMemcpyAsync(av.p, host, sizeof(float) * 2 * na, hipMemcpyHostToDevice, (hipStream_t)stream));
-    launch_yolo_decode(p, n, na, no, ny, nx, av.as<float>(), (float)ystride, io, io_rows, row_offset,
-                       (hipStream_t)stream);
-    // the host staging array must outlive the async copy
-    RTDM_HIP(hipStreamSynchronize((hipStream_t)stream));
+    // anchor_vec (<= 16 floats) rides in the kernel arguments: asynchronous, no staging buffer
+    AnchorVec av{};
+    for (int i = 0; i < 2 * na; ++i) av.v[i] = anchors[i] / (float)ystride;
+    launch_yolo_decode(p, n, na, no, ny, nx, av, (float)ystride, io, io_rows, row_offset, (hipStream_t)stream);
   });
 }
 
@@ -115,6 +113,8 @@ rtdm_status rtdm_nms(const float* io, int n, int n_anchors, int no, float conf_t
     if (n == 0) return;
     RTDM_REQUIRE(io && det && count && workspace, RTDM_E_INVALID, "nms: NULL pointer");
     RTDM_REQUIRE(n > 0 && n_anchors > 0 && no >= 6, RTDM_E_INVALID, "nms: bad shape");
+    RTDM_REQUIRE(class_mask == ~0ull || no - 5 <= 64, RTDM_E_UNSUPPORTED,
+                 "nms: a classes filter needs nc <= 64 (class_mask is one 64-bit word)");
     RTDM_REQUIRE(workspace_bytes >= nms_workspace_size(n, n_anchors, no - 5), RTDM_E_CAPACITY,
                  "nms: workspace too small");
     launch_nms(io, n, n_anchors, no, conf_thres, iou_thres, multi_label, agnostic, class_mask, max_det, workspace, det,
@@ -127,13 +127,35 @@ rtdm_status rtdm_preprocess_frames(const uint8_t* frames, int n, int in_h, int i
   return guard([&] {
     if (n == 0) return;
     RTDM_REQUIRE(frames && out, RTDM_E_INVALID, "preprocess: NULL pointer");
-    ResizePlan p;
-    build_resize_plan(p, in_h, in_w, out_size, true);
-    DevBuf tmp;
-    tmp.alloc((size_t)n * p.rows * p.out * 3);
-    launch_preprocess(p, frames, n, tmp.as<uint8_t>(), out, 1, RTDM_F32, (hipStream_t)stream);
-    // plan + tmp are released on return: finish the work first
-    RTDM_HIP(hipStreamSynchronize((hipStream_t)stream));
+    RTDM_REQUIRE(n > 0 && in_h > 0 && in_w > 0 && out_size > 0, RTDM_E_INVALID, "preprocess: bad shape");
+    // resize tables: built (and uploaded) once per device and geometry, kept for the process
+    int dev = 0;
+    RTDM_HIP(hipGetDevice(&dev));
+    const ResizePlan* p;
+    {
+      static std::mutex mu;
+      static std::map<std::array<int, 4>, std::unique_ptr<ResizePlan>> plans;
+      std::lock_guard<std::mutex> lock(mu);
+      auto& slot = plans[{dev, in_h, in_w, out_size}];
+      if (!slot) {
+        auto np = std::make_unique<ResizePlan>();
+        build_resize_plan(*np, in_h, in_w, out_size, true);
+        slot = std::move(np);
+      }
+      p = slot.get();
+    }
+    // the horizontal-pass scratch is stream-ordered: allocated and freed on the caller's
+    // stream, so the call returns without waiting for the work
+    const hipStream_t s = (hipStream_t)stream;
+    void* tmp = nullptr;
+    RTDM_HIP(hipMallocAsync(&tmp, (size_t)n * p->rows * p->out * 3, s));
+    try {
+      launch_preprocess(*p, frames, n, (uint8_t*)tmp, out, 1, RTDM_F32, s);
+    } catch (...) {
+      (void)hipFreeAsync(tmp, s);
+      throw;
+    }
+    RTDM_HIP(hipFreeAsync(tmp, s));
   });
 }
 

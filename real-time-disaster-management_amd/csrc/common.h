@@ -292,7 +292,10 @@ void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_
 void launch_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int new_h, int new_w, int out_h,
                       int out_w, int top, int left, uint32_t pad_rgb, int swap_rb, uint8_t* out, hipStream_t s);
 
-void launch_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const float* anchor_vec, float ystride,
+struct AnchorVec {  // anchor_vec = anchors / stride of one [yolo] head (<= 8 anchors), by value
+  float v[16];
+};
+void launch_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const AnchorVec& anchor_vec, float ystride,
                         float* io, int io_rows, int row_off, hipStream_t s);
 
 // TensorRT YoloLayer_TRT decode (CalDetection / CalDetection_NewCoords,

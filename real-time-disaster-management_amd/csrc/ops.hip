@@ -1059,8 +1059,9 @@ void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_
 
 // ------------------------------------------------------------ YOLO decode --
 // YOLOLayer inference branch (models.py:252-258) on a raw NCHW head map.
+// The anchors travel in the kernel arguments (no staging buffer, no host sync).
 __global__ __launch_bounds__(256) void yolo_decode_kernel(const float* __restrict__ p, int n, int na, int no, int ny,
-                                                          int nx, const float* __restrict__ anchor_vec, float ystride,
+                                                          int nx, AnchorVec anchor_vec, float ystride,
                                                           float* __restrict__ io, int io_rows, int row_off) {
   const int64_t total = (int64_t)n * na * ny * nx * no;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -1078,7 +1079,7 @@ __global__ __launch_bounds__(256) void yolo_decode_kernel(const float* __restric
     if (k < 2)
       o = (1.f / (1.f + expf(-v)) + (float)(k == 0 ? x : y)) * ystride;
     else if (k < 4)
-      o = (expf(v) * anchor_vec[2 * a + (k - 2)]) * ystride;
+      o = (expf(v) * anchor_vec.v[2 * a + (k - 2)]) * ystride;
     else
       o = 1.f / (1.f + expf(-v));
     const size_t row = (size_t)row_off + ((size_t)a * ny + y) * nx + x;
@@ -1086,8 +1087,8 @@ __global__ __launch_bounds__(256) void yolo_decode_kernel(const float* __restric
   }
 }
 
-void launch_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const float* anchor_vec, float ystride,
-                        float* io, int io_rows, int row_off, hipStream_t s) {
+void launch_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const AnchorVec& anchor_vec,
+                        float ystride, float* io, int io_rows, int row_off, hipStream_t s) {
   const int64_t total = (int64_t)n * na * ny * nx * no;
   if (total <= 0) return;
   hipLaunchKernelGGL(yolo_decode_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, p, n, na, no, ny, nx,
@@ -1233,6 +1234,12 @@ __device__ __forceinline__ NmsWs nms_ws(void* ws, int img, size_t cap, int n_anc
   return w;
 }
 
+// classes filter (utils.py:539-540): bit c of the mask; ~0 = every class (also the only
+// mask accepted for nc > 64, checked in rtdm_nms)
+__device__ __forceinline__ bool nms_class_ok(uint64_t class_mask, int c) {
+  return class_mask == ~0ull || (c < 64 && ((class_mask >> c) & 1ull));
+}
+
 // 1. candidates (utils.py:505-536), spread over the whole chip: each block filters
 // kNmsCandBlk anchors of one image and writes its keys to its own segment (+ count).
 __global__ __launch_bounds__(kNmsCandBlk) void nms_cand_kernel(const float* __restrict__ io, int n_anchors, int no,
@@ -1260,7 +1267,7 @@ __global__ __launch_bounds__(kNmsCandBlk) void nms_cand_kernel(const float* __re
         for (int j = 0; j < nc; ++j) {
           const float sc = r[5 + j] * obj;
           if (!(sc > conf)) continue;
-          if (!((class_mask >> (j & 63)) & 1ull)) continue;
+          if (!nms_class_ok(class_mask, j)) continue;
           if (!box_finite || !isfinite(sc)) continue;
           seg[atomicAdd(&s_n, 1)] = ((uint64_t)(~__float_as_uint(sc)) << 32) | (uint32_t)(a * nc + j);
         }
@@ -1271,7 +1278,7 @@ __global__ __launch_bounds__(kNmsCandBlk) void nms_cand_kernel(const float* __re
           const float sc = r[5 + j] * obj;
           if (sc > best) { best = sc; bj = j; }
         }
-        if (((class_mask >> (bj & 63)) & 1ull) && box_finite && isfinite(best))
+        if (nms_class_ok(class_mask, bj) && box_finite && isfinite(best))
           seg[atomicAdd(&s_n, 1)] = ((uint64_t)(~__float_as_uint(best)) << 32) | (uint32_t)(a * npa + bj);
       }
     }
@@ -1305,10 +1312,10 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
   const float* P = io + (size_t)img * n_anchors * no;
   NmsWs g = nms_ws(ws, img, cap, n_anchors, nc);
   // phase timestamps (100 MHz s_memrealtime) in the slice's slack bytes: diagnostics
-  // for tools/nms_phases.py, 8 stores per image
+  // for tools/nms_phases.py only (variant bit 2, rtdm_set_tuning("nms_variant", 4))
   uint64_t* stamps = (uint64_t*)((char*)g.supp + (cap / 32 + 1) * 4);
 #define NMS_STAMP(k) \
-  if (tid == 0) stamps[k] = __builtin_amdgcn_s_memrealtime()
+  if ((variant & 4) && tid == 0) stamps[k] = __builtin_amdgcn_s_memrealtime()
   NMS_STAMP(0);
   __shared__ int s_off[kNmsThreads + 1];  // candidate offset of each anchor block (nms_cand_kernel)
   __shared__ int s_wsum[kNmsThreads / 64];

@@ -7,9 +7,10 @@ data path.  Collectives exist only at the edges:
   * broadcast_array: rank 0's weights to every rank once at start (RCCL
     broadcast over xGMI when the group backend is 'nccl'; the reference's
     nn.DataParallel re-broadcasts all weights on every forward, yolov3/test.py:42-43);
-  * gather_results: optional collection of fixed-size per-frame records
-    (logits, detections padded to max_det, counts) on rank 0 (the DataParallel
-    gather), for callers that need every result in one process.
+  * gather_records: per batch, each rank's flat output record (logits, probs,
+    detections padded to max_det, indices, counts) to rank 0 in one gather (the
+    DataParallel gather of io, yolov3/test.py:42-43, but of the post-NMS results);
+    gather_results does the same field by field.
 """
 from __future__ import annotations
 
@@ -50,6 +51,25 @@ def broadcast_state_dict(sd, shapes: dict, src: int = 0, device=None) -> dict:
         out[k] = flat[o:o + c].reshape(shapes[k])
         o += c
     return out
+
+
+def gather_records(record: torch.Tensor, out: torch.Tensor | None = None, dst: int = 0):
+    """One collective per batch: every rank's flat output record (TwoStagePipeline.record:
+    logits, probs, detections, indices and counts of its frame shard) lands in row r of
+    `out` [world, record.numel()] on `dst` (RCCL over xGMI with the 'nccl' backend: each rank
+    sends on its own link to dst; a gather of ~77 KB per rank at b8 is latency-bound, so
+    one message instead of one per field).  Ranks hold equal shard sizes.  Returns `out`
+    on dst, None elsewhere."""
+    rank = dist.get_rank()
+    world = dist.get_world_size()
+    flat = record.reshape(-1)
+    if rank == dst:
+        if out is None:
+            out = torch.empty((world, flat.numel()), dtype=flat.dtype, device=flat.device)
+        dist.gather(flat, list(out.unbind(0)), dst=dst)
+        return out
+    dist.gather(flat, None, dst=dst)
+    return None
 
 
 def gather_results(tensors: dict, dst: int = 0):

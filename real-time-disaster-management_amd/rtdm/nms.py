@@ -30,6 +30,8 @@ def class_mask(classes) -> int:
         return (1 << 64) - 1
     m = 0
     for c in classes:
+        if not 0 <= int(c) < 64:
+            raise ValueError(f"classes filter: class {c} outside the 64-bit mask (nc > 64 needs classes=None)")
         m |= 1 << int(c)
     return m
 

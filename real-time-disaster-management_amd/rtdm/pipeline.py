@@ -20,9 +20,27 @@ from . import _lib as L
 from .nms import nms_batched
 
 
+def unpack_record(flat: torch.Tensor, pipe, n: int) -> dict:
+    """Views of one flat output record (TwoStagePipeline.record_layout) as named tensors."""
+    lay, total = pipe.record_layout(n)
+    if flat.numel() != total:
+        raise ValueError(f"record has {flat.numel()} floats, layout needs {total}")
+    out = {"record": flat}
+    for k, (o, s) in lay.items():
+        c = 1
+        for d in s:
+            c *= d
+        v = flat[o:o + c]
+        if k in ("idx", "count"):
+            v = v.view(torch.int32)
+        out[k] = v.view(s)
+    return out
+
+
 class TwoStagePipeline:
     def __init__(self, classifier, detector, conf_thres: float = 0.3, iou_thres: float = 0.4, max_det: int = 300,
-                 multi_label: bool = True, agnostic: bool = False, overlap: bool = True, priority: bool = False):
+                 multi_label: bool = True, agnostic: bool = False, overlap: bool = True, priority: bool = False,
+                 graphs: bool = False):
         self.classifier = classifier
         self.detector = detector
         self.conf_thres = conf_thres
@@ -36,8 +54,14 @@ class TwoStagePipeline:
         # priority=True: detector + NMS on a high-priority stream, classifier on a low one
         # (measured: no gain over one priority, 34.4k vs 34.7k frames/s)
         self.priority = priority
+        # graphs=True: the whole batch (both stages, NMS, every cross-stream fork/join) is
+        # captured once per (batch size, input buffer, handles) into a hipGraph and replayed:
+        # one host call per batch instead of ~35 launches + stream/event operations, so the
+        # small per-rank batches of frame-sharded multi-GPU runs are not host-bound
+        self.graphs = graphs
         self._bufs = {}
         self._side = {}
+        self._graphs = {}
 
     def _side_stream(self, device):
         key = str(device)
@@ -49,21 +73,68 @@ class TwoStagePipeline:
                                torch.cuda.Stream(device=device, priority=hi), torch.cuda.Event())
         return self._side[key]
 
+    def record_layout(self, n):
+        """Field -> (offset, shape) in the flat per-batch output record: every per-frame
+        output (logits, probs, det, idx, count) is a contiguous slice of ONE float32 buffer,
+        so a rank ships its whole result to rank 0 with a single gather (SURVEY.md §8e);
+        idx and count are int32 bit patterns in that buffer."""
+        shapes = (("logits", (n, 5)), ("probs", (n, 5)), ("det", (n, self.max_det, 6)),
+                  ("idx", (n, self.max_det, 2)), ("count", (n,)))
+        out, o = {}, 0
+        for k, s in shapes:
+            out[k] = (o, s)
+            c = 1
+            for d in s:
+                c *= d
+            o += c
+        return out, o
+
     def _buffers(self, n, device):
         key = (n, str(device))
         b = self._bufs.get(key)
         if b is None:
-            f32 = dict(device=device, dtype=torch.float32)
-            b = dict(logits=torch.empty((n, 5), **f32), probs=torch.empty((n, 5), **f32),
-                     io=torch.empty((n, self.detector.n_anchors, self.detector.no), **f32),
-                     det=torch.empty((n, self.max_det, 6), **f32),
-                     idx=torch.empty((n, self.max_det, 2), device=device, dtype=torch.int32),
-                     count=torch.empty((n,), device=device, dtype=torch.int32))
+            b = unpack_record(torch.empty(self.record_layout(n)[1], device=device, dtype=torch.float32), self, n)
+            b["io"] = torch.empty((n, self.detector.n_anchors, self.detector.no), device=device, dtype=torch.float32)
             self._bufs[key] = b
         return b
 
+    def record(self, n, device):
+        """The flat output record of batch size n (valid after a call with that n)."""
+        return self._buffers(n, device)["record"]
+
     def __call__(self, frames: torch.Tensor, stream=None) -> dict:
-        """frames: [B,H,W,3] uint8 CUDA (H,W = detector img_size)."""
+        """frames: [B,H,W,3] uint8 CUDA (H,W = detector img_size).  Returns the output views
+        (logits, probs, det, idx, count, io, record), valid once `stream` reaches this point."""
+        if not self.graphs:
+            return self._launch(frames, stream)
+        n = frames.shape[0]
+        with torch.cuda.device(frames.device):
+            key = self._graph_key(frames)
+            g = self._graphs.get(key)
+            if g is None:
+                self._launch(frames)  # first call: handles, plans, workspaces, resize tables
+                torch.cuda.synchronize()
+                key = self._graph_key(frames)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._launch(frames)
+                self._graphs[key] = g
+            if stream is None:
+                g.replay()
+            else:
+                with torch.cuda.stream(stream):
+                    g.replay()
+        return self._buffers(n, frames.device)
+
+    def _graph_key(self, frames):
+        from .nms import _workspace
+        n = frames.shape[0]
+        hc = self.classifier._get_handle(n)
+        hd = self.detector.handle(n)
+        ws, _ = _workspace(frames.device, n, self.detector.n_anchors, self.detector.no - 5)
+        return (n, frames.data_ptr(), tuple(frames.shape), str(frames.device), hc.value, hd.value, ws.data_ptr())
+
+    def _launch(self, frames: torch.Tensor, stream=None) -> dict:
         n = frames.shape[0]
         b = self._buffers(n, frames.device)
         with torch.cuda.device(frames.device):

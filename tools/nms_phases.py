@@ -33,6 +33,7 @@ det.load_weight_stream(synth_darknet_weights(text, calib=load_calibration(cfg)))
 det.half()
 frames = torch.from_numpy(synth_frames(args.batch, 608, 608)).cuda()
 io, _ = det(frames)
+L.check(L.lib().rtdm_set_tuning(b"nms_variant", 4))  # diagnostic build path: phase stamps on
 for _ in range(3):
     d, i, c = N.nms_batched(io, args.conf, args.iou)
 torch.cuda.synchronize()
