@@ -194,6 +194,9 @@ void launch_abshist(View v, int n, int h, int w, int c, const unsigned* amax, un
 bool conv_pipe_ok(const ConvArgs& a);
 void launch_conv_pipe(const ConvArgs& a, hipStream_t s);
 int conv_pipe_mode();
+int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 / 128 / 64)
+void set_pipe_bm(int v);                  // 0 = cost model, else forced
+const char* conv_pipe_name(const ConvArgs& a);  // kernel symbol of that launch
 // diagnostics: conv_stem3 ablation builds (tools/ab_conv.py --key stem_abl)
 int stem_abl();
 void set_stem_abl(int v);

@@ -1281,7 +1281,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     const int bn = direct_cfg(a.cout_pad).bn;
     return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
   }
-  if (use_pipe(a, dtype)) return a.head_w ? "conv_pipe_f16+head" : "conv_pipe_f16";
+  if (use_pipe(a, dtype)) return conv_pipe_name(a);
   if (dtype == RTDM_F16 && glds_ok(a)) {
     static const char* names[2][2] = {{"conv_glds_f16<128,2>", "conv_glds_f16<128,3>"},
                                       {"conv_glds_f16<256,2>", "conv_glds_f16<256,3>"}};

@@ -3,9 +3,14 @@
 // global->LDS buffer loads, source-swizzled LDS image, scalar tap cursor) in a
 // schedule built for one workgroup per CU.
 //
-//   tile        256 (pixels) x 128 (output channels), BK = 64
-//   waves       8 = 4 (M) x 2 (N), 64 x 64 outputs each (FM x FN = 4 x 4
-//               accumulators of v_mfma_f32_16x16x32_f16), 2 waves per SIMD.
+//   tile        BM (pixels) x 128 (output channels), BK = 64; BM = 256, 128 or 64,
+//               picked per launch from the tile count (pipe_bm): small per-rank
+//               batches (M = 8 frames x 19^2 = 2,888 rows) need the smaller tiles to
+//               reach every CU.  Every BM accumulates each output in the same K
+//               order, so the results are bit-identical across BM (batch-invariant).
+//   waves       8: BM 256 = 4 (M) x 2 (N) waves of 64 x 64 outputs (FM x FN = 4 x 4
+//               accumulators of v_mfma_f32_16x16x32_f16); BM 128 = 2 x 4 waves of
+//               64 x 32; BM 64 = 2 x 4 waves of 32 x 32.  2 waves per SIMD.
 //               (Measured alternative: 4 waves of 128 x 64 — 3/4 of the LDS read
 //               bytes per FLOP — ran 30 % slower: one wave per SIMD, and hipcc
 //               spills the 128 accumulators into AGPR copy chains in the loop.)
@@ -26,15 +31,23 @@
 namespace rtdm {
 
 namespace {
-constexpr int kPBM = 256, kPBN = 128, kPBK = 64, kPNS = 3;
-constexpr int kPStage = (kPBM + kPBN) * kPBK;  // halfs per stage
+constexpr int kPBN = 128, kPBK = 64, kPNS = 3;
 constexpr int kPCstr = kPBN + 4;
-constexpr int kPSmem = kPNS * kPStage * 2 > kPBM * kPCstr * 4 ? kPNS * kPStage * 2 : kPBM * kPCstr * 4;
+template <int BM>
+struct PipeCfg {
+  static constexpr int WM = BM == 256 ? 4 : 2, WN = 8 / WM;
+  static constexpr int Stage = (BM + kPBN) * kPBK;  // halfs per stage
+  static constexpr int Smem = kPNS * Stage * 2 > BM * kPCstr * 4 ? kPNS * Stage * 2 : BM * kPCstr * 4;
+};
 
 template <int N>
 __device__ __forceinline__ void wait_vm_lgkm0() {
   if constexpr (N == 6)
     asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 4)
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 3)
+    asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
   else if constexpr (N == 12)
     asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
   else
@@ -79,17 +92,18 @@ __device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v
 // 4 = no wait + barrier in the K-loop, 16 = no epilogue (one guarded store keeps the
 // MFMAs live), 32 = no K-loop (prologue + epilogue only).  Bit 8 (not an ablation):
 // fused YOLO head; bit 128 (not an ablation): lean epilogue (epi_vec8_lean).
-// One 256 x 128 output tile (logical tile index bid, M-major over N tiles).
-template <int ABL>
+// One BM x 128 output tile (logical tile index bid, M-major over N tiles).
+template <int ABL, int BM>
 __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem_raw, int bid) {
-  constexpr int WM = 4, WN = 2;
-  constexpr int BM = kPBM, BN = kPBN, BK = kPBK;
+  constexpr int WM = PipeCfg<BM>::WM, WN = PipeCfg<BM>::WN;
+  constexpr int BN = kPBN, BK = kPBK;
+  constexpr int kPStage = PipeCfg<BM>::Stage;
   constexpr int WAVES = WM * WN, NT = 64 * WAVES;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // accumulators per wave
   constexpr int NA = BM * BK * 2 / (NT * 16);          // A buffer->LDS ops per thread per stage
   constexpr int NB = BN * BK * 2 / (NT * 16);          // B ops
   constexpr int VM = NA + NB;
-  static_assert(VM == 6 || VM == 12, "wait literal");
+  static_assert(VM == 6 || VM == 4 || VM == 3, "wait literal");
   _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -335,33 +349,37 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
         }
     }
     __syncthreads();
-    f4 hacc[2][2];
+    // each wave: BM / 8 rows (HT fragments of 16) x the 32 head channels
+    constexpr int HR = BM / WAVES, HT = HR / 16;
+    static_assert(HT >= 1, "fused head needs BM >= 128");
+    f4 hacc[HT][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < HT; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) hacc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
     const _Float16* hw = (const _Float16*)a.head_w;  // [32][128]
 #pragma unroll
     for (int ks = 0; ks < BN / 32; ++ks) {
-      h8 af[2], bf[2];
+      h8 af[HT], bf[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int row = 32 * wid + 16 * t + fr;
+      for (int t = 0; t < HT; ++t) {
+        const int row = HR * wid + 16 * t + fr;
         af[t] = *(const h8*)(Hs + row * BN + 8 * ((4 * ks + g) ^ (row & 15)));
-        bf[t] = *(const h8*)(hw + (16 * t + fr) * BN + 32 * ks + 8 * g);
       }
 #pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
+      for (int t = 0; t < 2; ++t) bf[t] = *(const h8*)(hw + (16 * t + fr) * BN + 32 * ks + 8 * g);
+#pragma unroll
+      for (int tm = 0; tm < HT; ++tm)
 #pragma unroll
         for (int tq = 0; tq < 2; ++tq)
           hacc[tm][tq] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[tm], bf[tq], hacc[tm][tq], 0, 0, 0);
     }
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+    for (int tm = 0; tm < HT; ++tm)
 #pragma unroll
       for (int tq = 0; tq < 2; ++tq) {
         const int c = 16 * tq + fr;
-        if (c < a.head_cout) head_epi4(a, m_base + 32 * wid + 16 * tm + 4 * g, c, hacc[tm][tq]);
+        if (c < a.head_cout) head_epi4(a, m_base + HR * wid + 16 * tm + 4 * g, c, hacc[tm][tq]);
       }
     return;
   }
@@ -414,16 +432,16 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 // XCD (A panels shared in that XCD's L2), so a tile's epilogue stores drain while the
 // next tile's first K-blocks load, instead of every CU storing, then loading, in
 // lockstep rounds.  Between tiles only LDS is fenced (lgkmcnt): the stores stay in flight.
-template <int ABL>
+template <int ABL, int BM>
 __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a, int ntiles) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kPSmem];
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[PipeCfg<BM>::Smem];
   const int nb = gridDim.x, xcd = blockIdx.x & 7, l = blockIdx.x >> 3;
   const int q = ntiles >> 3, r = ntiles & 7;
   const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   const int hi = lo + q + (xcd < r ? 1 : 0);
   const int bx = (nb - xcd + 7) >> 3;  // workgroups on this XCD (>= 1: this one)
   for (int t = lo + l; t < hi; t += bx) {
-    pipe_tile<ABL>(a, smem_raw, t);
+    pipe_tile<ABL, BM>(a, smem_raw, t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
@@ -458,33 +476,78 @@ static int pipe_cus() {
   return n;
 }
 
+// Tile rows per launch.  A tile of BM rows costs about BM/256 of a 256-row tile's
+// K-loop at a lower per-CU rate (fewer MFMAs per LDS byte and per barrier) plus a
+// fixed prologue / epilogue; the launch takes ceil(tiles / CUs) such rounds.  The
+// smallest estimated time wins (ties: the larger tile).  rtdm_set_tuning("conv_pipe_bm",
+// 256 | 128 | 64) forces one (0 = this model).  Batch-invariant: only the tiling changes.
+static int g_pipe_bm = 0;
+void set_pipe_bm(int v) { g_pipe_bm = (v == 256 || v == 128 || v == 64) ? v : 0; }
+int pipe_bm(const ConvArgs& a) {
+  const bool head = a.head_w != nullptr;
+  if (g_pipe_bm && !(head && g_pipe_bm == 64)) return g_pipe_bm;
+  const int nk = a.kpad / kPBK, ntn = a.cout_pad / kPBN, cus = pipe_cus();
+  static const int bms[3] = {256, 128, 64};
+  static const double eff[3] = {1.0, 0.85, 0.65};
+  const double ovh = 3.0 + (head ? 4.0 : 0.0);
+  int best = 256;
+  double best_t = 1e300;
+  for (int i = 0; i < (head ? 2 : 3); ++i) {
+    const int64_t tiles = (int64_t)((a.M + bms[i] - 1) / bms[i]) * ntn;
+    const double rounds = (double)((tiles + cus - 1) / cus);
+    const double t = rounds * (bms[i] / 256.0 * nk / eff[i] + ovh * bms[i] / 256.0 + 1.0);
+    if (t < best_t * 0.97) {
+      best_t = t;
+      best = bms[i];
+    }
+  }
+  return best;
+}
+
+template <int BM>
+static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid) {
+  if (a.head_w) {
+    if constexpr (BM >= 128) hipLaunchKernelGGL((conv_pipe_f16<8, BM>), grid, dim3(512), 0, s, a, ntiles);
+  } else if (epi_lean_ok(a)) {
+    hipLaunchKernelGGL((conv_pipe_f16<128, BM>), grid, dim3(512), 0, s, a, ntiles);
+  } else {
+    hipLaunchKernelGGL((conv_pipe_f16<0, BM>), grid, dim3(512), 0, s, a, ntiles);
+  }
+}
+
+const char* conv_pipe_name(const ConvArgs& a) {
+  const int bm = pipe_bm(a);
+  if (a.head_w) return bm == 256 ? "conv_pipe_f16<8,256>" : "conv_pipe_f16<8,128>";
+  if (epi_lean_ok(a)) return bm == 256 ? "conv_pipe_f16<128,256>" : bm == 128 ? "conv_pipe_f16<128,128>" : "conv_pipe_f16<128,64>";
+  return bm == 256 ? "conv_pipe_f16<0,256>" : bm == 128 ? "conv_pipe_f16<0,128>" : "conv_pipe_f16<0,64>";
+}
+
 void launch_conv_pipe(const ConvArgs& a, hipStream_t s) {
-  const int64_t nt = (int64_t)((a.M + kPBM - 1) / kPBM) * (a.cout_pad / kPBN);
+  const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
+  const int64_t nt = (int64_t)((a.M + bm - 1) / bm) * (a.cout_pad / kPBN);
   RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
   const int ntiles = (int)nt;
   // mode 13: one workgroup per tile (non-persistent), for A/B runs
   const int cap = conv_pipe_mode() == 13 ? ntiles : pipe_cus();
   const dim3 grid((unsigned)(ntiles < cap ? ntiles : cap));
-  if (a.head_w) {
-    hipLaunchKernelGGL((conv_pipe_f16<8>), grid, dim3(512), 0, s, a, ntiles);
-    return;
-  }
-  switch (conv_pipe_mode()) {
-    case 2: hipLaunchKernelGGL((conv_pipe_f16<1>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 3: hipLaunchKernelGGL((conv_pipe_f16<2>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 4: hipLaunchKernelGGL((conv_pipe_f16<3>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 5: hipLaunchKernelGGL((conv_pipe_f16<4>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 6: hipLaunchKernelGGL((conv_pipe_f16<16>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 7: hipLaunchKernelGGL((conv_pipe_f16<19>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 8: hipLaunchKernelGGL((conv_pipe_f16<32>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 9: hipLaunchKernelGGL((conv_pipe_f16<48>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 10: hipLaunchKernelGGL((conv_pipe_f16<96>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 11: hipLaunchKernelGGL((conv_pipe_f16<0>), grid, dim3(512), 0, s, a, ntiles); break;
+  switch (a.head_w ? 1 : conv_pipe_mode()) {
+    case 2: hipLaunchKernelGGL((conv_pipe_f16<1, 256>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 3: hipLaunchKernelGGL((conv_pipe_f16<2, 256>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 4: hipLaunchKernelGGL((conv_pipe_f16<3, 256>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 5: hipLaunchKernelGGL((conv_pipe_f16<4, 256>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 6: hipLaunchKernelGGL((conv_pipe_f16<16, 256>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 7: hipLaunchKernelGGL((conv_pipe_f16<19, 256>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 8: hipLaunchKernelGGL((conv_pipe_f16<32, 256>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 9: hipLaunchKernelGGL((conv_pipe_f16<48, 256>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 10: hipLaunchKernelGGL((conv_pipe_f16<96, 256>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 11: hipLaunchKernelGGL((conv_pipe_f16<0, 256>), grid, dim3(512), 0, s, a, ntiles); break;
     default:
-      if (epi_lean_ok(a))
-        hipLaunchKernelGGL((conv_pipe_f16<128>), grid, dim3(512), 0, s, a, ntiles);
+      if (bm == 256)
+        launch_pipe_bm<256>(a, s, ntiles, grid);
+      else if (bm == 128)
+        launch_pipe_bm<128>(a, s, ntiles, grid);
       else
-        hipLaunchKernelGGL((conv_pipe_f16<0>), grid, dim3(512), 0, s, a, ntiles);
+        launch_pipe_bm<64>(a, s, ntiles, grid);
       break;
   }
 }

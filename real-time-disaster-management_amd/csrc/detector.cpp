@@ -1022,6 +1022,16 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     a.zero = (const void*)64;
     a.kpad = st.pc.kpad;
     a.cout = st.cout;
+    // the kernel instance depends on the batch (conv_pipe tile rows): the last
+    // rtdm_detect call's, max_batch before any
+    a.n = h.last_n > 0 ? h.last_n : h.max_batch;
+    conv_set_rows(a);
+    a.e.bias = (const float*)64;
+    a.e.act = st.act;
+    if (st.pc.s_off != SIZE_MAX) {
+      a.e.scale = (const float*)64;
+      a.e.shift = (const float*)64;
+    }
     if (st.in_t >= 0) {
       const View iv = view_geom(h, st.in_t);
       a.in_cs = iv.cs;

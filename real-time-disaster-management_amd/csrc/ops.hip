@@ -1458,16 +1458,25 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
     const int W = (n + 63) >> 6;
     const bool in_lds = n <= kNmsMaskCap;
     uint64_t* M = in_lds ? s_mask : g.mask;
-    // one wave per (row i, 64-column word w): lane = column j, the word is a ballot
-    // one (row i, 64-column word w) per thread; the division only where boxes meet
+    // one (row i, 16-column quarter q of word w) per thread, rows fastest: the lanes of a
+    // wave share (w, q), so each B[j] / A[j] read is one broadcast LDS address, and a
+    // quarter word gives every wave of the block work at the typical n of 100-300
+    // (LDS path: quarters ORed into the zeroed word; workspace path: whole words); the
+    // division only where boxes meet
     const bool thr_nonneg = iou_thr >= 0.0;
-    for (int p = tid; p < n * W; p += kNmsThreads) {
-      const int i = p / W, w = p - (p / W) * W;
+    const int QS = in_lds ? 4 : 1, QW = 64 / QS;
+    if (in_lds) {
+      for (int p = tid; p < n * W; p += kNmsThreads) M[p] = 0ull;
+      __syncthreads();
+    }
+    for (int p = tid; p < n * W * QS; p += kNmsThreads) {
+      const int r = p / n, i = p - r * n;
+      const int w = r / QS, q = r - w * QS;
       const float4 bi = B[i];
       const float ai = A[i];
       uint64_t bits = 0;
-      const int j0 = w * 64;
-      const int j1 = j0 + 64 < n ? j0 + 64 : n;
+      const int jw = w * 64, j0 = jw + q * QW;
+      const int j1 = j0 + QW < n ? j0 + QW : n;
       for (int j = j0 > i + 1 ? j0 : i + 1; j < j1; ++j) {
         const float4 bj = B[j];
         const float xx1 = fmaxf(bi.x, bj.x);
@@ -1479,57 +1488,107 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
         const float inter = w2 * h2;
         if (inter > 0.f || !thr_nonneg) {  // inter == 0: IoU 0 is never > a threshold >= 0
           const float ovr = inter / ((ai + A[j]) - inter);
-          if ((double)ovr > iou_thr) bits |= 1ull << (j - j0);
+          if ((double)ovr > iou_thr) bits |= 1ull << (j - jw);
         }
       }
-      M[p] = bits;
+      if (in_lds) {
+        if (bits) atomicOr((unsigned long long*)&M[(size_t)i * W + w], (unsigned long long)bits);
+      } else {
+        M[(size_t)i * W + w] = bits;
+      }
     }
     __syncthreads();
     NMS_STAMP(4);
-    // rows per LDS chunk: whole 64-candidate words
-    const int rows = in_lds ? n : ((kNmsMaskCap * (kNmsMaskCap / 64)) / W) & ~63;
-    uint64_t removed = 0;  // wave 0: lane l < W holds word l of the suppressed set
     int nk = 0;
-    for (int c0 = 0; c0 < n; c0 += rows) {
-      const int c1 = c0 + rows < n ? c0 + rows : n;
-      if (!in_lds) {
-        for (int p = tid; p < (c1 - c0) * W; p += kNmsThreads) s_mask[p] = g.mask[(size_t)c0 * W + p];
-        __syncthreads();
-      }
+    if (in_lds) {
+      // n <= 512 (W <= 8 words): wave 0, lane b holding every mask word of row 64c + b in
+      // registers while word block c is scanned.  In-word greedy pass: jump from kept
+      // candidate to the next unsuppressed one (find-first-set), so the serial chain is as
+      // long as the survivors, not the candidates; the kept rows' masks reach the later
+      // words through one wave-wide OR per word.
       if (tid < 64) {
-        // word by word: the in-word greedy pass on scalars (lane b holds row 64w+b's
-        // bits of word w), then every kept row's mask ORed into the later words
-        for (int w = c0 >> 6; w * 64 < c1; ++w) {
-          const int cnt = c1 - w * 64 < 64 ? c1 - w * 64 : 64;
-          const int i = w * 64 + tid;
-          const uint64_t mw = tid < cnt ? s_mask[(i - c0) * W + w] : 0ull;
-          uint64_t rem = readlane_u64(removed, w);
-          uint64_t kept = 0;
-          for (int b = 0; b < cnt; ++b) {
-            if ((rem >> b) & 1ull) continue;
-            kept |= 1ull << b;
-            rem |= readlane_u64(mw, b);
-          }
-          if ((kept >> tid) & 1ull) g.keep[nk + __popcll(kept & ((1ull << tid) - 1ull))] = i;
-          nk += __popcll(kept);
-          // kept rows' masks into the later words, 8 rows (LDS reads) in flight per step
-          const int tl = tid < W ? tid : W - 1;
-          for (uint64_t k = kept; k;) {
-            int bs[8];
+        uint64_t removed[kNmsMaskCap / 64];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              bs[u] = k ? __builtin_ctzll(k) : -1;
-              k &= k - 1;
+        for (int w = 0; w < kNmsMaskCap / 64; ++w) removed[w] = 0;
+#pragma unroll
+        for (int c = 0; c < kNmsMaskCap / 64; ++c) {
+          if (c < W) {
+            const int cnt = n - 64 * c < 64 ? n - 64 * c : 64;
+            const int i = 64 * c + tid;
+            uint64_t mrow[kNmsMaskCap / 64];
+#pragma unroll
+            for (int w = 0; w < kNmsMaskCap / 64; ++w) mrow[w] = (w < W && tid < cnt) ? M[(size_t)i * W + w] : 0ull;
+            const uint64_t valid = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
+            uint64_t rem = removed[c], kept = 0;
+            uint64_t todo = valid & ~rem;
+            while (todo) {
+              const int b = __builtin_ctzll(todo);
+              kept |= 1ull << b;
+              rem |= readlane_u64(mrow[c], b);
+              todo = valid & ~rem & (b == 63 ? 0ull : ~((2ull << b) - 1ull));
             }
-            uint64_t v[8];
+            if ((kept >> tid) & 1ull) g.keep[nk + __popcll(kept & ((1ull << tid) - 1ull))] = i;
+            nk += __popcll(kept);
+            const bool mine = (kept >> tid) & 1ull;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = s_mask[(w * 64 + (bs[u] < 0 ? bs[0] : bs[u]) - c0) * W + tl];
+            for (int w = c + 1; w < kNmsMaskCap / 64; ++w) {
+              if (w < W) {
+                uint32_t lo = mine ? (uint32_t)mrow[w] : 0u, hi = mine ? (uint32_t)(mrow[w] >> 32) : 0u;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) removed |= bs[u] >= 0 ? v[u] : 0ull;
+                for (int off = 32; off > 0; off >>= 1) {
+                  lo |= (uint32_t)__shfl_xor((int)lo, off);
+                  hi |= (uint32_t)__shfl_xor((int)hi, off);
+                }
+                removed[w] |= ((uint64_t)hi << 32) | lo;
+              }
+            }
           }
         }
       }
-      __syncthreads();  // the chunk's LDS rows are consumed before the next chunk lands
+    } else {
+      // kMaskCap < n <= kNmsMaskCapG: the bitmask in the workspace, scanned in chunks of
+      // whole 64-candidate words staged through the LDS mask buffer
+      const int rows = ((kNmsMaskCap * (kNmsMaskCap / 64)) / W) & ~63;
+      uint64_t removed = 0;  // wave 0: lane l < W holds word l of the suppressed set
+      for (int c0 = 0; c0 < n; c0 += rows) {
+        const int c1 = c0 + rows < n ? c0 + rows : n;
+        for (int p = tid; p < (c1 - c0) * W; p += kNmsThreads) s_mask[p] = g.mask[(size_t)c0 * W + p];
+        __syncthreads();
+        if (tid < 64) {
+          // word by word: the in-word greedy pass on scalars (lane b holds row 64w+b's
+          // bits of word w), then every kept row's mask ORed into the later words
+          for (int w = c0 >> 6; w * 64 < c1; ++w) {
+            const int cnt = c1 - w * 64 < 64 ? c1 - w * 64 : 64;
+            const int i = w * 64 + tid;
+            const uint64_t mw = tid < cnt ? s_mask[(i - c0) * W + w] : 0ull;
+            uint64_t rem = readlane_u64(removed, w);
+            uint64_t kept = 0;
+            for (int b = 0; b < cnt; ++b) {
+              if ((rem >> b) & 1ull) continue;
+              kept |= 1ull << b;
+              rem |= readlane_u64(mw, b);
+            }
+            if ((kept >> tid) & 1ull) g.keep[nk + __popcll(kept & ((1ull << tid) - 1ull))] = i;
+            nk += __popcll(kept);
+            // kept rows' masks into the later words, 8 rows (LDS reads) in flight per step
+            const int tl = tid < W ? tid : W - 1;
+            for (uint64_t k = kept; k;) {
+              int bs[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                bs[u] = k ? __builtin_ctzll(k) : -1;
+                k &= k - 1;
+              }
+              uint64_t v[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) v[u] = s_mask[(w * 64 + (bs[u] < 0 ? bs[0] : bs[u]) - c0) * W + tl];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) removed |= bs[u] >= 0 ? v[u] : 0ull;
+            }
+          }
+        }
+        __syncthreads();  // the chunk's LDS rows are consumed before the next chunk lands
+      }
     }
     if (tid == 0) s_n = nk;
     __syncthreads();

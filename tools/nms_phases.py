@@ -49,7 +49,10 @@ st = np.stack([ws[b * per + off: b * per + off + 56].view(np.uint64) for b in ra
 dt = np.diff(st, axis=1) * 10 / 1000.0  # us
 names = ["gather", "sort", "boxes", "mask", "scan", "output"]
 cnt = c.cpu().numpy()
-print(f"candidates kept per image: mean {cnt.mean():.1f} max {cnt.max()}")
+x = io.cpu().numpy()
+ok = (x[..., 4] > args.conf) & (x[..., 2] > 2) & (x[..., 3] > 2) & (x[..., 2] < 4096) & (x[..., 3] < 4096)
+ncand = ((x[..., 5:] * x[..., 4:5] > args.conf) & ok[..., None]).sum((1, 2))
+print(f"candidates per image: mean {ncand.mean():.1f} max {ncand.max()}; kept: mean {cnt.mean():.1f} max {cnt.max()}")
 print("phase      mean_us   max_us")
 for k, nm in enumerate(names):
     print(f"{nm:8s} {dt[:, k].mean():9.2f} {dt[:, k].max():8.2f}")
