@@ -28,6 +28,9 @@
  *   rtdm_yolo_layer_trt      <- YoloLayerPlugin::enqueue   tensorrt_inference/plugins/yolo_layer.cu:323-327
  *   rtdm_nms                 <- non_max_suppression()   victim_localization/yolov3/utils/utils.py:488-557
  *                               (+ torchvision.ops.boxes.nms, utils.py:552)
+ *   rtdm_letterbox           <- letterbox()             victim_localization/yolov3/utils/datasets.py:599-631
+ *   rtdm_resize_linear       <- cv2.resize(frame, (w, h)) disaster_detection/real-time-inference.py:185
+ *   rtdm_preprocess_frames   <- squeeze_transforms / aider_transforms  disaster_detection/dataloaders/aider.py:412-431
  *
  * Conventions
  *   - Plain C types only.  Device pointers are HIP device pointers owned by the
@@ -251,6 +254,15 @@ rtdm_status rtdm_letterbox_geometry(int in_h, int in_w, int shape_h, int shape_w
 rtdm_status rtdm_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int new_h, int new_w,
                            int out_h, int out_w, int top, int left, uint32_t pad_rgb, int swap_rb, uint8_t* out,
                            void* stream);
+
+/* ---- frame resize (real-time-inference.py:185, cv2.resize(frame, (width, height))) --
+ * cv2.INTER_LINEAR (the default interpolation) of uint8 3-channel frames [n, in_h, pitch]
+ * to [n, out_h, out_w, 3]: half-pixel source coordinates, 11-bit fixed-point weights
+ * (OpenCV resize.cpp restated; cv2 is not in this stack, so pixel parity with cv2 itself
+ * is unpinned, the kernel is bit-exact with oracle/letterbox.py resize_linear).
+ * swap_rb = 1 also turns BGR into RGB (the cv2.cvtColor of :70).                    */
+rtdm_status rtdm_resize_linear(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int out_h, int out_w,
+                               int swap_rb, uint8_t* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -121,6 +121,43 @@ def resize_area(img: np.ndarray, new_w: int, new_h: int) -> np.ndarray:
     return np.clip(out, 0, 255).astype(np.uint8)
 
 
+def _inter_linear_tab(ssize, dsize):
+    """cv2.INTER_LINEAR coefficients (resize.cpp): fx = (float)((d + 0.5) * scale - 0.5),
+    s = floor(fx), f = fx - s; clamped to the border pixel (f = 0) outside; 11-bit weights
+    by cvRound (nearest, ties to even)."""
+    scale = 1.0 / (dsize / ssize)
+    out = []
+    for d in range(dsize):
+        fx = np.float32((d + 0.5) * scale - 0.5)
+        s = int(np.floor(fx))
+        f = np.float32(fx - np.float32(s))
+        if s < 0:
+            s, f = 0, np.float32(0)
+        if s >= ssize - 1:
+            s, f = ssize - 1, np.float32(0)
+        c0 = int(np.rint(np.float32(np.float32(1) - f) * np.float32(2048)))
+        c1 = int(np.rint(f * np.float32(2048)))
+        out.append((s, min(s + 1, ssize - 1), c0, c1))
+    return out
+
+
+def resize_linear(img: np.ndarray, new_w: int, new_h: int) -> np.ndarray:
+    """cv2.resize(img, (new_w, new_h)) -- INTER_LINEAR, the default interpolation used by
+    real-time-inference.py:185 -- as restated above (same fixed-point sums as the
+    INTER_AREA growing path: int horizontal taps, (b0*h0 + b1*h1 + 2^21) >> 22)."""
+    src = img.astype(np.int64)
+    xt, yt = _inter_linear_tab(img.shape[1], new_w), _inter_linear_tab(img.shape[0], new_h)
+    x0 = np.array([t[0] for t in xt])
+    x1 = np.array([t[1] for t in xt])
+    c0 = np.array([t[2] for t in xt], np.int64)[None, :, None]
+    c1 = np.array([t[3] for t in xt], np.int64)[None, :, None]
+    hrow = src[:, x0, :] * c0 + src[:, x1, :] * c1
+    out = np.empty((new_h, new_w, 3), np.int64)
+    for dy, (y0, y1, b0, b1) in enumerate(yt):
+        out[dy] = (b0 * hrow[y0] + b1 * hrow[y1] + (1 << 21)) >> 22
+    return np.clip(out, 0, 255).astype(np.uint8)
+
+
 def letterbox(img: np.ndarray, geom, color=(128, 128, 128)) -> np.ndarray:
     """Resize to (new_w, new_h) and pad into the (out_h, out_w) canvas (datasets.py:626-630)."""
     new_h, new_w, out_h, out_w, top, left = geom

@@ -203,4 +203,15 @@ rtdm_status rtdm_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int
   });
 }
 
+rtdm_status rtdm_resize_linear(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int out_h, int out_w,
+                               int swap_rb, uint8_t* out, void* stream) {
+  return guard([&] {
+    if (n == 0) return;
+    RTDM_REQUIRE(frames && out, RTDM_E_INVALID, "resize_linear: NULL pointer");
+    RTDM_REQUIRE(out_h > 0 && out_w > 0, RTDM_E_INVALID, "resize_linear: bad output size");
+    launch_letterbox(frames, n, in_h, in_w, pitch, out_h, out_w, out_h, out_w, 0, 0, 0u, swap_rb, out,
+                     (hipStream_t)stream, 1);
+  });
+}
+
 }  // extern "C"

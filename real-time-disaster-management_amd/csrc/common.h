@@ -293,7 +293,8 @@ void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_
 // Letterbox (datasets.py:599-631): cv2 INTER_AREA resize to new_w x new_h at (left, top)
 // of an out_h x out_w canvas of pad_rgb; uint8 3-channel frames (row pitch in bytes).
 void launch_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int new_h, int new_w, int out_h,
-                      int out_w, int top, int left, uint32_t pad_rgb, int swap_rb, uint8_t* out, hipStream_t s);
+                      int out_w, int top, int left, uint32_t pad_rgb, int swap_rb, uint8_t* out, hipStream_t s,
+                      int interp = 0 /*0: INTER_AREA rules, 1: INTER_LINEAR*/);
 
 struct AnchorVec {  // anchor_vec = anchors / stride of one [yolo] head (<= 8 anchors), by value
   float v[16];

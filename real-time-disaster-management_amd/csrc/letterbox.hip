@@ -12,6 +12,8 @@
 //                                    v = sum beta*h in fp32 without contraction, cvRound
 //   * otherwise (growing)         -> linear with INTER_AREA's coefficients, 11-bit
 //                                    fixed point (HResizeLinear int + FixedPtCast 22)
+// The same kernel runs cv2.resize's default INTER_LINEAR (real-time-inference.py:185,
+// rtdm_resize_linear): a linear table with cv2's half-pixel source coordinates.
 // One thread per output pixel (3 channels); the pad region is a constant store.
 // Frames arrive once per batch and are small next to the detector's traffic (a
 // 640x480 frame is 0.9 MB in, 0.5 MB out at 416), so this is a plain L2-cached
@@ -82,14 +84,40 @@ void linear_tab(int ssize, int dsize, std::vector<int>& out) {
   }
 }
 
-std::mutex g_lb_mu;
-std::map<std::tuple<int, int, int, int, int>, std::unique_ptr<LbTables>> g_lb_cache;
+// cv2.INTER_LINEAR (resize.cpp, fixed-point 8-bit path): fx = (float)((d + 0.5) * scale
+// - 0.5), s = cvFloor(fx), f = fx - s; left of the first / right of the last source
+// pixel the coordinate collapses to that pixel (f = 0); 11-bit coefficients by cvRound.
+void inter_linear_tab(int ssize, int dsize, std::vector<int>& out) {
+  const double scale = 1.0 / ((double)dsize / (double)ssize);
+  out.resize(4 * (size_t)dsize);
+  for (int d = 0; d < dsize; ++d) {
+    float fx = (float)((d + 0.5) * scale - 0.5);
+    int s = (int)std::floor(fx);
+    fx -= (float)s;
+    if (s < 0) {
+      s = 0;
+      fx = 0.f;
+    }
+    if (s >= ssize - 1) {
+      s = ssize - 1;
+      fx = 0.f;
+    }
+    out[4 * d + 0] = s;
+    out[4 * d + 1] = std::min(s + 1, ssize - 1);
+    out[4 * d + 2] = (int)std::nearbyint((1.f - fx) * 2048.f);
+    out[4 * d + 3] = (int)std::nearbyint(fx * 2048.f);
+  }
+}
 
-const LbTables& lb_tables(int in_h, int in_w, int new_h, int new_w) {
+std::mutex g_lb_mu;
+std::map<std::tuple<int, int, int, int, int, int>, std::unique_ptr<LbTables>> g_lb_cache;
+
+// interp 0: INTER_AREA rules (letterbox); 1: INTER_LINEAR (cv2.resize default)
+const LbTables& lb_tables(int in_h, int in_w, int new_h, int new_w, int interp) {
   int dev = 0;
   RTDM_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_lb_mu);
-  auto key = std::make_tuple(dev, in_h, in_w, new_h, new_w);
+  auto key = std::make_tuple(dev, in_h, in_w, new_h, new_w, interp);
   auto it = g_lb_cache.find(key);
   if (it != g_lb_cache.end()) return *it->second;
   auto t = std::make_unique<LbTables>();
@@ -99,7 +127,14 @@ const LbTables& lb_tables(int in_h, int in_w, int new_h, int new_w) {
     const uint8_t* b = (const uint8_t*)p;
     host.insert(host.end(), b, b + bytes);
   };
-  if (scx >= 1.0 && scy >= 1.0) {
+  if (interp == 1) {
+    t->mode = LB_LINEAR;
+    std::vector<int> xt, yt;
+    inter_linear_tab(in_w, new_w, xt);
+    inter_linear_tab(in_h, new_h, yt);
+    append(xt.data(), xt.size() * 4);
+    append(yt.data(), yt.size() * 4);
+  } else if (scx >= 1.0 && scy >= 1.0) {
     const int isx = (int)std::lround(scx), isy = (int)std::lround(scy);
     if (std::fabs(scx - isx) < 2.220446049250313e-16 && std::fabs(scy - isy) < 2.220446049250313e-16) {
       RTDM_REQUIRE(isx * isy <= 65536, RTDM_E_INVALID, "letterbox: shrink factor too large");
@@ -251,13 +286,14 @@ __global__ void __launch_bounds__(256) letterbox_kernel(LbArgs a) {
 }  // namespace
 
 void launch_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int new_h, int new_w, int out_h,
-                      int out_w, int top, int left, uint32_t pad_rgb, int swap_rb, uint8_t* out, hipStream_t s) {
+                      int out_w, int top, int left, uint32_t pad_rgb, int swap_rb, uint8_t* out, hipStream_t s,
+                      int interp) {
   RTDM_REQUIRE(n > 0 && n <= 65535, RTDM_E_INVALID, "letterbox: n must be in [1, 65535]");
   RTDM_REQUIRE(in_h > 0 && in_w > 0 && new_h > 0 && new_w > 0, RTDM_E_INVALID, "letterbox: bad shape");
   RTDM_REQUIRE(pitch >= in_w * 3, RTDM_E_INVALID, "letterbox: pitch < 3 * in_w");
   RTDM_REQUIRE(top >= 0 && left >= 0 && top + new_h <= out_h && left + new_w <= out_w, RTDM_E_INVALID,
                "letterbox: resized frame does not fit the canvas");
-  const LbTables& t = lb_tables(in_h, in_w, new_h, new_w);
+  const LbTables& t = lb_tables(in_h, in_w, new_h, new_w, interp);
   LbArgs a;
   a.src = frames;
   a.frame_bytes = (int64_t)pitch * in_h;

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Drop-in for disaster_detection/real-time-inference.py on the HIP runtime.
 
-Same flags (:134-152) and statistics (average / min / max FPS, :218-221).  Per frame:
-resize to --width x --height (the reference's cv2.resize, here Pillow bilinear), then the
-on-device CLI transform + classifier (rtdm_classify on the uint8 frame).  Video decoding
+Same flags (:134-152) and statistics (average / min / max FPS, :218-221).  Per frame, on
+the device: cv2.resize(frame, (--width, --height)) with its default INTER_LINEAR (:185;
+rtdm_resize_linear, OpenCV's algorithm restated), then the CLI transform + classifier
+(rtdm_classify on the uint8 frame, :62-107).  Video decoding
 (imutils/cv2) is not part of this stack: --video takes a directory of image frames or an
 .npy array [T,H,W,3] uint8; webcam capture is not available.  ``--batch`` > 1 classifies
 that many frames per call (throughput mode); the default 1 is the reference's per-frame loop.
@@ -21,12 +22,13 @@ import torch  # noqa: E402
 
 from rtdm.classifier import load_model  # noqa: E402
 from rtdm.cli import list_images, predict_frames, read_image_rgb, select_device  # noqa: E402
+from rtdm.letterbox import resize_linear  # noqa: E402
 
 logger = logging.getLogger(__name__)
 
 
-def frame_source(video: str, width: int, height: int):
-    from PIL import Image
+def frame_source(video: str):
+    """Host RGB frames, in order (decoding stays on the host)."""
     if video is None:
         raise SystemExit("webcam capture needs cv2/imutils, which this stack does not ship: pass --video")
     if video.endswith(".npy"):
@@ -34,10 +36,7 @@ def frame_source(video: str, width: int, height: int):
         it = (frames[i] for i in range(frames.shape[0]))
     else:
         it = (read_image_rgb(p) for p in list_images(video))
-    for f in it:
-        if f.shape[0] != height or f.shape[1] != width:
-            f = np.asarray(Image.fromarray(f).resize((width, height), Image.BILINEAR), dtype=np.uint8)
-        yield f
+    yield from it
 
 
 def main(argv=None):
@@ -63,7 +62,7 @@ def main(argv=None):
 
     def flush():
         nonlocal prev
-        frames = torch.from_numpy(np.stack(pending)).to(device)
+        frames = torch.stack(pending)
         _, names, conf = predict_frames(model, frames)
         now = time.time()
         fps_list.append(len(pending) / (now - prev))
@@ -71,8 +70,9 @@ def main(argv=None):
         results.extend(zip(names, conf))
         pending.clear()
 
-    for f in frame_source(args.video, args.width, args.height):
-        pending.append(f)
+    for f in frame_source(args.video):
+        # upload the decoded frame, cv2.resize(frame, (width, height)) on the device (:185)
+        pending.append(resize_linear(torch.from_numpy(np.ascontiguousarray(f)).to(device), args.height, args.width))
         if len(pending) == args.batch:
             flush()
     if pending:

@@ -87,6 +87,7 @@ SIGNATURES = {
     "rtdm_letterbox_geometry": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, POINTER(c_int)]),
     "rtdm_letterbox": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_uint32, c_int, c_void_p, c_void_p]),
+    "rtdm_resize_linear": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -176,15 +176,53 @@ def build_model(model_name: str) -> _ACFFClassifier:
     raise ValueError(f"Unsupported model: {model_name}")
 
 
+# Full-module pickles (disaster_detection/weights/Squeeze-ernet-92f1score.pt, ernet.pt, ...:
+# torch.save(model) of the reference classes; their ACFF blocks pickle under the legacy
+# path model.ernet.ACFF).  They load with torch.load(weights_only=True): the restricted
+# unpickler only builds the allowlisted globals below -- these empty nn.Module stand-ins
+# for the reference classes plus plain torch.nn layers -- and runs no code from the file.
+class _PickledACFF(torch.nn.Module):
+    """Stand-in for the pickled model.ernet.ACFF / model.acff.ACFF (acff.py:8)."""
+
+
+class _PickledSqueezeErNET(torch.nn.Module):
+    """Stand-in for model.squeeze_ernet.Squeeze_ErNET (squeeze_ernet.py:7)."""
+
+
+class _PickledSqueezeRedConv(torch.nn.Module):
+    """Stand-in for model.squeeze_ernet_redconv.Squeeze_RedConv (squeeze_ernet_redconv.py:7)."""
+
+
+class _PickledErNET(torch.nn.Module):
+    """Stand-in for model.ernet.ErNET (ernet.py:6)."""
+
+
+def _pickle_allowlist():
+    import collections
+    nn = torch.nn
+    return [(_PickledACFF, "model.ernet.ACFF"), (_PickledACFF, "model.acff.ACFF"),
+            (_PickledSqueezeErNET, "model.squeeze_ernet.Squeeze_ErNET"),
+            (_PickledSqueezeRedConv, "model.squeeze_ernet_redconv.Squeeze_RedConv"),
+            (_PickledErNET, "model.ernet.ErNET"),
+            nn.Conv2d, nn.BatchNorm2d, nn.LeakyReLU, nn.Dropout, nn.MaxPool2d, nn.AvgPool2d, nn.Linear, nn.Softmax,
+            set, collections.OrderedDict]
+
+
 def read_weights(weights_path: str) -> dict:
-    """State dict from a reference checkpoint: plain state dict or {'model_state_dict': ...}
-    (.pt via torch.load(weights_only=True)), or an .npz of arrays."""
+    """State dict from a reference checkpoint (SURVEY.md §8b "weight inputs"): a plain state
+    dict (weights/*-state_dict.pt), a {'model_state_dict': ...} training checkpoint
+    (train.py:310-321), a full-module pickle (weights/Squeeze-ernet-92f1score.pt etc.,
+    through the allowlist above), or an .npz of arrays.  Every .pt goes through
+    torch.load(weights_only=True)."""
     if not os.path.exists(weights_path):
         raise FileNotFoundError(f"No weights found at {weights_path}")
     if weights_path.endswith(".npz"):
         z = np.load(weights_path, allow_pickle=False)
         return {k: z[k] for k in z.files}
-    ckpt = torch.load(weights_path, map_location="cpu", weights_only=True)
+    with torch.serialization.safe_globals(_pickle_allowlist()):
+        ckpt = torch.load(weights_path, map_location="cpu", weights_only=True)
+    if isinstance(ckpt, torch.nn.Module):
+        return {k: v for k, v in ckpt.state_dict().items() if not k.endswith("num_batches_tracked")}
     if isinstance(ckpt, dict) and "model_state_dict" in ckpt:
         return ckpt["model_state_dict"]
     return ckpt

@@ -129,3 +129,19 @@ def labels_to_letterbox(x: np.ndarray, ratio, pad, h: int, w: int, out_h: int, o
     lab[:, [2, 4]] /= out_h
     lab[:, [1, 3]] /= out_w
     return lab
+
+
+def resize_linear(frames: torch.Tensor, out_h: int, out_w: int, swap_rb: bool = False, stream=None) -> torch.Tensor:
+    """cv2.resize(frame, (out_w, out_h)) with the default INTER_LINEAR, on the device
+    (rtdm_resize_linear; real-time-inference.py:185).  frames: uint8 [N,H,W,3] (or [H,W,3])
+    CUDA; swap_rb=True also turns BGR into RGB.  Returns uint8 [N,out_h,out_w,3]."""
+    if not frames.is_cuda or frames.dtype != torch.uint8 or frames.shape[-1] != 3:
+        raise ValueError("frames must be uint8 [N,H,W,3] on the GPU")
+    one = frames.dim() == 3
+    x = (frames[None] if one else frames).contiguous()
+    n, h, w, _ = x.shape
+    out = torch.empty((n, out_h, out_w, 3), dtype=torch.uint8, device=x.device)
+    with torch.cuda.device(x.device):
+        L.check(L.lib().rtdm_resize_linear(L.ptr(x), n, h, w, w * 3, out_h, out_w, 1 if swap_rb else 0, L.ptr(out),
+                                           L.stream_ptr(stream)))
+    return out[0] if one else out

@@ -144,3 +144,36 @@ def test_detect_cli_matches_oracle(tmp_path):
     rows = res[str(tmp_path / "src" / "a.png")]
     n_ref = 0 if ref is None else len(ref)
     assert abs(len(rows) - n_ref) <= max(1, n_ref // 20)
+
+
+@pytest.mark.gpu
+def test_real_time_inference_cli_matches_oracle(tmp_path, cls_weights):
+    """real-time-inference.py: cv2.resize(frame, (640, 480)) INTER_LINEAR restated on the
+    device (bit-exact with oracle/letterbox.py resize_linear), then the classifier; class
+    names and confidences equal the oracle's (resize -> CLI transform -> model, double
+    softmax, real-time-inference.py:80-107)."""
+    from oracle import letterbox as OL
+    from rtdm.classifier import CLASSES
+    from rtdm.letterbox import resize_linear
+    from rtdm.synth import synth_frames
+    cli = _load_cli("real-time-inference")
+    name = "squeeze-ernet"
+    sd = cls_weights[name]
+    wpath = tmp_path / "w.pt"
+    torch.save({k: torch.from_numpy(v) for k, v in sd.items()}, wpath)
+    os.makedirs(tmp_path / "v")
+    imgs = [synth_frames(1, h, w, seed=500 + i)[0] for i, (h, w) in enumerate([(720, 1280), (480, 640), (300, 451),
+                                                                               (97, 133)])]
+    for i, im in enumerate(imgs):
+        _write_png(tmp_path / "v" / f"{i:03d}.png", im)
+    # the device resize alone, up and down, both interpolation directions
+    for im in imgs:
+        for (oh, ow) in ((480, 640), (240, 320), (512, 1000)):
+            got = resize_linear(torch.from_numpy(im).cuda(), oh, ow).cpu().numpy()
+            assert np.array_equal(got, OL.resize_linear(im, ow, oh)), (im.shape, oh, ow)
+    results, fps = cli.main(["--model", name, "--weights", str(wpath), "--video", str(tmp_path / "v"),
+                             "--width", "640", "--height", "480"])
+    cls, conf = _cls_oracle(name, sd, [OL.resize_linear(im, 640, 480) for im in imgs])
+    assert [r[0] for r in results] == [CLASSES[c] for c in cls]
+    assert np.allclose([r[1] for r in results], conf, atol=1e-3)
+    assert len(fps) == len(imgs)

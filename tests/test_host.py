@@ -100,7 +100,25 @@ def _dist_worker(rank, world, port, q):
         frames = synth_frames(c, 32, 32, first=s)
         rec = {"sum": torch.tensor([float(frames.sum())]), "rank": torch.tensor([rank])}
         out = gather_results(rec)
+        # bench.py's per-step gather: one flat record per rank (float fields + int32 bit
+        # patterns), unpacked on rank 0
+        from rtdm.distributed import gather_records
+        from rtdm.pipeline import TwoStagePipeline, unpack_record
+        pipe = TwoStagePipeline(None, None, max_det=7)
+        lay, total_len = pipe.record_layout(c)
+        mine = unpack_record(torch.zeros(total_len), pipe, c)
+        mine["logits"][:] = torch.arange(c * 5, dtype=torch.float32).view(c, 5) + 100 * rank
+        mine["det"][:] = float(rank) + 0.5
+        mine["idx"][:] = torch.arange(c * 7 * 2, dtype=torch.int32).view(c, 7, 2) - rank
+        mine["count"][:] = torch.arange(s, s + c, dtype=torch.int32)
+        allrec = gather_records(mine["record"])
         if rank == 0:
+            for r in range(world):
+                u = unpack_record(allrec[r], pipe, c)
+                ok = ok and torch.equal(u["logits"], torch.arange(c * 5, dtype=torch.float32).view(c, 5) + 100 * r)
+                ok = ok and bool((u["det"] == float(r) + 0.5).all())
+                ok = ok and torch.equal(u["idx"], torch.arange(c * 14, dtype=torch.int32).view(c, 7, 2) - r)
+                ok = ok and torch.equal(u["count"], torch.arange(r * c, r * c + c, dtype=torch.int32))
             total = sum(float(t.item()) for t in out["sum"])
             q.put((ok, total, [int(t.item()) for t in out["rank"]]))
         else:
@@ -157,3 +175,35 @@ def test_yolo_acff_stream_from_reference_state_dict():
     assert np.array_equal(state_dict_to_stream(text, sd), stream)
     assert Darknet(text, (416, 416)).info.weight_floats == stream.size
 
+
+
+REF_WEIGHTS = "/root/reference/code/disaster_detection/weights"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_WEIGHTS), reason="reference checkpoints not present")
+@pytest.mark.parametrize("model,pickle_name", [("squeeze-ernet", "Squeeze-ernet-92f1score.pt"),
+                                               ("squeeze-redconv", "Squeeze-ernet-redconv92acc.pt"),
+                                               ("ernet", "ernet-96f1scor.pt")])
+def test_full_module_pickle_loads_allowlisted(model, pickle_name, cls_weights):
+    """The reference's full-module pickles load through torch.load(weights_only=True) with
+    the allowlist (no code from the file runs) and give the same tensors as the state-dict
+    checkpoints (*-state_dict.pt are bit-identical to these)."""
+    from rtdm.classifier import build_model, read_weights
+    sd = read_weights(os.path.join(REF_WEIGHTS, pickle_name))
+    ref = cls_weights[model]
+    assert set(sd) == set(ref)
+    for k in ref:
+        assert np.array_equal(sd[k].numpy(), ref[k]), k
+    build_model(model).load_state_dict(sd)  # strict key / shape check
+
+
+def test_read_weights_checkpoint_formats(tmp_path, cls_weights):
+    """Plain state dict, {'model_state_dict': ...} and .npz all give the same tensors."""
+    from rtdm.classifier import read_weights
+    sd = {k: torch.from_numpy(v) for k, v in cls_weights["ernet"].items()}
+    torch.save(sd, tmp_path / "a.pt")
+    torch.save({"model_state_dict": sd, "epoch": 3}, tmp_path / "b.pt")
+    np.savez(tmp_path / "c.npz", **cls_weights["ernet"])
+    for f in ("a.pt", "b.pt", "c.npz"):
+        got = read_weights(str(tmp_path / f))
+        assert all(np.array_equal(np.asarray(got[k]), cls_weights["ernet"][k]) for k in cls_weights["ernet"]), f
