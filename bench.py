@@ -67,12 +67,17 @@ def parse():
     ap.add_argument("--conf", type=float, default=0.3)
     ap.add_argument("--iou", type=float, default=0.4)
     ap.add_argument("--max-det", type=int, default=300)
-    ap.add_argument("--overlap", type=int, default=1,
-                    help="1: classifier on a side stream beside the detector; 0: both stages serial")
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="1: classifier on a side stream beside the detector; 0: both stages on the batch's stream")
     ap.add_argument("--priority", type=int, default=0,
                     help="1: detector + NMS on a high-priority stream, classifier on a low-priority one")
+    ap.add_argument("--det-streams", type=int, default=1, help="detector head branches on a side stream (2) or not (1)")
     ap.add_argument("--graphs", type=int, default=1, help="1: replay each step as a hipGraph; 0: eager launches")
     ap.add_argument("--rotate", type=int, default=4, help="distinct frame batches the steps cycle over")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="batches in flight per GPU (0: 3 for <= 16 frames per GPU, else 2): step k runs on "
+                         "pipeline k %% inflight (own handles, buffers and ONE stream), so consecutive batches "
+                         "run concurrently and fill the CUs one batch's low-occupancy kernels leave idle")
     ap.add_argument("--roofline-steps", type=int, default=20,
                     help="eager steps with per-launch hipEvents after the timed region (0: no roofline)")
     ap.add_argument("--h2d-steps", type=int, default=20, help="PCIe-inclusive steps (0: skip)")
@@ -110,6 +115,8 @@ def build(args, world, rank):
     from rtdm.synth import classifier_param_shapes, inline_acff, load_calibration, synth_acff_params, \
         synth_darknet_weights
 
+    from rtdm import _lib as L
+    L.check(L.lib().rtdm_set_tuning(b"two_streams", 1 if args.det_streams > 1 else 0))
     cfg_path = os.path.join(ROOT, "real-time-disaster-management_amd", "rtdm", "cfg", args.cfg + ".cfg")
     text = open(cfg_path).read()
     det = Darknet(text, (args.img, args.img))
@@ -132,9 +139,18 @@ def build(args, world, rank):
     if args.dtype == "f16":
         det.half()
         cls.half()
-    pipe = TwoStagePipeline(cls, det, args.conf, args.iou, args.max_det, overlap=bool(args.overlap),
-                            priority=bool(args.priority), graphs=bool(args.graphs))
-    return pipe, det, cls, text, stream, sd
+    pipes = []
+    for j in range(args.inflight):
+        if j:  # another instance: own device weights, arenas, buffers and streams
+            det, cls = Darknet(text, (args.img, args.img)), build_model(args.classifier)
+            det.load_weight_stream(stream)
+            cls.load_state_dict(sd)
+            if args.dtype == "f16":
+                det.half()
+                cls.half()
+        pipes.append(TwoStagePipeline(cls, det, args.conf, args.iou, args.max_det, overlap=bool(args.overlap),
+                                      priority=bool(args.priority), graphs=bool(args.graphs)))
+    return pipes, text, stream, sd
 
 
 def step_table(det, n):
@@ -157,7 +173,6 @@ def pmc_traffic(kernel, per_gpu_batch):
     from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench command;
     FETCH_SIZE doubled per the gfx950 correction).  None when no pass covers it."""
     import glob
-    base = kernel.split("<")[0]
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))  # tags sort by round
     for path in reversed(files):
         try:
@@ -169,7 +184,7 @@ def pmc_traffic(kernel, per_gpu_batch):
         for k, t in d.items():
             if k.startswith("_") or not isinstance(t, dict):
                 continue
-            if k.split("<")[0] == base and "fetch_size_bytes_avg" in t and "write_size_bytes_avg" in t:
+            if k == kernel and "fetch_size_bytes_avg" in t and "write_size_bytes_avg" in t:
                 return {"bytes_per_launch": t["hbm_bytes_avg"], "source": os.path.relpath(path, ROOT)}
     return None
 
@@ -249,16 +264,29 @@ def main():
     if global_batch % world:
         raise SystemExit(f"global batch {global_batch} does not shard evenly over {world} ranks")
     first, b = shard_range(global_batch, world, rank)
-    pipe, det, cls, text, stream, sd = build(args, world, rank)
+    if args.inflight <= 0:
+        # measured on MI355X (profiles/r02k_*): b8 1 / 2 / 3 / 4 in flight 18.5k / 21.6k / 24.2k / 21.2k
+        # frames/s; b64 1 / 2 / 3: 37.3k / 41.4k / 40.6k.  GPU_MAX_HW_QUEUES is 4: one hardware
+        # queue per in-flight batch, plus RCCL's
+        args.inflight = 3 if b <= 16 else 2
+    pipes, text, stream, sd = build(args, world, rank)
+    pipe, det = pipes[0], pipes[0].detector
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in pipes[1:]]
     frames = make_frames(args, first, b, dev)
     rec_len = pipe.record_layout(b)[1]
     gathered = torch.empty((world, rec_len), device=dev, dtype=torch.float32) if world > 1 and rank == 0 else None
     torch.cuda.synchronize()
 
-    def step(k):
-        out = pipe(frames[k % len(frames)])
-        if world > 1:
-            gather_records(out["record"], gathered if rank == 0 else None)
+    def step(k, ev=None):
+        j = k % len(pipes)
+        with torch.cuda.stream(streams[j]):
+            if ev is not None:
+                ev[0].record()
+            out = pipes[j](frames[k % len(frames)])
+            if world > 1:
+                gather_records(out["record"], gathered if rank == 0 else None)
+            if ev is not None:
+                ev[1].record()
         return out
 
     for k in range(args.warmup):
@@ -270,9 +298,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        evs[k][0].record()
-        out = step(k)
-        evs[k][1].record()
+        out = step(k, evs[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -336,6 +362,7 @@ def main():
         for k in range(2):
             dst.copy_(host[k % len(host)], non_blocking=True)
             pipe(dst)
+        torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -371,9 +398,9 @@ def main():
                    "global_batch": global_batch, "per_gpu_batch": b, "img": args.img,
                    "parallelism": f"dp{world}: frame-sharded global batch"
                                   + (", per-step RCCL gather of every rank's results to rank 0" if world > 1 else ""),
-                   "graphs": bool(args.graphs)},
-        "step_ms_median": round(statistics.median(step_ms), 4),
-        "step_ms_p90": round(sorted(step_ms)[int(0.9 * (len(step_ms) - 1))], 4),
+                   "graphs": bool(args.graphs), "inflight": len(pipes)},
+        "step_latency_ms_median": round(statistics.median(step_ms), 4),
+        "step_latency_ms_p90": round(sorted(step_ms)[int(0.9 * (len(step_ms) - 1))], 4),
         "roofline": rl,
         "pipeline": {"flop_per_frame": pipe_flop,
                      "pipeline_tflops": round(pipe_flop * value / world / 1e12, 2),

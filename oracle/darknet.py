@@ -83,7 +83,7 @@ class DarknetRef:
         assert ptr == stream.size, (ptr, stream.size)
 
     @torch.no_grad()
-    def forward(self, x: torch.Tensor, keep_layers=False, raw=False, f16_storage=False):
+    def forward(self, x: torch.Tensor, keep_layers=False, raw=False, f16_storage=False, conv_hook=None):
         """x: [N,3,H,W] fp32 in [0,1] -> io [N, sum(A*ny*nx), 5+nc] (and per-layer outputs).
         raw=True: the undecoded p rows instead (YOLOLayer training branch, models.py:240-250).
 
@@ -92,7 +92,10 @@ class DarknetRef:
         activation in fp16 too): BN folded into the conv weights (eps 1e-4), weights and the
         input rounded to fp16, fp32 arithmetic, every layer output rounded to fp16 except the
         raw head maps (decoded in fp32).  The fp16 parity tests bound the HIP fp16 io's
-        deviation from the fp32 oracle by a small multiple of this mode's own deviation."""
+        deviation from the fp32 oracle by a small multiple of this mode's own deviation.
+
+        conv_hook(i, x, w, b) -> (x, w, b): test-only hook on each [convolutional] layer's
+        input and BN-folded weights (f16_storage mode), e.g. to model int8 quantisation."""
         h16 = (lambda t: t.half().float()) if f16_storage else (lambda t: t)
         img_size = x.shape[-2:]
         x = h16(x)
@@ -111,7 +114,10 @@ class DarknetRef:
                         sc = p["gamma"].double() / torch.sqrt(p["var"].double() + 1e-4)
                         w = w * sc.view(-1, 1, 1, 1)
                         b = (p["beta"].double() - p["mean"].double() * sc).float()
-                    x = F.conv2d(x, h16(w.float()), b, s, pad)
+                    w = h16(w.float())
+                    if conv_hook is not None:
+                        x, w, b = conv_hook(i, x, w, b)
+                    x = F.conv2d(x, w, b, s, pad)
                 else:
                     x = F.conv2d(x, p["w"], p.get("bias"), s, pad)
                     if "gamma" in p:

@@ -36,11 +36,17 @@ def class_mask(classes) -> int:
     return m
 
 
+def workspace_bytes(n, n_anchors, nc) -> int:
+    return int(L.lib().rtdm_nms_workspace_size(n, n_anchors, nc))
+
+
 def nms_batched(prediction: torch.Tensor, conf_thres: float = 0.1, iou_thres: float = 0.6, multi_label: bool = True,
-                classes=None, agnostic: bool = False, max_det: int = 300, out=None, stream=None):
+                classes=None, agnostic: bool = False, max_det: int = 300, out=None, stream=None, workspace=None):
     """prediction: io [N, A, 5+nc] fp32 CUDA.  Returns (det [N,max_det,6], idx [N,max_det,2] int32
     (anchor row, class), count [N] int32 = survivors per image; rows >= min(count, max_det) are
-    undefined).  No host synchronisation."""
+    undefined).  No host synchronisation.  workspace: a caller-owned uint8 device buffer of
+    workspace_bytes(...) (callers with work in flight on several streams need their own);
+    default: one shared per device."""
     if prediction.dtype != torch.float32:
         prediction = prediction.float()
     prediction = prediction.contiguous()
@@ -53,7 +59,12 @@ def nms_batched(prediction: torch.Tensor, conf_thres: float = 0.1, iou_thres: fl
     else:
         det, idx, count = out
     with torch.cuda.device(dev):
-        ws, need = _workspace(dev, n, a, no - 5)
+        if workspace is not None:
+            ws, need = workspace, workspace_bytes(n, a, no - 5)
+            if ws.numel() < need:
+                raise ValueError(f"nms workspace has {ws.numel()} bytes, needs {need}")
+        else:
+            ws, need = _workspace(dev, n, a, no - 5)
         L.check(L.lib().rtdm_nms(L.ptr(prediction), n, a, no, float(conf_thres), float(iou_thres),
                                  1 if multi_label else 0, 1 if agnostic else 0, class_mask(classes), int(max_det),
                                  L.ptr(ws), need, L.ptr(det), L.ptr(idx), L.ptr(count), L.stream_ptr(stream)))

@@ -17,7 +17,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib as L
-from .nms import nms_batched
+from .nms import nms_batched, workspace_bytes
 
 
 def unpack_record(flat: torch.Tensor, pipe, n: int) -> dict:
@@ -95,6 +95,9 @@ class TwoStagePipeline:
         if b is None:
             b = unpack_record(torch.empty(self.record_layout(n)[1], device=device, dtype=torch.float32), self, n)
             b["io"] = torch.empty((n, self.detector.n_anchors, self.detector.no), device=device, dtype=torch.float32)
+            # NMS scratch of this pipeline alone: pipelines may run on several streams at once
+            b["ws"] = torch.empty(workspace_bytes(n, self.detector.n_anchors, self.detector.no - 5), device=device,
+                                  dtype=torch.uint8)
             self._bufs[key] = b
         return b
 
@@ -127,12 +130,10 @@ class TwoStagePipeline:
         return self._buffers(n, frames.device)
 
     def _graph_key(self, frames):
-        from .nms import _workspace
         n = frames.shape[0]
         hc = self.classifier._get_handle(n)
         hd = self.detector.handle(n)
-        ws, _ = _workspace(frames.device, n, self.detector.n_anchors, self.detector.no - 5)
-        return (n, frames.data_ptr(), tuple(frames.shape), str(frames.device), hc.value, hd.value, ws.data_ptr())
+        return (n, frames.data_ptr(), tuple(frames.shape), str(frames.device), hc.value, hd.value)
 
     def _launch(self, frames: torch.Tensor, stream=None) -> dict:
         n = frames.shape[0]
@@ -156,7 +157,7 @@ class TwoStagePipeline:
             L.check(L.lib().rtdm_detect(hd, L.ptr(frames), L.RTDM_INPUT_FRAME_U8, n, L.ptr(b["io"]),
                                         L.stream_ptr(crit)))
             nms_batched(b["io"], self.conf_thres, self.iou_thres, self.multi_label, None, self.agnostic,
-                        self.max_det, out=(b["det"], b["idx"], b["count"]), stream=crit)
+                        self.max_det, out=(b["det"], b["idx"], b["count"]), stream=crit, workspace=b["ws"])
             crit_done.record(crit)
             main.wait_event(joined)
             main.wait_event(crit_done)

@@ -53,14 +53,14 @@ def _detector(cfg, size, half=True):
     return m, text, conv, acff
 
 
-def _pipeline(cls_weights, graphs=False):
+def _pipeline(cls_weights, graphs=False, overlap=True):
     from rtdm.classifier import build_model
     from rtdm.pipeline import TwoStagePipeline
     cls = build_model("ernet")
     cls.load_state_dict(cls_weights["ernet"])
     cls.half()
     det, text, conv, acff = _detector(CFG, IMG)
-    return TwoStagePipeline(cls, det, 0.3, 0.4, max_det=300, graphs=graphs), text, conv, acff
+    return TwoStagePipeline(cls, det, 0.3, 0.4, max_det=300, graphs=graphs, overlap=overlap), text, conv, acff
 
 
 def _host(out, rows=None):
@@ -118,6 +118,24 @@ def test_bench_config_batches_graph_and_oracle(dev, cls_weights):
     _same(g, b64, "graph replay")
     g8 = _host(pg(x[8:16].contiguous()))
     _same(g8, _host(b64, slice(8, 16)), "graph replay b8")
+    # bench.py's throughput configuration: one stream per batch (classifier and detector
+    # serial, no detector side stream), two batches in flight on two streams
+    from rtdm import _lib as L
+    L.check(L.lib().rtdm_set_tuning(b"two_streams", 0))
+    try:
+        ps = [_pipeline(cls_weights, graphs=True, overlap=False)[0] for _ in range(2)]
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"two_streams", 1))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for rep in range(2):  # capture, then replay with both batches in flight
+        outs = []
+        for j in range(2):
+            with torch.cuda.stream(streams[j]):
+                outs.append(ps[j](x[32 * j:32 * j + 32].contiguous()))
+        torch.cuda.synchronize()
+    for j in range(2):
+        _same(_host(outs[j]), _host(b64, slice(32 * j, 32 * j + 32)), f"in-flight single-stream batch {j}")
 
     # oracle: classifier on 8 frames --------------------------------------------------
     pick = [0, 9, 18, 27, 36, 45, 54, 63]
