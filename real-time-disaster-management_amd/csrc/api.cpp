@@ -33,6 +33,8 @@ rtdm_status rtdm_set_tuning(const char* key, int value) {
     RTDM_REQUIRE(key, RTDM_E_INVALID, "set_tuning: NULL key");
     if (!strcmp(key, "conv_pipe"))
       set_conv_pipe_mode(value);
+    else if (!strcmp(key, "conv_pipe_korder"))
+      set_pipe_korder(value);
     else if (!strcmp(key, "conv_pipe_bm"))
       set_pipe_bm(value);
     else if (!strcmp(key, "fuse_head"))

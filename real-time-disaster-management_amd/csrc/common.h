@@ -167,6 +167,7 @@ struct ConvArgs {
   const void* zero = nullptr;    // >= 16 zero bytes in device memory (glds padding source)
   FastDiv fd_cin;                // set by conv_set_rows
   int glds_uni = 0;              // conv_glds_f16: uniform-tap staging (set by launch_conv)
+  int pipe_corder = 0;           // conv_pipe_f16: channel-block-outer K order (set by launch_conv_pipe)
   Epilogue e;
   // Fused YOLO head (conv_pipe_f16 only): a 1x1 conv over this conv's activated
   // output (cout <= 128 = one N tile), head_w fp16 [head_cout_pad][cout_pad] (k = c),
@@ -196,6 +197,7 @@ void launch_conv_pipe(const ConvArgs& a, hipStream_t s);
 int conv_pipe_mode();
 int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 / 128 / 64)
 void set_pipe_bm(int v);                  // 0 = cost model, else forced
+void set_pipe_korder(int v);              // conv_pipe K order: 0 tap outer, 1 channel-block outer
 const char* conv_pipe_name(const ConvArgs& a);  // kernel symbol of that launch
 // diagnostics: conv_stem3 ablation builds (tools/ab_conv.py --key stem_abl)
 int stem_abl();

@@ -177,7 +177,8 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       (void*)((const _Float16*)a.w + (size_t)n_base * a.kpad), 0, BN * a.kpad * 2, 0x00020000);
   const int nk = a.kpad / BK;
   const int cpt = a.cin / BK;  // K-blocks per tap
-  int st_tap = 0, st_c = 0, st_buf = 0, st_kb = 0;
+  const int ntap = a.ks * a.ks;
+  int st_tap = 0, st_c = 0, st_buf = 0;
 
   // Issue the VM buffer->LDS ops of the next K-block (cursor st_*) into stage st_buf.
   auto stage = [&]() {
@@ -190,15 +191,20 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       const int vo = ((vmask[j] >> st_tap) & 1u) ? voff_a[j] + tapoff : (int)0x80000000;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(As + 8 * (NA * wid + j) * BK), 16, vo, 0, 0, 0);
     }
+    const int koff = (st_tap * a.cin + st_c * BK) * 2;  // weight column of this K-block (tap-major packing)
 #pragma unroll
     for (int j = 0; j < NB; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j],
-                                               st_kb * BK * 2, 0, 0);
-    if (++st_c == cpt) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j], koff,
+                                               0, 0);
+    if (a.pipe_corder) {  // channel-block outer: the taps of one 64-channel slice back to back
+      if (++st_tap == ntap) {
+        st_tap = 0;
+        ++st_c;
+      }
+    } else if (++st_c == cpt) {  // tap outer
       st_c = 0;
       ++st_tap;
     }
-    ++st_kb;
     st_buf = st_buf == kPNS - 1 ? 0 : st_buf + 1;
   };
 
@@ -522,7 +528,17 @@ const char* conv_pipe_name(const ConvArgs& a) {
   return bm == 256 ? "conv_pipe_f16<0,256>" : bm == 128 ? "conv_pipe_f16<0,128>" : "conv_pipe_f16<0,64>";
 }
 
-void launch_conv_pipe(const ConvArgs& a, hipStream_t s) {
+// K order of the implicit GEMM: 0 = tap outer (each tap's whole channel run), 1 = 64-channel
+// block outer (the 9 taps of one channel slice back to back, so the shifted input rows
+// a tap re-reads are the slice's: an L2 working set of 1/(cin/64) of the tap-outer one).
+// rtdm_set_tuning("conv_pipe_korder", v).  Changes the fp32 summation order (not batch
+// invariance): results differ from the other order in the last bits.
+static int g_pipe_korder = 1;
+void set_pipe_korder(int v) { g_pipe_korder = v ? 1 : 0; }
+
+void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
+  ConvArgs a = a_in;
+  a.pipe_corder = g_pipe_korder && a.ks == 3 ? 1 : 0;
   const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
   const int64_t nt = (int64_t)((a.M + bm - 1) / bm) * (a.cout_pad / kPBN);
   RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
