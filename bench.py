@@ -48,7 +48,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "real-time-disaster-management_amd"))
 
 MFMA_F16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/fp16
-CLASSIFIER_FLOP = {"squeeze-ernet": 90953544.0, "squeeze-redconv": 77593080.0, "ernet": 319307650.0}
+CLASSIFIER_FLOP = {"squeeze-ernet": 90953544.0, "squeeze-redconv": 77593080.0, "ernet": 319307650.0, "none": 0.0}
 METRIC = "frames/sec two-stage (ErNET→YOLOv4) 608×608 b64 @1/2/4/8 GPU; top-1/mAP parity"
 
 
@@ -62,7 +62,8 @@ def parse():
                     help="> 0: frames per GPU per step instead (weak scaling; global = this * N)")
     ap.add_argument("--img", type=int, default=608)
     ap.add_argument("--cfg", default="yolov4-tiny-aider-416")
-    ap.add_argument("--classifier", default="ernet", choices=["ernet", "squeeze-ernet", "squeeze-redconv"])
+    ap.add_argument("--classifier", default="ernet", choices=["ernet", "squeeze-ernet", "squeeze-redconv", "none"],
+                    help="none: detection only (BASELINE config 3)")
     ap.add_argument("--dtype", default="f16", choices=["f16", "f32"])
     ap.add_argument("--conf", type=float, default=0.3)
     ap.add_argument("--iou", type=float, default=0.4)
@@ -120,34 +121,39 @@ def build(args, world, rank):
     cfg_path = os.path.join(ROOT, "real-time-disaster-management_amd", "rtdm", "cfg", args.cfg + ".cfg")
     text = open(cfg_path).read()
     det = Darknet(text, (args.img, args.img))
-    cls = build_model(args.classifier)
+    use_cls = args.classifier != "none"
+    cls = build_model(args.classifier) if use_cls else None
     # rank 0 makes / loads the weights; RCCL broadcast to the other ranks (once, untimed)
     if rank == 0:
         calib = load_calibration(args.cfg)
         conv, acff = synth_darknet_weights(text, calib=calib), synth_acff_params(text, calib=calib)
         stream = inline_acff(text, conv, acff)  # YOLO-ACFF cfgs: [acff] params inline
         args.ref_weights = (conv, acff)         # the CPU oracle takes them apart
-        sd = trained_classifier(args.classifier)
+        sd = trained_classifier(args.classifier) if use_cls else {}
     else:
         stream, sd = None, None
     if world > 1:
         from rtdm.distributed import broadcast_array, broadcast_state_dict
         stream = broadcast_array(stream)
-        sd = broadcast_state_dict(sd, classifier_param_shapes(args.classifier))
+        sd = broadcast_state_dict(sd, classifier_param_shapes(args.classifier)) if use_cls else {}
     det.load_weight_stream(stream)
-    cls.load_state_dict(sd)
+    if use_cls:
+        cls.load_state_dict(sd)
     if args.dtype == "f16":
         det.half()
-        cls.half()
+        if use_cls:
+            cls.half()
     pipes = []
     for j in range(args.inflight):
         if j:  # another instance: own device weights, arenas, buffers and streams
-            det, cls = Darknet(text, (args.img, args.img)), build_model(args.classifier)
+            det, cls = Darknet(text, (args.img, args.img)), (build_model(args.classifier) if use_cls else None)
             det.load_weight_stream(stream)
-            cls.load_state_dict(sd)
+            if use_cls:
+                cls.load_state_dict(sd)
             if args.dtype == "f16":
                 det.half()
-                cls.half()
+                if use_cls:
+                    cls.half()
         pipes.append(TwoStagePipeline(cls, det, args.conf, args.iou, args.max_det, overlap=bool(args.overlap),
                                       priority=bool(args.priority), graphs=bool(args.graphs)))
     return pipes, text, stream, sd
@@ -216,9 +222,10 @@ def cpu_baseline(args, text, stream, sd):
     sdt = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in sd.items()}
 
     def run(frames):
-        x = torch.from_numpy(np.stack([OP.cli_transform(f, s) for f in frames]))
         with torch.no_grad():
-            OC.forward(args.classifier, sdt, x)
+            if args.classifier != "none":
+                x = torch.from_numpy(np.stack([OP.cli_transform(f, s) for f in frames]))
+                OC.forward(args.classifier, sdt, x)
             io = ref.forward(torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0)
         ON.non_max_suppression(io.numpy(), args.conf, args.iou)
 
@@ -392,9 +399,10 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": "f16" if args.dtype == "f16" else "f32",
         "data": f"synthetic {args.img}x{args.img} uint8 frames (seeded, {len(frames)} rotations), synthetic "
-                f"calibrated detector weights, the reference's trained {args.classifier} weights",
-        "config": {"workload": f"two-stage {args.classifier} -> {args.cfg}@{args.img} + decode + NMS "
-                               f"(conf {args.conf}, iou {args.iou})",
+                f"calibrated detector weights"
+                + (f", the reference's trained {args.classifier} weights" if args.classifier != "none" else ""),
+        "config": {"workload": (f"two-stage {args.classifier} -> " if args.classifier != "none" else "detection only: ")
+                               + f"{args.cfg}@{args.img} + decode + NMS (conf {args.conf}, iou {args.iou})",
                    "global_batch": global_batch, "per_gpu_batch": b, "img": args.img,
                    "parallelism": f"dp{world}: frame-sharded global batch"
                                   + (", per-step RCCL gather of every rank's results to rank 0" if world > 1 else ""),

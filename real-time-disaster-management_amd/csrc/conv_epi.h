@@ -253,6 +253,9 @@ __device__ __forceinline__ void epi_vec8(const ConvArgs& a, int m0, int c0, cons
 // residual, swish or YOLO decode paths: the generic epilogue compiles to ~7k
 // instructions, and fetching them cold at every tile's end cost ~10 us per tile
 // round in the MFMA-bound convs (tools/ab_conv.py modes 8-10).
+// RES: the fused shortcut add (weightedFeatureFusion, models.py:135-155) of a same-shape
+// 8-aligned residual view, in epi_vec8's order (act -> affine -> + residual).
+template <bool RES = false>
 __device__ __forceinline__ void epi_vec8_lean(const ConvArgs& a, int m0, int c0, const float (&v)[4][8],
                                               const float (&bias)[8], const float (&sc)[8], const float (&sh)[8]) {
   const Epilogue& e = a.e;
@@ -269,12 +272,15 @@ __device__ __forceinline__ void epi_vec8_lean(const ConvArgs& a, int m0, int c0,
     int n, oy, ox;
     row_pix4(a, m0, r, pn, poy, pox, n, oy, ox);
     const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
+    h8v rv;
+    if constexpr (RES) rv = *(const h8v*)((const _Float16*)e.res.ptr + pix * e.res.cs + e.res.co + c0);
     h8v hv;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = v[r][j] + bias[j];
       t = leaky ? (t > 0.f ? t : t * e.slope) : t;
       t = t * sc[j] + sh[j];
+      if constexpr (RES) t += (float)rv[j];
       hv[j] = (_Float16)t;
       pmax[j] = fmaxf(pmax[j], t);
     }
@@ -355,9 +361,11 @@ inline bool epi_io_ok(const ConvArgs& a) {
          (e.act == ACT_LEAKY || e.act == ACT_LINEAR) && (!e.scale || e.shift);
 }
 
-inline bool epi_lean_ok(const ConvArgs& a) {
+inline bool epi_lean_ok(const ConvArgs& a, bool allow_res = false) {
   const Epilogue& e = a.e;
-  if (e.res.ptr || e.io || (e.act != ACT_LEAKY && e.act != ACT_LINEAR) || a.cout % 8 != 0) return false;
+  if ((e.res.ptr && (!allow_res || ((e.res.cs | e.res.co) & 7) != 0)) || e.io ||
+      (e.act != ACT_LEAKY && e.act != ACT_LINEAR) || a.cout % 8 != 0)
+    return false;
   if (!e.bias || (e.scale && !e.shift)) return false;
   for (const View* v : {&e.full, &e.pool, &e.up})
     if (v->ptr && ((v->cs | v->co) & 7) != 0) return false;

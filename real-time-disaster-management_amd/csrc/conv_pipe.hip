@@ -91,7 +91,8 @@ __device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v
 // 1 = no buffer->LDS loads in the K-loop, 2 = no fragment ds_reads in the K-loop,
 // 4 = no wait + barrier in the K-loop, 16 = no epilogue (one guarded store keeps the
 // MFMAs live), 32 = no K-loop (prologue + epilogue only).  Bit 8 (not an ablation):
-// fused YOLO head; bit 128 (not an ablation): lean epilogue (epi_vec8_lean).
+// fused YOLO head; bit 128 (not an ablation): lean epilogue (epi_vec8_lean); bit 256 with
+// 128: lean epilogue with the fused shortcut add.
 // One BM x 128 output tile (logical tile index bid, M-major over N tiles).
 template <int ABL, int BM>
 __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem_raw, int bid) {
@@ -428,7 +429,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[r][j] = Cs[(q * 4 + r) * kPCstr + gg * 8 + j];
     if constexpr ((ABL & 128) != 0)
-      epi_vec8_lean(a, m0, c0, v, lb, ls, lh);
+      epi_vec8_lean<(ABL & 256) != 0>(a, m0, c0, v, lb, ls, lh);
     else
       epi_vec8(a, m0, c0, v);
   }
@@ -516,6 +517,8 @@ static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 gr
     if constexpr (BM >= 128) hipLaunchKernelGGL((conv_pipe_f16<8, BM>), grid, dim3(512), 0, s, a, ntiles);
   } else if (epi_lean_ok(a)) {
     hipLaunchKernelGGL((conv_pipe_f16<128, BM>), grid, dim3(512), 0, s, a, ntiles);
+  } else if (epi_lean_ok(a, true)) {
+    hipLaunchKernelGGL((conv_pipe_f16<384, BM>), grid, dim3(512), 0, s, a, ntiles);
   } else {
     hipLaunchKernelGGL((conv_pipe_f16<0, BM>), grid, dim3(512), 0, s, a, ntiles);
   }
@@ -525,6 +528,8 @@ const char* conv_pipe_name(const ConvArgs& a) {
   const int bm = pipe_bm(a);
   if (a.head_w) return bm == 256 ? "conv_pipe_f16<8,256>" : "conv_pipe_f16<8,128>";
   if (epi_lean_ok(a)) return bm == 256 ? "conv_pipe_f16<128,256>" : bm == 128 ? "conv_pipe_f16<128,128>" : "conv_pipe_f16<128,64>";
+  if (epi_lean_ok(a, true))
+    return bm == 256 ? "conv_pipe_f16<384,256>" : bm == 128 ? "conv_pipe_f16<384,128>" : "conv_pipe_f16<384,64>";
   return bm == 256 ? "conv_pipe_f16<0,256>" : bm == 128 ? "conv_pipe_f16<0,128>" : "conv_pipe_f16<0,64>";
 }
 

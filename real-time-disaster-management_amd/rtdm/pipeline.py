@@ -131,9 +131,9 @@ class TwoStagePipeline:
 
     def _graph_key(self, frames):
         n = frames.shape[0]
-        hc = self.classifier._get_handle(n)
+        hc = self.classifier._get_handle(n).value if self.classifier is not None else 0
         hd = self.detector.handle(n)
-        return (n, frames.data_ptr(), tuple(frames.shape), str(frames.device), hc.value, hd.value)
+        return (n, frames.data_ptr(), tuple(frames.shape), str(frames.device), hc, hd.value)
 
     def _launch(self, frames: torch.Tensor, stream=None) -> dict:
         n = frames.shape[0]
@@ -148,10 +148,11 @@ class TwoStagePipeline:
             forked.record(main)
             side.wait_event(forked)
             crit.wait_event(forked)
-            hc = self.classifier._get_handle(n)
-            L.check(L.lib().rtdm_classify(hc, L.ptr(frames), L.RTDM_INPUT_FRAME_U8, n, frames.shape[1],
-                                          frames.shape[2], L.ptr(b["logits"]), L.ptr(b["probs"]),
-                                          L.stream_ptr(side)))
+            if self.classifier is not None:  # None: detection only (BASELINE config 3)
+                hc = self.classifier._get_handle(n)
+                L.check(L.lib().rtdm_classify(hc, L.ptr(frames), L.RTDM_INPUT_FRAME_U8, n, frames.shape[1],
+                                              frames.shape[2], L.ptr(b["logits"]), L.ptr(b["probs"]),
+                                              L.stream_ptr(side)))
             joined.record(side)
             hd = self.detector.handle(n)
             L.check(L.lib().rtdm_detect(hd, L.ptr(frames), L.RTDM_INPUT_FRAME_U8, n, L.ptr(b["io"]),

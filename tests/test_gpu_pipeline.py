@@ -206,3 +206,30 @@ def test_pipe_tile_rows_bit_identical(dev, case, bm):
     finally:
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
     assert torch.equal(outs[256], outs[bm])
+
+
+def test_lean_residual_epilogue_bit_identical(dev):
+    """The lean conv_pipe epilogue with the fused shortcut add (Darknet-53 residual
+    blocks, conv_pipe_f16<384,*>) gives the same io bits as the generic epilogue
+    (rtdm_set_tuning("conv_pipe", 11): generic epi_vec8 everywhere, 256-row tiles)."""
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    x = torch.from_numpy(synth_frames(2, 416, 416, seed=23)).to(dev)
+    outs = {}
+    try:
+        for mode in (11, 1):
+            L.check(L.lib().rtdm_set_tuning(b"conv_pipe", mode))
+            m, _, _, _ = _detector("yolov3-aider-416", 416)
+            outs[mode] = m(x)[0].cpu()
+            if mode == 1:
+                h = m.handle(2)
+                names = set()
+                import ctypes
+                for i in range(L.lib().rtdm_detector_num_steps(h)):
+                    nm = ctypes.create_string_buffer(64)
+                    L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, None, None, None))
+                    names.add(nm.value.decode())
+                assert any(n.startswith("conv_pipe_f16<384,") for n in names), names
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe", 1))
+    assert torch.equal(outs[11], outs[1])
