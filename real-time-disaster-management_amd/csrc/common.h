@@ -232,6 +232,12 @@ inline void conv_set_rows(ConvArgs& a) {
 void launch_dw3_acff(const void* in, int in_cs, int in_co, int n, int h, int w, int c, int lim_h, int lim_w,
                      const float* wts /*[3][c][9]*/, const float* bias /*[3][c]*/, void* out /*[n,h-2,w-2,3c]*/,
                      int dtype, hipStream_t s);
+// YOLO-ACFF (models.py:296-302): the three branches ADDED into one [n,h-2,w-2,c] map;
+// wts [27][c] (branch-major taps), bsum [c] = b1 + b2 + b3
+void launch_dw3_sum(const void* in, int in_cs, int in_co, int n, int h, int w, int c, const float* wts,
+                    const float* bsum, void* out, int dtype, hipStream_t s);
+bool dw3_sum_vec_ok(int c, int in_cs, int in_co, int dtype);
+bool dw3_sum_tile_ok(int c, int in_cs, int in_co, int dtype);
 // acff.hip: fused ACFF block (dw3 -> concat -> 1x1 -> LeakyReLU -> BN affine -> opt. 2x2 pool), fp16
 bool acff_fused_ok(int cin, int cout_pad, int kpad);
 void launch_acff_fused(const void* in, int in_cs, int in_co, int n, int h, int w, int cin, int lim_h, int lim_w,

@@ -85,8 +85,8 @@ static std::vector<CfgBlock> parse_cfg(const std::string& text) {
   return defs;
 }
 
-// ST_DW3: an [acff] block's three dilated depthwise branches into a [3C] scratch map
-// (its 1x1 fusion is the ST_CONV after it); ST_RESIZE: the route's nearest resize of the
+// ST_DW3: an [acff] block's three dilated depthwise branches, ADDED (models.py:302), into a
+// [C] scratch map (its 1x1 fusion is the ST_CONV after it); ST_RESIZE: the route's nearest resize of the
 // narrower of two maps (models.py:364-375)
 // ST_ADD: a [shortcut] that cannot ride the previous conv's epilogue (that conv's pre-add
 // output is also routed elsewhere): out = in + res
@@ -115,8 +115,8 @@ struct Step {
   bool quad = false;
   float slope = 0.1f;  // LeakyReLU slope: 0.1 Darknet conv (models.py:40), 0.01 ACFF (:291)
   // [acff] (models.py:46-55, ACFF :265-315): this ST_CONV is the 1x1 fusion over the
-  // ST_DW3 map [b1|b2|b3] with the weights repeated 3x along K (= W (b1+b2+b3)); BN is
-  // the post-activation affine a_bn = [gamma | beta | mean | var], eps 1e-5
+  // ST_DW3 map b1+b2+b3 with the fused_conv weights [F][C]; BN is the post-activation
+  // affine a_bn = [gamma | beta | mean | var], eps 1e-5
   bool acff = false;
   std::vector<float> a_W;
   const float* a_bn = nullptr;
@@ -295,7 +295,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       const int acff_c = cur_c;
       if (is_acff) {
         // three dilated depthwise branches d1p0 / d2p1 / d3p2, each [C, H-2, W-2] (+bias),
-        // written side by side as one [3C] map for the 1x1 fusion conv below
+        // summed into one [C] map for the 1x1 fusion conv below
         RTDM_REQUIRE(d.i("size", 3) == 3, RTDM_E_UNSUPPORTED, "cfg: acff size must be 3");
         RTDM_REQUIRE(cur_h > 2 && cur_w > 2 && cur_t >= 0, RTDM_E_UNSUPPORTED, "cfg: acff input too small");
         Step dw;
@@ -309,12 +309,11 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         dw.ow = cur_w - 2;
         dw.a_dw = take_w(3 * ((int64_t)cur_c * 9 + cur_c));
         h.tensors[cur_t].materialised = true;
-        dw.out_t = new_tensor(3 * cur_c, dw.oh, dw.ow, "acffdw" + std::to_string(i));
+        dw.out_t = new_tensor(cur_c, dw.oh, dw.ow, "acffdw" + std::to_string(i));
         h.tensors[dw.out_t].materialised = true;
         h.flop += 2.0 * dw.oh * dw.ow * 3.0 * cur_c * 9;
         h.steps.push_back(dw);
         cur_t = dw.out_t;
-        cur_c = 3 * cur_c;
         cur_h -= 2;
         cur_w -= 2;
       }
@@ -350,12 +349,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         const float* w1 = take_w((int64_t)filters * acff_c);
         bias = take_w(filters);
         s.a_bn = take_w(4 * (int64_t)filters);
-        if (w1) {
-          s.a_W.resize((size_t)filters * cur_c);
-          for (int o = 0; o < filters; ++o)
-            for (int r = 0; r < 3; ++r)
-              for (int c = 0; c < acff_c; ++c) s.a_W[((size_t)o * 3 + r) * acff_c + c] = w1[(size_t)o * acff_c + c];
-        }
+        if (w1) s.a_W.assign(w1, w1 + (size_t)filters * acff_c);
         s.acff = true;
         s.slope = 0.01f;
       } else {
@@ -705,13 +699,14 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
   h.per_image = off;
   // ---- pack conv weights: MFMA layout iff the input view is 16-byte aligned NHWC ----
   for (Step& st : h.steps) {
-    if (st.kind == ST_DW3 && weights) {  // [3][C][9] taps, [3][C] biases (launch_dw3_acff)
+    if (st.kind == ST_DW3 && weights) {  // [27][C] taps (branch-major), [C] bias sums (launch_dw3_sum)
       const int c = st.cin;
-      std::vector<float> w((size_t)3 * c * 9), b((size_t)3 * c);
+      std::vector<float> w((size_t)27 * c), b((size_t)c, 0.f);
       for (int r = 0; r < 3; ++r) {
-        const float* src = st.a_dw + (size_t)r * (c * 9 + c);
-        std::copy(src, src + (size_t)c * 9, w.begin() + (size_t)r * c * 9);
-        std::copy(src + (size_t)c * 9, src + (size_t)c * 10, b.begin() + (size_t)r * c);
+        const float* src = st.a_dw + (size_t)r * (c * 9 + c);  // conv{r+1}.weight [C][1][3][3], .bias [C]
+        for (int ch = 0; ch < c; ++ch)
+          for (int t = 0; t < 9; ++t) w[(size_t)(r * 9 + t) * c + ch] = src[(size_t)ch * 9 + t];
+        for (int ch = 0; ch < c; ++ch) b[ch] += src[(size_t)c * 9 + ch];  // (b1 + b2) + b3
       }
       st.dw_w_off = blob.add_f32(w);
       st.dw_b_off = blob.add_f32(b);
@@ -973,9 +968,9 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       launch_copy_slice(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, o, h.dtype, s);
     } else if (st.kind == ST_DW3) {
       const View iv = tensor_view(h, st.in_t), ov = tensor_view(h, st.out_t);
-      RTDM_REQUIRE(ov.cs == 3 * st.cin && ov.co == 0, RTDM_E_INVALID, "internal: acff branch map view");
-      launch_dw3_acff(iv.ptr, iv.cs, iv.co, n, st.ih, st.iw, st.cin, st.oh, st.ow, h.blob.at<float>(st.dw_w_off),
-                      h.blob.at<float>(st.dw_b_off), ov.ptr, h.dtype, s);
+      RTDM_REQUIRE(ov.cs == st.cin && ov.co == 0, RTDM_E_INVALID, "internal: acff branch map view");
+      launch_dw3_sum(iv.ptr, iv.cs, iv.co, n, st.ih, st.iw, st.cin, h.blob.at<float>(st.dw_w_off),
+                     h.blob.at<float>(st.dw_b_off), ov.ptr, h.dtype, s);
     } else if (st.kind == ST_ADD) {
       launch_add(tensor_view(h, st.in_t), tensor_view(h, st.res_t), n, st.ih, st.iw, st.cin, tensor_view(h, st.out_t),
                  h.dtype, s);
@@ -1064,9 +1059,12 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     flop = 0;
     bytes = ((double)st.ih * st.iw + (double)st.oh * st.ow) * st.cin * es;
   } else if (st.kind == ST_DW3) {
-    name = "dw3_acff_kernel";
+    const View iv = view_geom(h, st.in_t);
+    const bool vec = dw3_sum_vec_ok(st.cin, iv.cs, iv.co, h.dtype);
+    name = dw3_sum_tile_ok(st.cin, iv.cs, iv.co, h.dtype) ? "dw3_sum_tile_kernel" : vec ? (h.dtype == RTDM_F16 ? "dw3_sum_kernel<_Float16,8>" : "dw3_sum_kernel<float,4>")
+               : (h.dtype == RTDM_F16 ? "dw3_sum_kernel<_Float16,1>" : "dw3_sum_kernel<float,1>");
     flop = 2.0 * st.oh * st.ow * 3.0 * st.cin * 9;
-    bytes = ((double)st.ih * st.iw + 3.0 * st.oh * st.ow) * st.cin * es;
+    bytes = ((double)st.ih * st.iw + (double)st.oh * st.ow) * st.cin * es;
   } else if (st.kind == ST_ADD) {
     name = "add_kernel";
     flop = 0;

@@ -141,6 +141,192 @@ void launch_dw3_acff(const void* in, int in_cs, int in_co, int n, int h, int w, 
   RTDM_HIP(hipGetLastError());
 }
 
+// YOLO-ACFF depthwise stage, additive (models.py:296-302: conv1(x) + conv2(x) + conv3(x)):
+// the three dilated 3x3 depthwise branches d1p0 / d2p1 / d3p2 of channel c, all centred
+// on input (oy+1, ox+1), summed with their biases in fp32 and stored ONCE as a C-channel
+// map (rounded once in the fp16 path), which the 1x1 fusion conv then reads with its
+// original [F][C] weights (the classifier's ACFF, acff.py:46, concatenates instead:
+// dw3_acff_*kernel above).  The 27 tap weights [27][C] and the summed bias [C] sit in
+// LDS for the whole grid-stride loop; a thread owns VEC channels of one pixel (16-byte
+// loads of the NHWC input; the 27 shifted reads of neighbouring pixels hit L1/L2).
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void dw3_sum_kernel(const T* __restrict__ in, int in_cs, int in_co, int n, int h,
+                                                      int w, int c, const float* __restrict__ wts,
+                                                      const float* __restrict__ bsum, T* __restrict__ out) {
+  typedef T tv __attribute__((ext_vector_type(VEC)));
+  typedef float fv __attribute__((ext_vector_type(VEC)));
+  extern __shared__ float s_dw[];  // [27][c] taps (branch-major), then [c] bias sums
+  for (int i = threadIdx.x; i < 28 * c; i += blockDim.x) s_dw[i] = i < 27 * c ? wts[i] : bsum[i - 27 * c];
+  __syncthreads();
+  const int oh = h - 2, ow = w - 2;
+  const int cg = c / VEC;
+  const int64_t total = (int64_t)n * oh * ow * cg;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(idx % cg);
+    int64_t p = idx / cg;
+    const int ox = (int)(p % ow);
+    p /= ow;
+    const int oy = (int)(p % oh);
+    const int b = (int)(p / oh);
+    const int ch0 = g * VEC;
+    const T* src = in + (size_t)b * h * w * in_cs + in_co + ch0;
+    fv acc;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = s_dw[27 * c + ch0 + j];
+#pragma unroll
+    for (int br = 0; br < 3; ++br) {
+      const int d = br + 1;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int iy = oy + 1 + (kh - 1) * d;
+        if ((unsigned)iy >= (unsigned)h) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int ix = ox + 1 + (kw - 1) * d;
+          if ((unsigned)ix >= (unsigned)w) continue;
+          const tv x = *(const tv*)(src + ((size_t)iy * w + ix) * in_cs);
+          const float* wp = s_dw + (br * 9 + kh * 3 + kw) * c + ch0;
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) acc[j] = fmaf(wp[j], (float)x[j], acc[j]);
+        }
+      }
+    }
+    tv o;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = (T)acc[j];
+    *(tv*)(out + (((size_t)b * oh + oy) * ow + ox) * c + ch0) = o;
+  }
+}
+
+// LDS-tiled fp16 form of dw3_sum_kernel for C % 64 == 0: a block stages an 8 x 32 output
+// tile's input window (14 x 38 pixels: radius 3 around the tap centre) of one 64-channel
+// slice into LDS once (68 KB, zero outside the image = the branches' zero padding), then
+// each thread computes 4 neighbouring pixels x 8 channels, reading every tap's weights
+// once per 4 pixels.  The 27 shifted reads per output come from LDS (conflict-free
+// 16-byte reads: 8 pixels x 8 channel vectors = 1 KB contiguous per wave-instruction)
+// instead of L1/L2.  Same sum order as dw3_sum_kernel (bias, branch, kh, kw).
+constexpr int kDwTH = 8, kDwTW = 32, kDwCS = 64;
+__global__ __launch_bounds__(256) void dw3_sum_tile_kernel(const _Float16* __restrict__ in, int in_cs, int in_co,
+                                                           int n, int h, int w, int c, const float* __restrict__ wts,
+                                                           const float* __restrict__ bsum,
+                                                           _Float16* __restrict__ out) {
+  typedef _Float16 h8t __attribute__((ext_vector_type(8)));
+  constexpr int IH = kDwTH + 6, IW = kDwTW + 6, G = kDwCS / 8, QW = kDwTW / 4;
+  __shared__ h8t s_in[IH * IW * G];
+  __shared__ float s_w[28 * kDwCS];
+  const int oh = h - 2, ow = w - 2;
+  const int tx = (ow + kDwTW - 1) / kDwTW, ty = (oh + kDwTH - 1) / kDwTH, tc = c / kDwCS;
+  int bid = blockIdx.x;
+  const int ci = bid % tc;
+  bid /= tc;
+  const int xi = bid % tx;
+  bid /= tx;
+  const int yi = bid % ty;
+  const int b = bid / ty;
+  const int c0 = ci * kDwCS, oy0 = yi * kDwTH, ox0 = xi * kDwTW;
+  for (int i = threadIdx.x; i < 28 * kDwCS; i += 256) {
+    const int t = i / kDwCS, j = i - t * kDwCS;
+    s_w[i] = t < 27 ? wts[t * c + c0 + j] : bsum[c0 + j];
+  }
+  const _Float16* src = in + (size_t)b * h * w * in_cs + in_co + c0;
+  for (int i = threadIdx.x; i < IH * IW * G; i += 256) {
+    const int g = i % G, px = i / G;
+    const int gy = oy0 - 2 + px / IW, gx = ox0 - 2 + px % IW;
+    h8t v = {};
+    if ((unsigned)gy < (unsigned)h && (unsigned)gx < (unsigned)w) v = *(const h8t*)(src + ((size_t)gy * w + gx) * in_cs + g * 8);
+    s_in[i] = v;
+  }
+  __syncthreads();
+  for (int it = threadIdx.x; it < kDwTH * QW * G; it += 256) {
+    const int g = it % G, q = it / G;
+    const int y = q / QW, x0 = (q % QW) * 4;
+    float acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float bj = s_w[27 * kDwCS + g * 8 + j];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) acc[p][j] = bj;
+    }
+#pragma unroll
+    for (int br = 0; br < 3; ++br) {
+      const int d = br + 1;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int ly = y + 3 + (kh - 1) * d;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int lx = x0 + 3 + (kw - 1) * d;
+          const float* wp = s_w + (br * 9 + kh * 3 + kw) * kDwCS + g * 8;
+          float wv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) wv[j] = wp[j];
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const h8t xv = s_in[(ly * IW + lx + p) * G + g];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[p][j] = fmaf(wv[j], (float)xv[j], acc[p][j]);
+          }
+        }
+      }
+    }
+    const int oy = oy0 + y;
+    if (oy >= oh) continue;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int ox = ox0 + x0 + p;
+      if (ox >= ow) break;
+      h8t o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (_Float16)acc[p][j];
+      *(h8t*)(out + (((size_t)b * oh + oy) * ow + ox) * c + c0 + g * 8) = o;
+    }
+  }
+}
+
+bool dw3_sum_tile_ok(int c, int in_cs, int in_co, int dtype) {
+  return dtype == RTDM_F16 && c % kDwCS == 0 && in_cs % 8 == 0 && in_co % 8 == 0;
+}
+
+bool dw3_sum_vec_ok(int c, int in_cs, int in_co, int dtype) {
+  const int vec = dtype == RTDM_F16 ? 8 : 4;
+  return c % vec == 0 && in_cs % vec == 0 && in_co % vec == 0;
+}
+
+void launch_dw3_sum(const void* in, int in_cs, int in_co, int n, int h, int w, int c, const float* wts,
+                    const float* bsum, void* out, int dtype, hipStream_t s) {
+  const int64_t total = (int64_t)n * (h - 2) * (w - 2) * c;
+  if (total <= 0) return;
+  const size_t lds = (size_t)28 * c * sizeof(float);
+  RTDM_REQUIRE(lds <= 160 * 1024, RTDM_E_UNSUPPORTED, "acff: too many channels for the LDS tap table");
+  if (dw3_sum_tile_ok(c, in_cs, in_co, dtype)) {
+    const int64_t blocks = (int64_t)n * ((h - 2 + kDwTH - 1) / kDwTH) * ((w - 2 + kDwTW - 1) / kDwTW) * (c / kDwCS);
+    RTDM_REQUIRE(blocks < (1ll << 31), RTDM_E_CAPACITY, "acff: grid too large");
+    hipLaunchKernelGGL(dw3_sum_tile_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const _Float16*)in, in_cs, in_co,
+                       n, h, w, c, wts, bsum, (_Float16*)out);
+    RTDM_HIP(hipGetLastError());
+    return;
+  }
+  const bool vec = dw3_sum_vec_ok(c, in_cs, in_co, dtype);
+  const int g = grid_for(vec ? total / (dtype == RTDM_F16 ? 8 : 4) : total, 256);
+  if (dtype == RTDM_F16) {
+    if (vec)
+      hipLaunchKernelGGL((dw3_sum_kernel<_Float16, 8>), dim3(g), dim3(256), lds, s, (const _Float16*)in, in_cs, in_co,
+                         n, h, w, c, wts, bsum, (_Float16*)out);
+    else
+      hipLaunchKernelGGL((dw3_sum_kernel<_Float16, 1>), dim3(g), dim3(256), lds, s, (const _Float16*)in, in_cs, in_co,
+                         n, h, w, c, wts, bsum, (_Float16*)out);
+  } else {
+    if (vec)
+      hipLaunchKernelGGL((dw3_sum_kernel<float, 4>), dim3(g), dim3(256), lds, s, (const float*)in, in_cs, in_co, n, h,
+                         w, c, wts, bsum, (float*)out);
+    else
+      hipLaunchKernelGGL((dw3_sum_kernel<float, 1>), dim3(g), dim3(256), lds, s, (const float*)in, in_cs, in_co, n, h,
+                         w, c, wts, bsum, (float*)out);
+  }
+  RTDM_HIP(hipGetLastError());
+}
+
 // ----------------------------------------------------------------- maxpool --
 // nn.MaxPool2d(k, s, padding=pad) (implicit -inf padding), or, for the
 // Darknet size-2/stride-1 case, ZeroPad2d((0,1,0,1)) + MaxPool2d(2,1)
