@@ -83,7 +83,8 @@ class DarknetRef:
         assert ptr == stream.size, (ptr, stream.size)
 
     @torch.no_grad()
-    def forward(self, x: torch.Tensor, keep_layers=False, raw=False, f16_storage=False, conv_hook=None):
+    def forward(self, x: torch.Tensor, keep_layers=False, raw=False, f16_storage=False, conv_hook=None,
+                override=None):
         """x: [N,3,H,W] fp32 in [0,1] -> io [N, sum(A*ny*nx), 5+nc] (and per-layer outputs).
         raw=True: the undecoded p rows instead (YOLOLayer training branch, models.py:240-250).
 
@@ -95,8 +96,13 @@ class DarknetRef:
         deviation from the fp32 oracle by a small multiple of this mode's own deviation.
 
         conv_hook(i, x, w, b) -> (x, w, b): test-only hook on each [convolutional] layer's
-        input and BN-folded weights (f16_storage mode), e.g. to model int8 quantisation."""
+        input and BN-folded weights (f16_storage mode), e.g. to model int8 quantisation.
+
+        override {layer: tensor}: teacher forcing -- after layer i is computed (kept in
+        self.computed[i]), later layers consume override[i] instead (e.g. the HIP path's own
+        output of that layer), so each layer's deviation is its own, not compounded."""
         h16 = (lambda t: t.half().float()) if f16_storage else (lambda t: t)
+        self.computed = {}
         img_size = x.shape[-2:]
         x = h16(x)
         out, io_list = [], []
@@ -178,7 +184,11 @@ class DarknetRef:
             nxt = self.mdefs[i + 1]["type"] if i + 1 < len(self.mdefs) else ""
             if t != "yolo" and nxt != "yolo":
                 x = h16(x)
-            out.append(x if (keep_layers or i in self.routs) else [])
+            if override is not None:
+                self.computed[i] = x
+                if i in override:
+                    x = override[i].to(x.dtype)
+            out.append(x if (keep_layers or i in self.routs or override is not None) else [])
         io = torch.cat(io_list, 1)
         return (io, out) if keep_layers else io
 

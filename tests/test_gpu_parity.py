@@ -229,9 +229,11 @@ def test_detector_golden_full(dev, det_golden, case, half):
     assert list(io.shape) == list(det_golden[f"{case}/io_shape"])
     deep = not cfg.startswith("yolov4-tiny") and not cfg.startswith("yolov3-tiny")
     if cfg == "yolov3-acffx":
-        # 21 ACFF blocks on synthetic weights amplify rounding ~2x per block pair: fp32 reaches
-        # the heads at ~1.5e-3 relative (tools/acff_layers.py; per-layer test below), fp16
-        # is not comparable end to end.  Measured fp32: xy 0.017 px, wh 0.7 %, p 2.8e-3.
+        # fp32 reaches the heads at ~1.5e-3 relative (per-layer test below).  Measured fp32:
+        # xy 0.017 px, wh 0.7 %, p 2.8e-3.  fp16 end to end is not comparable on these
+        # synthetic weights (the oracle's own fp16-storage model drifts ~1.2x per layer): the
+        # fp16 path is checked teacher-forced, layer by layer and at io, in
+        # test_yolo_acff_layers_vs_oracle.
         if half:
             assert np.isfinite(io).all()
             return
@@ -338,29 +340,54 @@ def test_detector_layers_vs_oracle(dev, half):
 @pytest.mark.parametrize("half", [False, True])
 def test_yolo_acff_layers_vs_oracle(dev, half):
     """YOLO-ACFF (yolov3-acffx.cfg: [acff] blocks, unfused shortcuts, route resize) layer by
-    layer against the oracle.  fp32: every layer within 5e-3 of its max (measured growth
-    5e-7 -> 1.5e-3 from the stem to the heads).  fp16: the first two ACFF stages (through
-    L14) within 2e-2 (measured <= 8.8e-3); deeper layers inherit the amplified fp16 rounding."""
+    layer against the oracle.
+    fp32: the oracle run end to end; every materialised layer within 5e-3 of its max
+    (measured growth 5e-7 -> 1.5e-3 from the stem to the heads).
+    fp16: teacher forced -- the oracle computes each layer from the HIP path's own fp16
+    outputs of the layers it reads (DarknetRef.forward(override=...)), so each layer's
+    error is its own: every materialised layer within 5e-3 of its max, and io within the
+    tiny nets' fp16 bars.  End to end, fp16 on these synthetic BatchNorm-calibrated weights
+    is not comparable with fp32: the oracle's own fp16-storage model drifts by ~1.2x per
+    layer (rms 1.5e-3 at L0, 0.5 by the last head; mean-field BN nets are chaotic at
+    init), so a cumulative bar would test the weights, not the kernels."""
     from oracle.darknet import DarknetRef
     from rtdm.synth import load_calibration, synth_acff_params, synth_darknet_weights, synth_frames
     m, text, _ = _darknet("yolov3-acffx", 416, half)
     frames = synth_frames(2, 416, 416, seed=3)
-    m(torch.from_numpy(frames).to(dev))
+    io, _ = m(torch.from_numpy(frames).to(dev))
+    io = io.cpu().numpy()
     cal = load_calibration("yolov3-acffx")
     ref = DarknetRef(text, synth_darknet_weights(text, calib=cal), synth_acff_params(text, calib=cal))
-    _, outs = ref.forward(torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0, keep_layers=True)
-    checked = 0
-    for i, o in enumerate(outs):
-        if not isinstance(o, torch.Tensor) or (half and i > 14):
-            continue
+    xin = torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0
+    hip = {}
+    for i in range(len(ref.mdefs)):
         try:
-            got = m.layer_output(i, 2).cpu()
+            hip[i] = m.layer_output(i, 2).cpu()
         except RuntimeError:
             continue  # fused away
+    # a layer the route resize (models.py:364-375) replaced reads back resized: not comparable
+    ref.forward(xin, override={})
+    hip = {i: t for i, t in hip.items() if tuple(t.shape) == tuple(ref.computed[i].shape)}
+    if half:
+        ref_io, _ = ref.forward(xin, keep_layers=True, override=hip)
+        outs = [ref.computed.get(i) for i in range(len(ref.mdefs))]
+        bar = 5e-3  # measured worst 9.9e-4 (57 layers)
+    else:
+        ref_io, outs = ref.forward(xin, keep_layers=True)
+        bar = 5e-3
+    checked, worst = 0, 0.0
+    for i, got in hip.items():
+        o = outs[i]
+        if not isinstance(o, torch.Tensor):
+            continue
         rel = (got - o).abs().max().item() / (o.abs().max().item() + 1e-6)
-        assert rel <= (2e-2 if half else 5e-3), (i, ref.mdefs[i]["type"], rel)
+        worst = max(worst, rel)
+        assert rel <= bar, (i, ref.mdefs[i]["type"], rel)
         checked += 1
-    assert checked >= (10 if half else 50), checked
+    assert checked >= 50, checked
+    print("acffx", "fp16 teacher-forced" if half else "fp32", "layers", checked, "worst rel", worst)
+    if half:
+        _check_io(io, ref_io.numpy(), True)
 
 
 _ACFF_MINI = """[net]
