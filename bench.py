@@ -48,6 +48,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "real-time-disaster-management_amd"))
 
 MFMA_F16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/fp16
+MFMA_I8_DENSE_PEAK_TOPS = 5000.0     # int8 MFMA: 2x the bf16 rate per clock (same table)
 CLASSIFIER_FLOP = {"squeeze-ernet": 90953544.0, "squeeze-redconv": 77593080.0, "ernet": 319307650.0, "none": 0.0}
 METRIC = "frames/sec two-stage (ErNET→YOLOv4) 608×608 b64 @1/2/4/8 GPU; top-1/mAP parity"
 
@@ -64,7 +65,8 @@ def parse():
     ap.add_argument("--cfg", default="yolov4-tiny-aider-416")
     ap.add_argument("--classifier", default="ernet", choices=["ernet", "squeeze-ernet", "squeeze-redconv", "none"],
                     help="none: detection only (BASELINE config 3)")
-    ap.add_argument("--dtype", default="f16", choices=["f16", "f32"])
+    ap.add_argument("--dtype", default="f16", choices=["f16", "f32", "i8"],
+                    help="i8: int8-quantised detector (BASELINE config 5; classifier fp16)")
     ap.add_argument("--conf", type=float, default=0.3)
     ap.add_argument("--iou", type=float, default=0.4)
     ap.add_argument("--max-det", type=int, default=300)
@@ -139,8 +141,12 @@ def build(args, world, rank):
     det.load_weight_stream(stream)
     if use_cls:
         cls.load_state_dict(sd)
-    if args.dtype == "f16":
-        det.half()
+    calib = None
+    if args.dtype == "i8":  # calibration frames disjoint from the timed ones
+        from rtdm.synth import BASE_SEED, synth_frames
+        calib = torch.from_numpy(synth_frames(8, args.img, args.img, seed=BASE_SEED + 4321)).cuda()
+    if args.dtype in ("f16", "i8"):
+        det.half() if args.dtype == "f16" else det.int8(calib)
         if use_cls:
             cls.half()
     pipes = []
@@ -150,8 +156,8 @@ def build(args, world, rank):
             det.load_weight_stream(stream)
             if use_cls:
                 cls.load_state_dict(sd)
-            if args.dtype == "f16":
-                det.half()
+            if args.dtype in ("f16", "i8"):
+                det.half() if args.dtype == "f16" else det.int8(calib)
                 if use_cls:
                     cls.half()
         pipes.append(TwoStagePipeline(cls, det, args.conf, args.iou, args.max_det, overlap=bool(args.overlap),
@@ -345,8 +351,10 @@ def main():
         avg_ms = t_ms / launches
         achieved = (flop / launches) / (avg_ms * 1e-3) / 1e12
         tr = pmc_traffic(dom, b)
-        rl = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": MFMA_F16_DENSE_PEAK_TFLOPS,
-              "unit": "TFLOP/s", "frac": round(achieved / MFMA_F16_DENSE_PEAK_TFLOPS, 4),
+        i8k = "_i8" in dom
+        peak = MFMA_I8_DENSE_PEAK_TOPS if i8k else MFMA_F16_DENSE_PEAK_TFLOPS
+        rl = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak,
+              "unit": "TOP/s" if i8k else "TFLOP/s", "frac": round(achieved / peak, 4),
               "traffic": round(tr["bytes_per_launch"]) if tr else None,
               "avg_launch_ms": round(avg_ms, 4), "launches": launches,
               "algorithmic_flop_per_launch": round(flop / launches),
@@ -397,7 +405,7 @@ def main():
         "metric": METRIC,
         "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "f16" if args.dtype == "f16" else "f32",
+        "scaling": scaling, "vs_baseline": None, "dtype": args.dtype,
         "data": f"synthetic {args.img}x{args.img} uint8 frames (seeded, {len(frames)} rotations), synthetic "
                 f"calibrated detector weights"
                 + (f", the reference's trained {args.classifier} weights" if args.classifier != "none" else ""),

@@ -67,10 +67,11 @@ typedef enum rtdm_status {
 typedef enum rtdm_dtype {
   RTDM_F32 = 0, /* fp32 activations/weights, fp32 FMA (parity mode)            */
   RTDM_F16 = 1, /* fp16 activations/weights, fp32 accumulation on MFMA          */
-  RTDM_I8 = 2   /* detector only: fp16 activations, the Cin % 64 == 0 convs on
-                   int8 MFMA (per-channel int8 weights, per-tensor activation
-                   scales from rtdm_detector_calibrate); the reference's
-                   README --quant int8 (config 5)                               */
+  RTDM_I8 = 2   /* detector only: fp16 activations in HBM; every conv with Cin % 128 == 0
+                   runs on int8 MFMA (conv_pipe_i8: v_mfma_i32_16x16x64_i8) over a
+                   per-channel int8 copy of its input, per-channel activation scales
+                   folded into per-output-channel int8 weights (rtdm_detector_calibrate);
+                   the reference's README --quant int8 (config 5)                      */
 } rtdm_dtype;
 
 typedef enum rtdm_model_kind {
@@ -170,14 +171,16 @@ rtdm_status rtdm_detector_enable_timing(rtdm_detector h, int max_calls);
 rtdm_status rtdm_detector_read_timing(rtdm_detector h, double* ms_per_step, int* calls);
 /* io: [n, n_anchors_total, no] fp32, exactly the reference's torch.cat(io, 1). */
 rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float* io, void* stream);
-/* int8 calibration (RTDM_I8 handles): runs the network in fp16 on x (n images,
- * kinds as rtdm_detect) recording every int8 conv's input |x|max (max over all
- * calls since the last reset != 0), then sets the activation scales
- * s_x = |x|max / 127 and the per-channel dequantisation multipliers.  Synchronises
- * the stream (a setup step).  n = 0 with reset = 0 only recomputes the scales.
- * rtdm_detect on an uncalibrated RTDM_I8 handle returns RTDM_E_INVALID.  This
- * replaces the TensorRT entropy-calibration caches (calib_cache/ *.bin files), which the
- * reference builds with its own engines (build_tensorrt_model.py:256-259 is a stub). */
+/* int8 calibration (RTDM_I8 handles): runs the network in fp16 on x (n images, kinds
+ * as rtdm_detect) recording every int8 conv's per-input-channel |x|max (max over all
+ * calls since the last reset != 0), then sets the activation scales s_c = |x|max_c / 127,
+ * folds them into the conv's BN-folded weights and quantises those per output channel
+ * (symmetric int8, deq[o] = max|W'[o]| / 127).  Synchronises the stream (a setup step).
+ * n = 0 with reset = 0 only recomputes the weights from the recorded maxima.
+ * rtdm_detect on an uncalibrated RTDM_I8 handle returns RTDM_E_INVALID.  This replaces
+ * the TensorRT entropy-calibration caches (calib_cache/ *.bin), which the reference
+ * builds with its own engines (calibrator.py:87-153; build_tensorrt_model.py:256-259 is a
+ * stub).                                                                          */
 rtdm_status rtdm_detector_calibrate(rtdm_detector h, const void* x, int x_kind, int n, int reset, void* stream);
 /* Raw head predictions: p [n, n_anchors_total, no] fp32 in io's row order, i.e. the
  * YOLOLayer training-branch output p.view(bs,na,no,ny,nx).permute(0,1,3,4,2)

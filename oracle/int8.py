@@ -1,0 +1,50 @@
+"""int8 quantisation model of the detector's RTDM_I8 path (TEST INFRASTRUCTURE ONLY).
+
+The reference has no numeric int8 path (opaque TensorRT engines and
+entropy-calibration caches, tensorrt_inference/yolo/calibrator.py:87-153), so the int8
+check compares the HIP int8 io with the fp32 oracle relative to this model of the same
+scheme on the oracle (conv_hook of oracle.darknet.DarknetRef in f16_storage mode):
+  * quantised convs: [convolutional] layers with cin % 128 == 0 and cout % 128 == 0
+    (the int8-eligible convs of the C++ planner, detector.cpp);
+  * calibration: per input channel |x|max over the calibration frames' fp16-storage
+    forward; s_c = |x|max_c / 127;
+  * weights: BN-folded fp16 weights times s_c, symmetric int8 per output channel
+    (s_w[o] = max|W'[o]| / 127); activations q = clamp(rint(x / s_c), -127, 127).
+"""
+from __future__ import annotations
+
+import torch
+
+
+def eligible(mdefs, i, cin):
+    m = mdefs[i]
+    return (m["type"] == "convolutional" and cin % 128 == 0 and int(m["filters"]) % 128 == 0
+            and int(m["size"]) in (1, 3))
+
+
+def calibrate(ref, x):
+    """Per-channel |x|max of every eligible conv input on frames x ([N,3,H,W] in [0,1])."""
+    amax = {}
+
+    def hook(i, xi, w, b):
+        if eligible(ref.mdefs, i, xi.shape[1]):
+            m = xi.abs().amax(dim=(0, 2, 3))
+            amax[i] = torch.maximum(amax[i], m) if i in amax else m
+        return xi, w, b
+
+    ref.forward(x, f16_storage=True, conv_hook=hook)
+    return amax
+
+
+def int8_hook(amax):
+    """conv_hook applying the RTDM_I8 quantisation to the calibrated layers."""
+    def hook(i, x, w, b):
+        if i not in amax:
+            return x, w, b
+        s = torch.where(amax[i] > 0, amax[i] / 127.0, torch.ones_like(amax[i])).view(1, -1, 1, 1)
+        xq = torch.round(x / s).clamp(-127, 127)
+        wp = w * s.view(1, -1, 1, 1)  # fold the activation scales into the input channels
+        sw = wp.abs().flatten(1).amax(1).clamp_min(1e-30) / 127.0
+        wq = torch.round(wp / sw.view(-1, 1, 1, 1)).clamp(-127, 127)
+        return xq, wq * sw.view(-1, 1, 1, 1), b
+    return hook

@@ -176,21 +176,18 @@ struct ConvArgs {
   const void* head_w = nullptr;
   int head_cout = 0;
   Epilogue head_e;
-  // int8 path (conv_i8.hip): int8 weights [cout_pad][kpad], per-channel dequant
-  // multipliers deq[c] = s_x * s_w[c], activation quantisation scale 1 / s_x
+  // int8 path (conv_pipe_i8): int8 weights [cout_pad][kpad] with the input's per-channel
+  // activation scales folded in, per-output-channel dequantisation deq[o] = s_w[o]
   const void* w8 = nullptr;
   const float* deq = nullptr;
-  float qscale = 0.f;
 };
 
 // Launchers (conv.hip).  dtype = RTDM_F16 / RTDM_F32 (activation + weight type).
 void launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
-// conv_i8.hip: int8 MFMA implicit GEMM (RTDM_I8 detectors) + calibration |x|max
-bool conv_i8_ok(const ConvArgs& a);
-void launch_conv_i8(const ConvArgs& a, hipStream_t s);
-void launch_absmax(View v, int n, int h, int w, int c, unsigned* out, hipStream_t s);
-static constexpr int kCalBins = 2048;  // |x| histogram bins over [0, |x|max]
-void launch_abshist(View v, int n, int h, int w, int c, const unsigned* amax, unsigned* hist, hipStream_t s);
+// conv_i8.hip: int8 calibration (per-channel |x|max of an fp16 view, float bits) and the
+// per-channel quantisation of an fp16 view into a contiguous int8 copy
+void launch_chan_absmax(View v, int n, int h, int w, int c, unsigned* out, hipStream_t s);
+void launch_quantize(View v, int n, int h, int w, int c, const float* inv_scale, int8_t* q, hipStream_t s);
 // conv_pipe.hip: pipelined 256x128 implicit GEMM for Cin % 64 == 0 layers
 bool conv_pipe_ok(const ConvArgs& a);
 void launch_conv_pipe(const ConvArgs& a, hipStream_t s);
@@ -199,6 +196,11 @@ int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 
 void set_pipe_bm(int v);                  // 0 = cost model, else forced
 void set_pipe_korder(int v);              // conv_pipe K order: 0 tap outer, 1 channel-block outer
 const char* conv_pipe_name(const ConvArgs& a);  // kernel symbol of that launch
+// int8 twin (RTDM_I8): a.in = quantised contiguous int8 copy of the input, a.w8 int8
+// weights (per-channel activation scales folded in), a.deq per-output-channel scales
+bool conv_pipe_i8_ok(const ConvArgs& a);
+void launch_conv_pipe_i8(const ConvArgs& a, hipStream_t s);
+const char* conv_pipe_i8_name(const ConvArgs& a);
 // diagnostics: conv_stem3 ablation builds (tools/ab_conv.py --key stem_abl)
 int stem_abl();
 void set_stem_abl(int v);

@@ -94,10 +94,16 @@ __device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v
 // fused YOLO head; bit 128 (not an ablation): lean epilogue (epi_vec8_lean); bit 256 with
 // 128: lean epilogue with the fused shortcut add.
 // One BM x 128 output tile (logical tile index bid, M-major over N tiles).
-template <int ABL, int BM>
+// I8 (RTDM_I8 detectors, BASELINE config 5): int8 activations (a quantised copy of the
+// input view, per-channel scales folded into the weights) and int8 weights, the same
+// 128-byte LDS rows holding 128 K-elements instead of 64, v_mfma_i32_16x16x64_i8 in place
+// of v_mfma_f32_16x16x32_f16 (same issue count per K-block, twice the K), exact int32
+// sums dequantised per output channel (a.deq) before the unchanged fp32 epilogues.
+template <int ABL, int BM, bool I8 = false>
 __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem_raw, int bid) {
   constexpr int WM = PipeCfg<BM>::WM, WN = PipeCfg<BM>::WN;
-  constexpr int BN = kPBN, BK = kPBK;
+  constexpr int BN = kPBN, BK = kPBK;              // LDS row: BK halfs = 128 bytes
+  constexpr int ES = I8 ? 1 : 2, BKE = I8 ? 128 : 64;  // element bytes, K-elements per K-block
   constexpr int kPStage = PipeCfg<BM>::Stage;
   constexpr int WAVES = WM * WN, NT = 64 * WAVES;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // accumulators per wave
@@ -129,6 +135,14 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       lh[j] = cv && a.e.scale ? a.e.shift[c0 + j] : 0.f;
     }
   }
+  float dq[FN];  // int8: per-output-channel dequantisation of this lane's accumulator columns
+  if constexpr (I8) {
+#pragma unroll
+    for (int tn = 0; tn < FN; ++tn) {
+      const int col = n_base + wn * (BN / WN) + tn * 16 + (lane & 15);
+      dq[tn] = col < a.cout ? a.deq[col] : 0.f;
+    }
+  }
   float hb[FN], hs[FN], hh[FN];
   if constexpr ((ABL & 8) != 0) {
 #pragma unroll
@@ -150,13 +164,13 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
     const int r = 8 * (NA * wid + j) + (lane >> 3);
-    const int kofs = 8 * (slot ^ ((r >> 1) & 7));
+    const int kofs = 16 * (slot ^ ((r >> 1) & 7));  // bytes
     const int m = m_base + r;
     int n = 0, oy = 0, ox = 0;
     if (m < a.M) row_to_pix(a, m, n, oy, ox);
     const int iy0 = m < a.M ? oy * a.stride - a.pad : -(1 << 28);
     const int ix0 = ox * a.stride - a.pad;
-    voff_a[j] = m < a.M ? ((n * a.ih * a.iw + iy0 * a.iw + ix0) * a.in_cs + kofs) * 2 : 0;
+    voff_a[j] = m < a.M ? (n * a.ih * a.iw + iy0 * a.iw + ix0) * a.in_cs * ES + kofs : 0;
     uint32_t msk = 0;
     for (int t = 0; t < a.ks * a.ks; ++t) {
       const int kh = a.ks == 3 ? (t * 11) >> 5 : 0, kw = t - kh * a.ks;
@@ -169,15 +183,15 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int r = 8 * (NB * wid + j) + (lane >> 3);
-    voff_b[j] = (r * a.kpad + 8 * (slot ^ ((r >> 1) & 7))) * 2;
+    voff_b[j] = r * a.kpad * ES + 16 * (slot ^ ((r >> 1) & 7));
   }
-  const _Float16* in = (const _Float16*)a.in + a.in_co;
-  const int64_t in_bytes = ((int64_t)a.n * a.ih * a.iw * a.in_cs - a.in_co) * 2;
+  const char* in = (const char*)a.in + (size_t)a.in_co * ES;
+  const int64_t in_bytes = ((int64_t)a.n * a.ih * a.iw * a.in_cs - a.in_co) * ES;
   const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((const _Float16*)a.w + (size_t)n_base * a.kpad), 0, BN * a.kpad * 2, 0x00020000);
-  const int nk = a.kpad / BK;
-  const int cpt = a.cin / BK;  // K-blocks per tap
+      (void*)((const char*)(I8 ? a.w8 : a.w) + (size_t)n_base * a.kpad * ES), 0, BN * a.kpad * ES, 0x00020000);
+  const int nk = a.kpad / BKE;
+  const int cpt = a.cin / BKE;  // K-blocks per tap
   const int ntap = a.ks * a.ks;
   int st_tap = 0, st_c = 0, st_buf = 0;
 
@@ -186,13 +200,13 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     _Float16* As = smem + st_buf * kPStage;
     _Float16* Bs = As + BM * BK;
     const int kh = a.ks == 3 ? (st_tap * 11) >> 5 : 0, kw = st_tap - kh * a.ks;
-    const int tapoff = ((kh * a.iw + kw) * a.in_cs + st_c * BK) * 2;
+    const int tapoff = ((kh * a.iw + kw) * a.in_cs + st_c * BKE) * ES;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int vo = ((vmask[j] >> st_tap) & 1u) ? voff_a[j] + tapoff : (int)0x80000000;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(As + 8 * (NA * wid + j) * BK), 16, vo, 0, 0, 0);
     }
-    const int koff = (st_tap * a.cin + st_c * BK) * 2;  // weight column of this K-block (tap-major packing)
+    const int koff = (st_tap * a.cin + st_c * BKE) * ES;  // weight column of this K-block (tap-major packing)
 #pragma unroll
     for (int j = 0; j < NB; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j], koff,
@@ -214,11 +228,20 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   const int so0 = 8 * ((0 + g) ^ rsw), so1 = 8 * ((4 + g) ^ rsw);
   const int a_row = (wm * (BM / WM) + fr) * BK, b_row = (BM + wn * (BN / WN) + fr) * BK;
 
-  f4 acc[FM][FN];
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  using AccT = std::conditional_t<I8, i32x4, f4>;
+  AccT acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = AccT{0, 0, 0, 0};
+  auto mfma = [&](const h8& x, const h8& y, AccT c) -> AccT {
+    if constexpr (I8)
+      return __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, x), __builtin_bit_cast(i32x4, y), c, 0, 0,
+                                                   0);
+    else
+      return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
+  };
 
   h8 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
   auto read0 = [&](int buf) {
@@ -274,7 +297,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     for (int tm = 0; tm < FM; ++tm)
 #pragma unroll
       for (int tn = 0; tn < FN; ++tn)
-        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa0[tm], fb0[tn], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = mfma(fa0[tm], fb0[tn], acc[tm][tn]);
     if constexpr (STG && !(ABL & 1)) {
       // reads in the first half of the cluster, the VM loads in the second
       constexpr int half = NMF / 2;
@@ -313,7 +336,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     for (int tm = 0; tm < FM; ++tm)
 #pragma unroll
       for (int tn = 0; tn < FN; ++tn)
-        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa1[tm], fb1[tn], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = mfma(fa1[tm], fb1[tn], acc[tm][tn]);
     if constexpr (NXT) interleave_reads();
     __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
     __builtin_amdgcn_sched_barrier(0);
@@ -328,6 +351,18 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
+  f4 accf[FM][FN];
+#pragma unroll
+  for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < FN; ++tn) {
+      if constexpr (I8) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) accf[tm][tn][j] = (float)acc[tm][tn][j] * dq[tn];
+      } else {
+        accf[tm][tn] = acc[tm][tn];
+      }
+    }
 
   if constexpr ((ABL & 8) != 0) {
     // ---- fused head: activated conv output (fp16, the value the unfused path would
@@ -346,7 +381,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int row = wm * (BM / WM) + tm * 16 + g * 4 + j;
-          float x = acc[tm][tn][j] + bias;
+          float x = accf[tm][tn][j] + bias;
           if (e.act == ACT_LEAKY)
             x = x > 0.f ? x : x * e.slope;
           else if (e.act == ACT_SWISH)  // yolov4-tiny-swish.cfg (models.py:43-44)
@@ -396,7 +431,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 #pragma unroll
     for (int tm = 0; tm < FM; ++tm)
 #pragma unroll
-      for (int tn = 0; tn < FN; ++tn) t += acc[tm][tn][0] + acc[tm][tn][1] + acc[tm][tn][2] + acc[tm][tn][3];
+      for (int tn = 0; tn < FN; ++tn) t += accf[tm][tn][0] + accf[tm][tn][1] + accf[tm][tn][2] + accf[tm][tn][3];
     if (t == 1234.5f) ((float*)a.e.full.ptr)[tid] = t;
     return;
   }
@@ -410,7 +445,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       const int row = wm * (BM / WM) + tm * 16 + rq;
       const int col = wn * (BN / WN) + tn * 16 + fr;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) Cs[(row + j) * kPCstr + col] = acc[tm][tn][j];
+      for (int j = 0; j < 4; ++j) Cs[(row + j) * kPCstr + col] = accf[tm][tn][j];
     }
   __syncthreads();
   constexpr int UNITS = (BM / 4) * CG;
@@ -455,6 +490,22 @@ __global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a, int ntiles) 
 }
 
 
+// int8 twin of conv_pipe_f16 (same persistent XCD walk)
+template <int ABL, int BM>
+__global__ __launch_bounds__(512, 1) void conv_pipe_i8(ConvArgs a, int ntiles) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[PipeCfg<BM>::Smem];
+  const int nb = gridDim.x, xcd = blockIdx.x & 7, l = blockIdx.x >> 3;
+  const int q = ntiles >> 3, r = ntiles & 7;
+  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int hi = lo + q + (xcd < r ? 1 : 0);
+  const int bx = (nb - xcd + 7) >> 3;
+  for (int t = lo + l; t < hi; t += bx) {
+    pipe_tile<ABL, BM, true>(a, smem_raw, t);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
 bool conv_pipe_ok(const ConvArgs& a) {
   if (!a.zero || a.in_kind != IN_NHWC || a.w_f32 || (a.in_cs | a.in_co) % 8 != 0) return false;
   if (a.cin % 64 != 0 || a.cout_pad % kPBN != 0 || (a.ks != 1 && a.ks != 3)) return false;
@@ -490,10 +541,12 @@ static int pipe_cus() {
 // 256 | 128 | 64) forces one (0 = this model).  Batch-invariant: only the tiling changes.
 static int g_pipe_bm = 0;
 void set_pipe_bm(int v) { g_pipe_bm = (v == 256 || v == 128 || v == 64) ? v : 0; }
-int pipe_bm(const ConvArgs& a) {
+static int pipe_bm_nk(const ConvArgs& a, int nk);
+int pipe_bm(const ConvArgs& a) { return pipe_bm_nk(a, a.kpad / kPBK); }
+static int pipe_bm_nk(const ConvArgs& a, int nk) {
   const bool head = a.head_w != nullptr;
   if (g_pipe_bm && !(head && g_pipe_bm == 64)) return g_pipe_bm;
-  const int nk = a.kpad / kPBK, ntn = a.cout_pad / kPBN, cus = pipe_cus();
+  const int ntn = a.cout_pad / kPBN, cus = pipe_cus();
   static const int bms[3] = {256, 128, 64};
   static const double eff[3] = {1.0, 0.85, 0.65};
   const double ovh = 3.0 + (head ? 4.0 : 0.0);
@@ -571,6 +624,59 @@ void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
         launch_pipe_bm<64>(a, s, ntiles, grid);
       break;
   }
+}
+
+// ---- int8 (RTDM_I8): the quantised input copy is contiguous [n*ih*iw][cin] int8 ----
+bool conv_pipe_i8_ok(const ConvArgs& a) {
+  if (!a.zero || a.in_kind != IN_NHWC || !a.w8 || !a.deq || (a.in_cs | a.in_co) % 16 != 0) return false;
+  if (a.cin % 128 != 0 || a.cout_pad % kPBN != 0 || (a.ks != 1 && a.ks != 3) || a.kpad != a.ks * a.ks * a.cin)
+    return false;
+  if ((int64_t)a.n * a.ih * a.iw * a.in_cs >= (1ll << 31) || (int64_t)a.cout_pad * a.kpad >= (1ll << 31)) return false;
+  if (a.head_w) {
+    if (a.cout_pad != kPBN || a.head_cout < 1 || a.head_cout > 32 || !a.head_e.io || !a.head_e.bias) return false;
+    if (a.e.full.ptr || a.e.pool.ptr || a.e.up.ptr || a.e.res.ptr || a.e.io || a.quad) return false;
+  }
+  return true;
+}
+
+const char* conv_pipe_i8_name(const ConvArgs& a) {
+  const int bm = pipe_bm_nk(a, a.kpad / 128);
+  if (a.head_w) return bm == 256 ? "conv_pipe_i8<8,256>" : "conv_pipe_i8<8,128>";
+  if (epi_lean_ok(a)) return bm == 256 ? "conv_pipe_i8<128,256>" : bm == 128 ? "conv_pipe_i8<128,128>" : "conv_pipe_i8<128,64>";
+  if (epi_lean_ok(a, true))
+    return bm == 256 ? "conv_pipe_i8<384,256>" : bm == 128 ? "conv_pipe_i8<384,128>" : "conv_pipe_i8<384,64>";
+  return bm == 256 ? "conv_pipe_i8<0,256>" : bm == 128 ? "conv_pipe_i8<0,128>" : "conv_pipe_i8<0,64>";
+}
+
+template <int BM>
+static void launch_pipe_i8_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid) {
+  if (a.head_w) {
+    if constexpr (BM >= 128) hipLaunchKernelGGL((conv_pipe_i8<8, BM>), grid, dim3(512), 0, s, a, ntiles);
+  } else if (epi_lean_ok(a)) {
+    hipLaunchKernelGGL((conv_pipe_i8<128, BM>), grid, dim3(512), 0, s, a, ntiles);
+  } else if (epi_lean_ok(a, true)) {
+    hipLaunchKernelGGL((conv_pipe_i8<384, BM>), grid, dim3(512), 0, s, a, ntiles);
+  } else {
+    hipLaunchKernelGGL((conv_pipe_i8<0, BM>), grid, dim3(512), 0, s, a, ntiles);
+  }
+}
+
+void launch_conv_pipe_i8(const ConvArgs& a_in, hipStream_t s) {
+  ConvArgs a = a_in;
+  RTDM_REQUIRE(conv_pipe_i8_ok(a), RTDM_E_INVALID, "conv_pipe_i8: unsupported layer");
+  a.pipe_corder = g_pipe_korder && a.ks == 3 ? 1 : 0;
+  const int bm = pipe_bm_nk(a, a.kpad / 128);
+  const int64_t nt = (int64_t)((a.M + bm - 1) / bm) * (a.cout_pad / kPBN);
+  RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
+  const int ntiles = (int)nt;
+  const dim3 grid((unsigned)(ntiles < pipe_cus() ? ntiles : pipe_cus()));
+  if (bm == 256)
+    launch_pipe_i8_bm<256>(a, s, ntiles, grid);
+  else if (bm == 128)
+    launch_pipe_i8_bm<128>(a, s, ntiles, grid);
+  else
+    launch_pipe_i8_bm<64>(a, s, ntiles, grid);
+  RTDM_HIP(hipGetLastError());
 }
 
 }  // namespace rtdm

@@ -133,12 +133,15 @@ struct Step {
   bool bn = false;  // raw darknet weights (host), packed after planning
   const float *w_beta = nullptr, *w_gamma = nullptr, *w_mean = nullptr, *w_var = nullptr, *w_bias = nullptr,
               *w_W = nullptr;
-  // int8 (RTDM_I8 handles): slot of this conv in the calibration table (-1: fp16 conv),
-  // int8 weights, per-channel weight scales (host) and dequant multipliers (device)
+  // int8 (RTDM_I8 handles): slot of this conv among the int8 convs (-1: fp16 conv); its
+  // BN-folded fp32 weights [cout][k] (host, k = tap * cin + c) for the calibration that
+  // folds the per-channel activation scales in; device slots of the int8 weights, the
+  // dequantisation scales deq[o] and the input's inverse activation scales; the offsets
+  // of its per-channel |x|max (amax) and of its quantised input copy (qarena, per image)
   int q = -1;
-  size_t w8_off = SIZE_MAX, deq_off = SIZE_MAX;
-  std::vector<float> sw;
-  float qscale = 0.f;
+  size_t w8_off = SIZE_MAX, deq_off = SIZE_MAX, inv_off = SIZE_MAX;
+  std::vector<float> wf;
+  size_t amax_off = 0, qbuf_off = 0;
   // two-stream schedule (schedule_streams): stream 0 = the caller's, 1 = the side stream
   int stream = 0;
   std::vector<int> deps;    // earlier steps writing a buffer this step reads
@@ -165,13 +168,15 @@ struct YoloHead {
 struct rtdm_detector_s {
   int img_h = 0, img_w = 0, dtype = 0, max_batch = 0, dev = 0;
   bool planning_only = true;
-  // RTDM_I8: activations fp16 (dtype = RTDM_F16), Cin % 64 == 0 convs on int8 MFMA
-  // once calibrated (rtdm_detector_calibrate); calibrating = forward in fp16 recording
-  // each int8 conv's input |x|max into amax[q]
+  // RTDM_I8: activations fp16 (dtype = RTDM_F16) in the arena; the Cin % 128 == 0 convs
+  // run conv_pipe_i8 on a per-channel int8 copy of their input once calibrated
+  // (rtdm_detector_calibrate); calibrating = the fp16 forward recording every int8
+  // conv's per-channel input |x|max
   bool int8 = false, calibrated = false;
-  int calibrating = 0;  // 1: |x|max pass, 2: histogram pass
+  int calibrating = 0;
   int n_q = 0;
-  rtdm::DevBuf amax, hist;  // [n_q] float bits, [n_q][kCalBins] counts
+  size_t q_channels = 0, q_bytes = 0;  // sum of int8 conv input channels; int8 copy bytes per image
+  rtdm::DevBuf amax, qarena;           // [q_channels] float bits; [max_batch * q_bytes] int8
   std::vector<rtdm::CfgBlock> defs;  // without [net]
   std::vector<rtdm::Tensor> tensors;
   std::vector<rtdm::Step> steps;
@@ -407,7 +412,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
           h.layer_tensor[i] = -1;        // the pre-add conv output is never materialised
           h.layer_tensor[i + 1] = full;  // conv output with the residual added
           need_full = !consumers[i + 1].empty();
-        } else if (f16 && fuse_head() && !h.int8 && !is_acff && nx.type == "convolutional" && only_next && i + 2 < L && defs[i + 2].type == "yolo" &&
+        } else if (f16 && fuse_head() && !is_acff && nx.type == "convolutional" && only_next && i + 2 < L && defs[i + 2].type == "yolo" &&
                    consumers[i + 1].size() == 1 && consumers[i + 1][0] == i + 2 && consumers[i + 2].empty() &&
                    nx.i("size", 1) == 1 && nx.i("stride", 1) == 1 && nx.i("groups", 1) == 1 &&
                    nx.i("filters", 0) <= 32 && filters > 64 && filters <= 128 &&
@@ -768,33 +773,27 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         RTDM_REQUIRE(st.hpc.kpad == 128 && st.hpc.cout_pad == 32, RTDM_E_INVALID, "internal: head packing");
       }
       if (stem) st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr);
-      if (h.int8 && use_mfma && !st.head && !st.acff && st.yolo < 0 && st.cin % 64 == 0 && (size == 1 || size == 3) &&
-          st.pc.cout_pad % 128 == 0) {
-        // symmetric per-output-channel int8 of the BN-folded weights, [cout_pad][kpad]
+      if (h.int8 && use_mfma && !st.acff && (st.yolo < 0 || st.head) && st.cin % 128 == 0 && (size == 1 || size == 3) &&
+          st.pc.cout_pad % 128 == 0 && st.pc.kpad == size * size * st.cin) {
+        // BN-folded fp32 rows [cout][k] kept for calibration; int8 slots filled there
         const int kp = st.pc.kpad, cp = st.pc.cout_pad;
-        std::vector<int8_t> w8((size_t)cp * kp, 0);
-        st.sw.assign(cp, 0.f);
-        for (int o = 0; o < filters; ++o) {
-          double mx = 0.0;
-          std::vector<double> row((size_t)size * size * st.cin);
+        st.wf.assign((size_t)filters * kp, 0.f);
+        for (int o = 0; o < filters; ++o)
           for (int c = 0; c < st.cin; ++c)
             for (int kh = 0; kh < size; ++kh)
               for (int kw = 0; kw < size; ++kw) {
                 double v = st.w_W[(((size_t)o * st.cin + c) * size + kh) * size + kw];
                 if (st.bn) v *= sc[o];
-                row[(size_t)(kh * size + kw) * st.cin + c] = v;
-                mx = std::max(mx, std::fabs(v));
+                st.wf[(size_t)o * kp + (size_t)(kh * size + kw) * st.cin + c] = (float)v;
               }
-          const double sw = mx > 0 ? mx / 127.0 : 1.0;
-          st.sw[o] = (float)sw;
-          for (size_t k = 0; k < row.size(); ++k) {
-            const long q = std::lround(row[k] / sw);
-            w8[(size_t)o * kp + k] = (int8_t)std::max(-127L, std::min(127L, q));
-          }
-        }
-        st.w8_off = blob.add(w8.data(), w8.size());
+        st.w8_off = blob.add(nullptr, (size_t)cp * kp);
         st.deq_off = blob.add(nullptr, (size_t)cp * sizeof(float));
+        st.inv_off = blob.add(nullptr, (size_t)st.cin * sizeof(float));
         st.q = h.n_q++;
+        st.amax_off = h.q_channels;
+        h.q_channels += st.cin;
+        st.qbuf_off = h.q_bytes;
+        h.q_bytes += (size_t)round_up((int64_t)st.ih * st.iw * st.cin, 256);
       }
     } else {
       st.pc.cout = filters;
@@ -816,10 +815,9 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     h.zero.alloc(256);
     RTDM_HIP(hipMemset(h.zero.p, 0, 256));
     if (h.n_q) {
-      h.amax.alloc((size_t)h.n_q * sizeof(unsigned));
-      RTDM_HIP(hipMemset(h.amax.p, 0, (size_t)h.n_q * sizeof(unsigned)));
-      h.hist.alloc((size_t)h.n_q * kCalBins * sizeof(unsigned));
-      RTDM_HIP(hipMemset(h.hist.p, 0, (size_t)h.n_q * kCalBins * sizeof(unsigned)));
+      h.amax.alloc(h.q_channels * sizeof(unsigned));
+      RTDM_HIP(hipMemset(h.amax.p, 0, h.q_channels * sizeof(unsigned)));
+      h.qarena.alloc(h.q_bytes * h.max_batch);
     }
   }
 }
@@ -943,17 +941,17 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       a.w_stem = h.blob.at<void>(st.pc.stem_off);
       a.zero = h.zero.p;
       if (st.q >= 0 && h.calibrating) {
-        if (h.calibrating == 1)
-          launch_absmax(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, h.amax.as<unsigned>() + st.q, s);
-        else
-          launch_abshist(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, h.amax.as<unsigned>() + st.q,
-                         h.hist.as<unsigned>() + (size_t)st.q * kCalBins, s);
+        launch_chan_absmax(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, h.amax.as<unsigned>() + st.amax_off, s);
         launch_conv(a, h.dtype, s);
       } else if (st.q >= 0) {
+        int8_t* qb = h.qarena.as<int8_t>() + st.qbuf_off * h.max_batch;
+        launch_quantize(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, h.blob.at<float>(st.inv_off), qb, s);
+        a.in = qb;
+        a.in_cs = st.cin;
+        a.in_co = 0;
         a.w8 = h.blob.at<void>(st.w8_off);
         a.deq = h.blob.at<float>(st.deq_off);
-        a.qscale = st.qscale;
-        launch_conv_i8(a, s);
+        launch_conv_pipe_i8(a, s);
       } else {
         launch_conv(a, h.dtype, s);
       }
@@ -1044,7 +1042,13 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     } else if (st.yolo >= 0) {
       a.e.io = (float*)64;
     }
-    name = st.q >= 0 ? "conv_i8" : conv_kernel_name(a, h.dtype);
+    if (st.q >= 0) {
+      a.in_cs = st.cin;
+      a.in_co = 0;
+      a.w8 = (const void*)64;
+      a.deq = (const float*)64;
+    }
+    name = st.q >= 0 ? conv_pipe_i8_name(a) : conv_kernel_name(a, h.dtype);
     flop = 2.0 * st.oh * st.ow * (double)st.cout * st.cin * st.ks * st.ks +
            (st.head ? 2.0 * st.oh * st.ow * (double)st.head_cout * st.cout : 0.0);
     double out = 0;
@@ -1336,62 +1340,52 @@ rtdm_status rtdm_detector_calibrate(rtdm_detector h, const void* x, int x_kind, 
       return;
     }
     const hipStream_t s = (hipStream_t)stream;
-    if (reset) {
-      RTDM_HIP(hipMemsetAsync(h->amax.p, 0, (size_t)h->n_q * sizeof(unsigned), s));
-      RTDM_HIP(hipMemsetAsync(h->hist.p, 0, (size_t)h->n_q * kCalBins * sizeof(unsigned), s));
-    }
+    if (reset) RTDM_HIP(hipMemsetAsync(h->amax.p, 0, h->q_channels * sizeof(unsigned), s));
     if (n > 0) {
       const size_t need = (size_t)h->max_batch * h->n_anchors_total * h->no * sizeof(float);
       if (h->raw_buf.bytes < need) h->raw_buf.alloc(need);
-      // pass 1: |x|max; pass 2: |x| histograms over [0, |x|max] (bins of earlier calls
-      // keep their own range: a later larger max clamps nothing, it only coarsens)
-      for (int pass = 1; pass <= 2; ++pass) {
-        h->calibrating = pass;
-        try {
-          run_detector(*h, x, x_kind, n, h->raw_buf.as<float>(), s);
-        } catch (...) {
-          h->calibrating = 0;
-          throw;
-        }
+      h->calibrating = 1;  // fp16 forward, per-channel |x|max of every int8 conv's input
+      try {
+        run_detector(*h, x, x_kind, n, h->raw_buf.as<float>(), s);
+      } catch (...) {
+        h->calibrating = 0;
+        throw;
       }
       h->calibrating = 0;
     }
-    // scales: the clip c minimising the quantisation MSE of each int8 conv input
-    // (uniform error step^2/12 below c, (|x| - c)^2 above, step = c / 127), over the
-    // histogram; s_x = c / 127; deq[c] = s_x * s_w[c]
-    std::vector<unsigned> am(h->n_q), hc((size_t)h->n_q * kCalBins);
+    // per int8 conv: s_c = |x|max_c / 127 per input channel, folded into the weights
+    // (W'[o][k] = W[o][k] * s_c(k)); symmetric per-output-channel int8 of W':
+    // s_w[o] = max_k |W'[o][k]| / 127, W8 = rint(W' / s_w[o]); deq[o] = s_w[o]
+    std::vector<unsigned> am(h->q_channels);
     RTDM_HIP(hipMemcpyAsync(am.data(), h->amax.p, am.size() * sizeof(unsigned), hipMemcpyDeviceToHost, s));
-    RTDM_HIP(hipMemcpyAsync(hc.data(), h->hist.p, hc.size() * sizeof(unsigned), hipMemcpyDeviceToHost, s));
     RTDM_HIP(hipStreamSynchronize(s));
     for (Step& st : h->steps) {
       if (st.q < 0) continue;
-      float mx;
-      std::memcpy(&mx, &am[st.q], sizeof(float));
-      RTDM_REQUIRE(std::isfinite(mx), RTDM_E_INVALID, "calibrate: non-finite activations");
-      float clip = mx;
-      if (mx > 0.f) {
-        const unsigned* hh = &hc[(size_t)st.q * kCalBins];
-        const double bw = (double)mx / kCalBins;
-        double best = 1e300;
-        for (int t = kCalBins / 16; t <= kCalBins; ++t) {
-          const double c = t * bw, step = c / 127.0;
-          double e = 0.0;
-          for (int b = 0; b < kCalBins; ++b) {
-            if (!hh[b]) continue;
-            const double xc = (b + 0.5) * bw;
-            e += xc < c ? (double)hh[b] * step * step / 12.0 : (double)hh[b] * (xc - c) * (xc - c);
-          }
-          if (e < best) {
-            best = e;
-            clip = (float)c;
-          }
+      const int cin = st.cin, kp = st.pc.kpad, cp = st.pc.cout_pad, cout = st.cout;
+      std::vector<float> sx(cin), inv(cin);
+      for (int c = 0; c < cin; ++c) {
+        float mx;
+        std::memcpy(&mx, &am[st.amax_off + c], sizeof(float));
+        RTDM_REQUIRE(std::isfinite(mx), RTDM_E_INVALID, "calibrate: non-finite activations");
+        sx[c] = mx > 0.f ? mx / 127.f : 1.f;
+        inv[c] = 1.f / sx[c];
+      }
+      std::vector<int8_t> w8((size_t)cp * kp, 0);
+      std::vector<float> dq(cp, 0.f);
+      for (int o = 0; o < cout; ++o) {
+        const float* row = &st.wf[(size_t)o * kp];
+        double mx = 0.0;
+        for (int k = 0; k < kp; ++k) mx = std::max(mx, std::fabs((double)row[k] * sx[k % cin]));
+        const double sw = mx > 0.0 ? mx / 127.0 : 1.0;
+        dq[o] = (float)sw;
+        for (int k = 0; k < kp; ++k) {
+          const long q = std::lround((double)row[k] * sx[k % cin] / sw);
+          w8[(size_t)o * kp + k] = (int8_t)std::max(-127L, std::min(127L, q));
         }
       }
-      const float sx = clip > 0.f ? clip / 127.f : 1.f;
-      st.qscale = 1.f / sx;
-      std::vector<float> dq(st.sw.size());
-      for (size_t c = 0; c < dq.size(); ++c) dq[c] = sx * st.sw[c];
-      RTDM_HIP(hipMemcpy(h->blob.at<float>(st.deq_off), dq.data(), dq.size() * sizeof(float), hipMemcpyHostToDevice));
+      RTDM_HIP(hipMemcpy(h->blob.at<void>(st.w8_off), w8.data(), w8.size(), hipMemcpyHostToDevice));
+      RTDM_HIP(hipMemcpy(h->blob.at<void>(st.deq_off), dq.data(), dq.size() * sizeof(float), hipMemcpyHostToDevice));
+      RTDM_HIP(hipMemcpy(h->blob.at<void>(st.inv_off), inv.data(), inv.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     h->calibrated = true;
   });

@@ -122,10 +122,10 @@ class Darknet(torch.nn.Module):
         return self
 
     def int8(self, calib: torch.Tensor):
-        """int8-quantise the detector (README --quant int8; BASELINE config 5): the Cin % 64
-        convs run on int8 MFMA with per-channel weight scales and per-tensor activation
-        scales calibrated on `calib` (uint8 frames [N,H,W,3] or NCHW inputs on the GPU,
-        kept for handles created later)."""
+        """int8-quantise the detector (README --quant int8; BASELINE config 5): the Cin % 128
+        convs run on int8 MFMA (conv_pipe_i8) with per-input-channel activation scales,
+        calibrated on `calib` (uint8 frames [N,H,W,3] or NCHW inputs on the GPU, kept for
+        handles created later), folded into per-output-channel int8 weights."""
         if not calib.is_cuda:
             raise RuntimeError("calibration frames must be on the GPU")
         self._calib = calib.contiguous()
