@@ -193,12 +193,20 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   const int nk = a.kpad / BKE;
   const int cpt = a.cin / BKE;  // K-blocks per tap
   const int ntap = a.ks * a.ks;
-  int st_tap = 0, st_c = 0, st_buf = 0;
+  // K-block cursor: inner counter st_i (limit ni) and outer st_o; channel-block outer
+  // (pipe_corder) walks the taps inside, tap outer the channel blocks.  Plain scalars
+  // selected by value (a by-reference select of the counter to bump sends the cursor to
+  // scratch, and its loads' vmcnt(0) then drains the LDS-DMA pipeline every K-block).
+  const bool corder = a.pipe_corder != 0;
+  const int ni = corder ? ntap : cpt;
+  int st_i = 0, st_o = 0, st_buf = 0;
 
   // Issue the VM buffer->LDS ops of the next K-block (cursor st_*) into stage st_buf.
   auto stage = [&]() {
     _Float16* As = smem + st_buf * kPStage;
     _Float16* Bs = As + BM * BK;
+    const int st_tap = __builtin_amdgcn_readfirstlane(corder ? st_i : st_o);
+    const int st_c = __builtin_amdgcn_readfirstlane(corder ? st_o : st_i);
     const int kh = a.ks == 3 ? (st_tap * 11) >> 5 : 0, kw = st_tap - kh * a.ks;
     const int tapoff = ((kh * a.iw + kw) * a.in_cs + st_c * BKE) * ES;
 #pragma unroll
@@ -211,14 +219,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     for (int j = 0; j < NB; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j], koff,
                                                0, 0);
-    if (a.pipe_corder) {  // channel-block outer: the taps of one 64-channel slice back to back
-      if (++st_tap == ntap) {
-        st_tap = 0;
-        ++st_c;
-      }
-    } else if (++st_c == cpt) {  // tap outer
-      st_c = 0;
-      ++st_tap;
+    if (++st_i == ni) {
+      st_i = 0;
+      ++st_o;
     }
     st_buf = st_buf == kPNS - 1 ? 0 : st_buf + 1;
   };

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void dw3_sum_kernel(const T* __restrict__ in, 
 // 16-byte reads: 8 pixels x 8 channel vectors = 1 KB contiguous per wave-instruction)
 // instead of L1/L2.  Same sum order as dw3_sum_kernel (bias, branch, kh, kw).
 constexpr int kDwTH = 8, kDwTW = 32, kDwCS = 64;
-__global__ __launch_bounds__(256) void dw3_sum_tile_kernel(const _Float16* __restrict__ in, int in_cs, int in_co,
+__global__ __launch_bounds__(256, 2) void dw3_sum_tile_kernel(const _Float16* __restrict__ in, int in_cs, int in_co,
                                                            int n, int h, int w, int c, const float* __restrict__ wts,
                                                            const float* __restrict__ bsum,
                                                            _Float16* __restrict__ out) {
@@ -248,16 +248,17 @@ __global__ __launch_bounds__(256) void dw3_sum_tile_kernel(const _Float16* __res
 #pragma unroll
       for (int p = 0; p < 4; ++p) acc[p][j] = bj;
     }
-#pragma unroll
-    for (int br = 0; br < 3; ++br) {
-      const int d = br + 1;
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
+    // one (branch, kernel row) per iteration: 3 taps x 4 pixels of operands live at a time
+    // (fully unrolled, the compiler hoisted all 108 LDS reads: 512 registers, 1 wave/SIMD)
+#pragma unroll 1
+    for (int bk = 0; bk < 9; ++bk) {
+      const int br = bk / 3, kh = bk - br * 3, d = br + 1;
+      {
         const int ly = y + 3 + (kh - 1) * d;
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
           const int lx = x0 + 3 + (kw - 1) * d;
-          const float* wp = s_w + (br * 9 + kh * 3 + kw) * kDwCS + g * 8;
+          const float* wp = s_w + (bk * 3 + kw) * kDwCS + g * 8;
           float wv[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) wv[j] = wp[j];

@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
 """Per-dispatch PMC table from tools/pmc_detector.sh output (last iteration of run_detector.py).
-python tools/pmc_table.py TAG [npasses]"""
+python tools/pmc_table.py TAG [npasses]
+
+Columns: us = dispatch time; GHz = GRBM_GUI_ACTIVE / 8 XCDs / wall (effective clock);
+mfma% = SQ_VALU_MFMA_BUSY_CYCLES over all SIMD-cycles (GRBM_GUI_ACTIVE x 128);
+wait/inst/act = SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY shares of SQ_WAVE_CYCLES;
+ldsconf = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; l2hit = TCC_HIT / (TCC_HIT + TCC_MISS)."""
 import sqlite3
 import sys
 
@@ -23,17 +28,24 @@ for rows in zip(*passes):
     for r in rows:
         m.update(r)
     merged.append(m)
-print(f"{'kernel':34s} {'us':>7s} {'waves':>7s} {'valu/w':>8s} {'salu/w':>7s} {'lds/w':>6s} {'vmrd/w':>6s} {'mfma/w':>7s} "
-      f"{'valu/mfma':>9s} {'mfma%':>6s} {'waitI/cyc':>9s} {'wait/cyc':>8s} {'ldsconf':>7s}")
+
+
+def g(m, k, default=0.0):
+    return float(m.get(k, default))
+
+
+print(f"{'kernel':34s} {'us':>7s} {'GHz':>5s} {'waves':>6s} {'mfma/w':>7s} {'mfma%':>6s} {'wait':>5s} {'inst':>5s} "
+      f"{'act':>5s} {'ldsI/w':>6s} {'ldsconf':>7s} {'vmrd/w':>6s} {'valu/w':>7s} {'l2hit':>6s}")
 for m in merged:
-    w = max(1, m.get("SQ_WAVES", 1))
-    mf = m.get("SQ_INSTS_MFMA", 0)
-    busy = m.get("SQ_BUSY_CYCLES", 0)
-    cyc = max(1, m.get("SQ_WAVE_CYCLES", 1))
+    w = max(1.0, g(m, "SQ_WAVES", 1))
+    cyc = max(1.0, g(m, "SQ_WAVE_CYCLES", 1))
+    dur = g(m, "dur") / 1e9
+    ghz = g(m, "GRBM_GUI_ACTIVE") / 8 / dur / 1e9 if dur > 0 and "GRBM_GUI_ACTIVE" in m else 0.0
+    gui = g(m, "GRBM_GUI_ACTIVE")  # summed over the 8 XCDs: x 1024 SIMDs / 8 = SIMD-cycles / 128
+    mf = 100 * g(m, "SQ_VALU_MFMA_BUSY_CYCLES") / max(1.0, gui * 128) if gui else 0.0
+    hit, miss = g(m, "TCC_HIT_sum"), g(m, "TCC_MISS_sum")
     name = m["k"].replace("void ", "").replace("rtdm::", "")[:34]
-    print(f"{name:34s} {m.get('dur', 0)/1000:7.1f} {w:7.0f} {m.get('SQ_INSTS_VALU', 0)/w:8.1f} "
-          f"{m.get('SQ_INSTS_SALU', 0)/w:7.1f} {m.get('SQ_INSTS_LDS', 0)/w:6.1f} {m.get('SQ_INSTS_VMEM_RD', 0)/w:6.1f} "
-          f"{mf/w:7.1f} {m.get('SQ_INSTS_VALU', 0)/max(1, mf):9.2f} "
-          f"{100*m.get('SQ_VALU_MFMA_BUSY_CYCLES', 0)/max(1, busy)/4:6.1f} "
-          f"{m.get('SQ_WAIT_INST_ANY', 0)/cyc:9.3f} {m.get('SQ_WAIT_ANY', 0)/cyc:8.3f} "
-          f"{m.get('SQ_LDS_BANK_CONFLICT', 0)/max(1, m.get('SQ_ACTIVE_INST_LDS', 1)):7.2f}")
+    print(f"{name:34s} {g(m, 'dur') / 1000:7.1f} {ghz:5.2f} {w:6.0f} {g(m, 'SQ_INSTS_MFMA') / w:7.1f} {mf:6.1f} "
+          f"{g(m, 'SQ_WAIT_ANY') / cyc:5.2f} {g(m, 'SQ_WAIT_INST_ANY') / cyc:5.2f} {g(m, 'SQ_ACTIVE_INST_ANY') / cyc:5.2f} "
+          f"{g(m, 'SQ_INSTS_LDS') / w:6.1f} {g(m, 'SQ_LDS_BANK_CONFLICT') / max(1.0, g(m, 'SQ_LDS_IDX_ACTIVE', 1)):7.3f} "
+          f"{g(m, 'SQ_INSTS_VMEM_RD') / w:6.1f} {g(m, 'SQ_INSTS_VALU') / w:7.1f} {hit / max(1.0, hit + miss):6.3f}")
