@@ -179,11 +179,12 @@ def step_table(det, n):
     return h, rows
 
 
-def pmc_traffic(kernel, per_gpu_batch):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary that was
-    measured at this per-GPU batch (profiles/*_traffic.json, written by tools/prof_summary.py
-    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench command;
-    FETCH_SIZE doubled per the gfx950 correction).  None when no pass covers it."""
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of the same
+    workload (profiles/*_traffic.json "_workload": config.workload, dtype, per-GPU batch;
+    written by tools/prof_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    passes over this bench command; FETCH_SIZE doubled per the gfx950 correction).  None
+    when no pass covers it."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))  # tags sort by round
     for path in reversed(files):
@@ -191,13 +192,11 @@ def pmc_traffic(kernel, per_gpu_batch):
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if d.get("_per_gpu_batch", 64) != per_gpu_batch:
+        if d.get("_workload") != workload:
             continue
-        for k, t in d.items():
-            if k.startswith("_") or not isinstance(t, dict):
-                continue
-            if k == kernel and "fetch_size_bytes_avg" in t and "write_size_bytes_avg" in t:
-                return {"bytes_per_launch": t["hbm_bytes_avg"], "source": os.path.relpath(path, ROOT)}
+        t = d.get(kernel)
+        if isinstance(t, dict) and "fetch_size_bytes_avg" in t and "write_size_bytes_avg" in t:
+            return {"bytes_per_launch": t["hbm_bytes_avg"], "source": os.path.relpath(path, ROOT)}
     return None
 
 
@@ -327,6 +326,8 @@ def main():
         counts = torch.cat([unpack_record(gathered[r], pipe, b)["count"].cpu() for r in range(world)])
 
     # ---- roofline: per-launch hipEvents on the detector's launch streams, eager steps ----
+    workload = ((f"two-stage {args.classifier} -> " if args.classifier != "none" else "detection only: ")
+                + f"{args.cfg}@{args.img} + decode + NMS (conf {args.conf}, iou {args.iou})")
     from rtdm import _lib as L
     h, steps = step_table(det, b)
     rl = None
@@ -350,7 +351,7 @@ def main():
         t_ms, flop, byt, launches = agg[dom]
         avg_ms = t_ms / launches
         achieved = (flop / launches) / (avg_ms * 1e-3) / 1e12
-        tr = pmc_traffic(dom, b)
+        tr = pmc_traffic(dom, {"workload": workload, "dtype": args.dtype, "per_gpu_batch": b})
         i8k = "_i8" in dom
         peak = MFMA_I8_DENSE_PEAK_TOPS if i8k else MFMA_F16_DENSE_PEAK_TFLOPS
         rl = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak,
@@ -409,8 +410,7 @@ def main():
         "data": f"synthetic {args.img}x{args.img} uint8 frames (seeded, {len(frames)} rotations), synthetic "
                 f"calibrated detector weights"
                 + (f", the reference's trained {args.classifier} weights" if args.classifier != "none" else ""),
-        "config": {"workload": (f"two-stage {args.classifier} -> " if args.classifier != "none" else "detection only: ")
-                               + f"{args.cfg}@{args.img} + decode + NMS (conf {args.conf}, iou {args.iou})",
+        "config": {"workload": workload,
                    "global_batch": global_batch, "per_gpu_batch": b, "img": args.img,
                    "parallelism": f"dp{world}: frame-sharded global batch"
                                   + (", per-step RCCL gather of every rank's results to rank 0" if world > 1 else ""),

@@ -79,12 +79,26 @@ def main():
             traffic[k]["launches"] = len(v)
     if traffic:
         for k, t in traffic.items():
+            if k.startswith("_"):
+                continue
             t["hbm_bytes_avg"] = t.get("fetch_size_bytes_avg", 0.0) + t.get("write_size_bytes_avg", 0.0)
         lines += ["", "## HBM traffic per launch (PMC passes, FETCH_SIZE ×2 gfx950 correction)", "",
                   "| kernel | launches | read MB | write MB | total MB |", "|---|---|---|---|---|"]
-        for k, t in sorted(traffic.items(), key=lambda kv: -kv[1]["hbm_bytes_avg"]):
+        for k, t in sorted(((k, t) for k, t in traffic.items() if not k.startswith("_")),
+                           key=lambda kv: -kv[1]["hbm_bytes_avg"]):
             lines.append(f"| `{k}` | {t['launches']} | {t.get('fetch_size_bytes_avg', 0)/1e6:.2f} | "
                          f"{t.get('write_size_bytes_avg', 0)/1e6:.2f} | {t['hbm_bytes_avg']/1e6:.2f} |")
+        # the workload the PMC passes ran (bench.py's JSON line in their logs): bench.py only
+        # takes traffic from a summary of the same workload, dtype and per-GPU batch
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            log = os.path.join(a.gpurun, f"pmc_{ctr}_{a.tag}.log")
+            if os.path.exists(log):
+                for line in open(log):
+                    if line.startswith("{"):
+                        d = json.loads(line)
+                        traffic["_workload"] = {"workload": d["config"]["workload"], "dtype": d["dtype"],
+                                                "per_gpu_batch": d["config"]["per_gpu_batch"]}
+                break
         with open(os.path.join(a.out, f"{a.tag}_traffic.json"), "w") as f:
             json.dump(traffic, f, indent=1, sort_keys=True)
     with open(os.path.join(a.out, f"{a.tag}_kernel_stats.md"), "w") as f:
