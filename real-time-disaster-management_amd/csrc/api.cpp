@@ -37,6 +37,8 @@ rtdm_status rtdm_set_tuning(const char* key, int value) {
       set_pipe_korder(value);
     else if (!strcmp(key, "conv_pipe_bm"))
       set_pipe_bm(value);
+    else if (!strcmp(key, "conv_pipe_win"))
+      set_pipe_win(value);
     else if (!strcmp(key, "fuse_head"))
       set_fuse_head(value);
     else if (!strcmp(key, "two_streams"))

@@ -40,6 +40,14 @@ struct PipeCfg {
   static constexpr int Smem = kPNS * Stage * 2 > BM * kPCstr * 4 ? kPNS * Stage * 2 : BM * kPCstr * 4;
 };
 
+// Window mode (3x3 / stride 1 / pad 1, linear row order): per 64-channel block the tile's
+// input rows m_base - W - 1 .. m_base + BM + W (BM + 2W + 2 pixels, at most kWinRows) sit
+// in LDS once; the 9 taps read shifted views of it.  Layout: two window buffers (channel
+// blocks alternate), the 3-stage B ring, a 1 KB zero area (out-of-image taps read it).
+constexpr int kWinRows = 440;
+constexpr int kWinSmem = (2 * kWinRows * kPBK + kPNS * kPBN * kPBK + 8 * kPBK) * 2;
+static_assert(kWinSmem <= 163840, "window LDS");
+
 template <int N>
 __device__ __forceinline__ void wait_vm_lgkm0() {
   if constexpr (N == 6)
@@ -87,6 +95,87 @@ __device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v
   }
 }
 
+// Register epilogue of a lean conv_pipe tile (D^T accumulators: acc[tm][tn][r] = output
+// channel n_base + wn*BN/WN + tn*16 + 4g + r of GEMM row m_base + wm*BM/WM + tm*16 + fr).
+// Same per-element operations, in the same order, as epi_vec8_lean.
+template <bool RES, int FM, int FN, int WM, int WN, int BM, typename AccT, int NDQ>
+__device__ __forceinline__ void pipe_epi_regs(const ConvArgs& a, int m_base, int n_base, int wm, int wn, int lane,
+                                              const AccT (&acc)[FM][FN], const f4 (&rb)[FN], const f4 (&dq4)[NDQ]) {
+  constexpr bool I8 = !std::is_same_v<AccT, f4>;
+  constexpr int BN = kPBN;
+  const Epilogue& e = a.e;
+  const int fr = lane & 15, g = lane >> 4;
+  const bool leaky = e.act == ACT_LEAKY;
+  const float slope = e.slope;
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int tm = 0; tm < FM; ++tm) {
+    const int m = m_base + wm * (BM / WM) + tm * 16 + fr;
+    const bool mv = m < a.M;
+    int n = 0, oy = 0, ox = 0;
+    if (mv) row_to_pix(a, m, n, oy, ox);
+    const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
+#pragma unroll
+    for (int tn = 0; tn < FN; ++tn) {
+      const int c0 = n_base + wn * (BN / WN) + tn * 16 + 4 * g;
+      const bool cv = c0 < a.cout;  // cout % 8 == 0 (epi_lean_ok): all 4 or none
+      f4 t;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (I8)
+          t[r] = (float)acc[tm][tn][r] * dq4[NDQ == FN ? tn : 0][r];
+        else
+          t[r] = acc[tm][tn][r];
+        t[r] = t[r] + rb[tn][r];
+        t[r] = leaky ? (t[r] > 0.f ? t[r] : t[r] * slope) : t[r];
+      }
+      if (e.scale && cv) {
+        const f4 sc = *(const f4*)(e.scale + c0), sh = *(const f4*)(e.shift + c0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[r] = t[r] * sc[r] + sh[r];
+      }
+      if constexpr (RES) {
+        if (mv && cv) {
+          const h4 rv = *(const h4*)((const _Float16*)e.res.ptr + pix * e.res.cs + e.res.co + c0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t[r] += (float)rv[r];
+        }
+      }
+      h4 hv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hv[r] = (_Float16)t[r];
+      if (mv && cv) {
+        if (e.full.ptr) *(h4*)((_Float16*)e.full.ptr + pix * e.full.cs + e.full.co + c0) = hv;
+        if (e.up.ptr) {
+          const int uw = a.ow * 2;
+          const size_t u0 = ((size_t)n * a.oh * 2 + 2 * oy) * uw + 2 * ox;
+          _Float16* up = (_Float16*)e.up.ptr + e.up.co + c0;
+          *(h4*)(up + u0 * e.up.cs) = hv;
+          *(h4*)(up + (u0 + 1) * e.up.cs) = hv;
+          *(h4*)(up + (u0 + uw) * e.up.cs) = hv;
+          *(h4*)(up + (u0 + uw + 1) * e.up.cs) = hv;
+        }
+      }
+      if (e.pool.ptr) {  // quad order: rows 4q..4q+3 = lanes fr 4q..4q+3 (a DPP quad)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = t[r];
+          v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false)));
+          v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)));
+          t[r] = v;
+        }
+        if (mv && cv && (fr & 3) == 0) {
+          const size_t pp = ((size_t)n * a.qh + (oy >> 1)) * a.qw + (ox >> 1);
+          h4 pv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pv[r] = (_Float16)t[r];
+          *(h4*)((_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0) = pv;
+        }
+      }
+    }
+  }
+}
+
 // ABL: ablation bits for diagnostic builds only (outputs are wrong when non-zero):
 // 1 = no buffer->LDS loads in the K-loop, 2 = no fragment ds_reads in the K-loop,
 // 4 = no wait + barrier in the K-loop, 16 = no epilogue (one guarded store keeps the
@@ -99,17 +188,21 @@ __device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v
 // 128-byte LDS rows holding 128 K-elements instead of 64, v_mfma_i32_16x16x64_i8 in place
 // of v_mfma_f32_16x16x32_f16 (same issue count per K-block, twice the K), exact int32
 // sums dequantised per output channel (a.deq) before the unchanged fp32 epilogues.
-template <int ABL, int BM, bool I8 = false>
+// WIN: window mode (see kWinRows): per K-block B ops + ONE window op (a 64-row slice of
+// the next channel block's window, or a dummy zero load into the zero area, so every
+// stage issues the same op count for the counted waits).
+template <int ABL, int BM, bool I8 = false, bool WIN = false>
 __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem_raw, int bid) {
   constexpr int WM = PipeCfg<BM>::WM, WN = PipeCfg<BM>::WN;
   constexpr int BN = kPBN, BK = kPBK;              // LDS row: BK halfs = 128 bytes
   constexpr int ES = I8 ? 1 : 2, BKE = I8 ? 128 : 64;  // element bytes, K-elements per K-block
-  constexpr int kPStage = PipeCfg<BM>::Stage;
+  constexpr int kPStage = WIN ? BN * BK : PipeCfg<BM>::Stage;  // halfs per ring stage
   constexpr int WAVES = WM * WN, NT = 64 * WAVES;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // accumulators per wave
-  constexpr int NA = BM * BK * 2 / (NT * 16);          // A buffer->LDS ops per thread per stage
+  constexpr int NA = WIN ? 1 : BM * BK * 2 / (NT * 16);  // A buffer->LDS ops per thread per stage
   constexpr int NB = BN * BK * 2 / (NT * 16);          // B ops
   constexpr int VM = NA + NB;
+  static_assert(!WIN || BM >= 128, "window mode: 256- / 128-row tiles");
   static_assert(VM == 6 || VM == 4 || VM == 3, "wait literal");
   _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
 
@@ -120,12 +213,27 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   const int mt = bid / ntn;
   const int m_base = mt * BM, n_base = (bid - mt * ntn) * BN;
 
+  // Register epilogue (ABL bit 512, lean layers without pool / upsample outputs, whose
+  // scattered 8-byte stores measured slower than the LDS path): the MFMA operands are swapped (weights as
+  // A, activations as B), so a lane's accumulator holds 4 consecutive output channels
+  // of one pixel (D^T; every output is the same K-ordered dot product, bit-identical)
+  // and bias -> act -> affine -> stores run straight from registers, 8 bytes per lane
+  // per 16x16 block, with the 2x2 pool as two DPP max steps over quad-order rows: no
+  // fp32 C tile through LDS and no barrier between the K-loop and the stores.
+  constexpr bool REG = (ABL & 512) != 0;
   // Epilogue channel constants, loaded at the tile's start so their latency hides under
-  // the K-loop.  Lean epilogue: this thread's 8 channels are the same in both of its
-  // units (NT % CG == 0).  Fused head: the FN columns of this lane's accumulators.
+  // the K-loop.  Register epilogue: the 4 channels (4g..4g+3 of each 16-column block)
+  // of this lane's accumulators.  Fused head: the FN columns of this lane's accumulators.
   constexpr int CG = BN / 8;
   float lb[8], ls[8], lh[8];
-  if constexpr ((ABL & 128) != 0) {
+  f4 rb[REG ? FN : 1];
+  if constexpr (REG) {
+#pragma unroll
+    for (int tn = 0; tn < FN; ++tn) {
+      const int c0 = n_base + wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
+      rb[tn] = c0 < a.cout ? *(const f4*)(a.e.bias + c0) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  } else if constexpr ((ABL & 128) != 0) {
     const int c0 = n_base + (tid % CG) * 8;
     const bool cv = c0 < a.cout;
 #pragma unroll
@@ -136,7 +244,14 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     }
   }
   float dq[FN];  // int8: per-output-channel dequantisation of this lane's accumulator columns
-  if constexpr (I8) {
+  f4 dq4[REG && I8 ? FN : 1];
+  if constexpr (I8 && REG) {
+#pragma unroll
+    for (int tn = 0; tn < FN; ++tn) {
+      const int c0 = n_base + wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
+      dq4[tn] = c0 < a.cout ? *(const f4*)(a.deq + c0) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  } else if constexpr (I8) {
 #pragma unroll
     for (int tn = 0; tn < FN; ++tn) {
       const int col = n_base + wn * (BN / WN) + tn * 16 + (lane & 15);
@@ -159,10 +274,10 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   //      B op j rows 8(NB w + j) + lane/8; LDS slot lane%8 of a row holds k-vector
   //      slot ^ ((row >> 1) & 7) (the read side applies the same involution). ----
   const int slot = lane & 7;
-  int voff_a[NA];
-  uint32_t vmask[NA];
+  int voff_a[WIN ? 1 : NA];
+  uint32_t vmask[WIN ? 1 : NA];
 #pragma unroll
-  for (int j = 0; j < NA; ++j) {
+  for (int j = 0; j < (WIN ? 0 : NA); ++j) {
     const int r = 8 * (NA * wid + j) + (lane >> 3);
     const int kofs = 16 * (slot ^ ((r >> 1) & 7));  // bytes
     const int m = m_base + r;
@@ -201,18 +316,50 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   const int ni = corder ? ntap : cpt;
   int st_i = 0, st_o = 0, st_buf = 0;
 
+  // window mode: buffers, window geometry (rows of the channel block's window: pixels
+  // m_base - W - 1 + row of the flattened batch, zero outside it)
+  _Float16* const Bring = WIN ? smem + 2 * kWinRows * BK : smem;
+  _Float16* const zarea = smem + 2 * kWinRows * BK + kPNS * BN * BK;
+  const int wr = BM + 2 * a.iw + 2;              // window rows used
+  const int npix = a.n * a.ih * a.iw;
+  const int ncb = a.cin / BKE;
+  // one 64-row slice j of channel block cw's window (or a dummy zero load)
+  // (branch-free: a divergent branch here would split the loop body, and the MFMA /
+  // DS-read / VMEM interleave groups do not cross basic blocks)
+  // per-lane row of slice 0 (this wave's 8 rows, lane / 8) and its source offset
+  const int wrow0 = 8 * wid + (lane >> 3);
+  const int wp0 = m_base - a.iw - 1 + wrow0;
+  const int wv0 = wp0 * a.in_cs * ES + 16 * (slot ^ ((wrow0 >> 1) & 7));  // + 64j rows keeps the swizzle
+  auto win_op = [&](int j, int cw, bool live) {
+    const int r0 = 64 * j + 8 * wid;  // this wave's 8 rows
+    const bool real = live & (r0 < kWinRows);
+    _Float16* dst = real ? smem + ((cw & 1) * kWinRows + r0) * BK : zarea;
+    const int p = wp0 + 64 * j;
+    const int vraw = wv0 + (64 * j * a.in_cs + cw * BKE) * ES;
+    const bool ok = real & (wrow0 < wr - 64 * j) & ((unsigned)p < (unsigned)npix);
+    const int vo = vraw | (int)((uint32_t)!ok << 31);  // >= 2^31: out of range, loads 0
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)dst, 16, vo, 0, 0, 0);
+  };
+
   // Issue the VM buffer->LDS ops of the next K-block (cursor st_*) into stage st_buf.
   auto stage = [&]() {
     _Float16* As = smem + st_buf * kPStage;
-    _Float16* Bs = As + BM * BK;
+    _Float16* Bs = WIN ? Bring + st_buf * kPStage : As + BM * BK;
     const int st_tap = __builtin_amdgcn_readfirstlane(corder ? st_i : st_o);
     const int st_c = __builtin_amdgcn_readfirstlane(corder ? st_o : st_i);
     const int kh = a.ks == 3 ? (st_tap * 11) >> 5 : 0, kw = st_tap - kh * a.ks;
-    const int tapoff = ((kh * a.iw + kw) * a.in_cs + st_c * BKE) * ES;
+    if constexpr (WIN) {
+      // K-block s = 9 st_c + st_tap is staged during body s - 2: it carries slice
+      // j = st_tap - 2 (taps 2..8 -> slices 0..6) of channel block st_c + 1's window
+      const int j = st_tap - 2, cw = st_c + 1;
+      win_op(j < 0 ? 0 : j, cw, j >= 0 && cw < ncb && 64 * j < wr);
+    } else {
+      const int tapoff = ((kh * a.iw + kw) * a.in_cs + st_c * BKE) * ES;
 #pragma unroll
-    for (int j = 0; j < NA; ++j) {
-      const int vo = ((vmask[j] >> st_tap) & 1u) ? voff_a[j] + tapoff : (int)0x80000000;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(As + 8 * (NA * wid + j) * BK), 16, vo, 0, 0, 0);
+      for (int j = 0; j < NA; ++j) {
+        const int vo = ((vmask[j] >> st_tap) & 1u) ? voff_a[j] + tapoff : (int)0x80000000;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(As + 8 * (NA * wid + j) * BK), 16, vo, 0, 0, 0);
+      }
     }
     const int koff = (st_tap * a.cin + st_c * BKE) * ES;  // weight column of this K-block (tap-major packing)
 #pragma unroll
@@ -229,7 +376,45 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   const int fr = lane & 15, g = lane >> 4;
   const int rsw = (fr >> 1) & 7;
   const int so0 = 8 * ((0 + g) ^ rsw), so1 = 8 * ((4 + g) ^ rsw);
-  const int a_row = (wm * (BM / WM) + fr) * BK, b_row = (BM + wn * (BN / WN) + fr) * BK;
+  const int a_row = (wm * (BM / WM) + fr) * BK, b_row = ((WIN ? 0 : BM) + wn * (BN / WN) + fr) * BK;
+
+  // window mode read side: validity of the 9 taps for this lane's FM fragment rows
+  // (out-of-image taps, and window rows of a neighbouring image, read the zero area)
+  // and the LDS byte offsets of the next K-block's A fragments (half 1: ^ 64)
+  uint32_t amask[WIN ? FM : 1];
+  int aoff[WIN ? FM : 1];
+  int rd_i = 0, rd_o = 0;  // cursor of the next K-block read0 reads
+  if constexpr (WIN) {
+#pragma unroll
+    for (int tm = 0; tm < FM; ++tm) {
+      const int m = m_base + wm * (BM / WM) + tm * 16 + fr;
+      uint32_t msk = 0;
+      if (m < a.M) {
+        int n, oy, ox;
+        row_to_pix(a, m, n, oy, ox);
+        for (int t = 0; t < 9; ++t) {
+          const int kh = (t * 11) >> 5, kw = t - 3 * kh;
+          if ((unsigned)(oy + kh - 1) < (unsigned)a.ih && (unsigned)(ox + kw - 1) < (unsigned)a.iw) msk |= 1u << t;
+        }
+      }
+      amask[tm] = msk;
+    }
+  }
+  // byte offsets; the 16-row fragment blocks tm share the swizzle of block 0 (rows + 16 tm)
+  const int zoff = (2 * kWinRows * BK + kPNS * BN * BK + 8 * g) * 2;
+  const int wrd0 = wm * (BM / WM) + fr;
+  auto win_addr = [&]() {  // aoff for K-block (rd_o, rd_i), then advance the read cursor
+    const int t = __builtin_amdgcn_readfirstlane(rd_i);
+    const int kh = (t * 11) >> 5, kw = t - 3 * kh;
+    const int i = wrd0 + kh * a.iw + kw;
+    const int off = ((rd_o & 1) * kWinRows + i) * BK * 2 + 16 * (g ^ ((i >> 1) & 7));
+#pragma unroll
+    for (int tm = 0; tm < FM; ++tm) aoff[tm] = ((amask[tm] >> t) & 1u) ? off + tm * 16 * BK * 2 : zoff;
+    if (++rd_i == 9) {
+      rd_i = 0;
+      ++rd_o;
+    }
+  };
 
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   using AccT = std::conditional_t<I8, i32x4, f4>;
@@ -238,7 +423,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = AccT{0, 0, 0, 0};
-  auto mfma = [&](const h8& x, const h8& y, AccT c) -> AccT {
+  auto mfma = [&](const h8& x_, const h8& y_, AccT c) -> AccT {
+    const h8& x = REG ? y_ : x_;  // register epilogue: weights as A (D^T)
+    const h8& y = REG ? x_ : y_;
     if constexpr (I8)
       return __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, x), __builtin_bit_cast(i32x4, y), c, 0, 0,
                                                    0);
@@ -248,16 +435,26 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 
   h8 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
   auto read0 = [&](int buf) {
-    const _Float16* S = smem + buf * kPStage;
+    const _Float16* S = (WIN ? Bring : smem) + buf * kPStage;
+    if constexpr (WIN) {
 #pragma unroll
-    for (int t = 0; t < FM; ++t) fa0[t] = *(const h8*)(S + a_row + t * 16 * BK + so0);
+      for (int t = 0; t < FM; ++t) fa0[t] = *(const h8*)(smem_raw + aoff[t]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < FM; ++t) fa0[t] = *(const h8*)(S + a_row + t * 16 * BK + so0);
+    }
 #pragma unroll
     for (int t = 0; t < FN; ++t) fb0[t] = *(const h8*)(S + b_row + t * 16 * BK + so0);
   };
   auto read1 = [&](int buf) {
-    const _Float16* S = smem + buf * kPStage;
+    const _Float16* S = (WIN ? Bring : smem) + buf * kPStage;
+    if constexpr (WIN) {
 #pragma unroll
-    for (int t = 0; t < FM; ++t) fa1[t] = *(const h8*)(S + a_row + t * 16 * BK + so1);
+      for (int t = 0; t < FM; ++t) fa1[t] = *(const h8*)(smem_raw + (aoff[t] ^ 64));
+    } else {
+#pragma unroll
+      for (int t = 0; t < FM; ++t) fa1[t] = *(const h8*)(S + a_row + t * 16 * BK + so1);
+    }
 #pragma unroll
     for (int t = 0; t < FN; ++t) fb1[t] = *(const h8*)(S + b_row + t * 16 * BK + so1);
   };
@@ -272,7 +469,12 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     }
   };
 
-  // prologue: K-blocks 0 and 1 in flight, wait for 0
+  // prologue: (window mode: channel block 0's whole window,) K-blocks 0 and 1 in flight,
+  // wait for 0
+  if constexpr (WIN) {
+    for (int j = 0; 64 * j < wr; ++j) win_op(j, 0, true);
+    win_addr();
+  }
   stage();
   if (nk > 1) {
     stage();
@@ -322,6 +524,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NXT && WIN) win_addr();
     if constexpr (NXT) {
       // retire kb+1 (kb+2 stays in flight); lgkmcnt(0): this stage's reads are done
       // in every wave before any wave restages it (kb+3, issued after this barrier)
@@ -351,6 +554,10 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     for (int kb = 0; kb + 2 < nk; ++kb) body(T_{}, T_{});
     if (nk >= 2) body(F_{}, T_{});
     body(F_{}, F_{});
+  }
+  if constexpr (REG) {
+    pipe_epi_regs<(ABL & 256) != 0, FM, FN, WM, WN, BM>(a, m_base, n_base, wm, wn, lane, acc, rb, dq4);
+    return;
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
@@ -477,36 +684,52 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 // XCD (A panels shared in that XCD's L2), so a tile's epilogue stores drain while the
 // next tile's first K-blocks load, instead of every CU storing, then loading, in
 // lockstep rounds.  Between tiles only LDS is fenced (lgkmcnt): the stores stay in flight.
-template <int ABL, int BM>
-__global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a, int ntiles) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[PipeCfg<BM>::Smem];
+template <int ABL, int BM, bool I8, bool WIN>
+__device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem_raw, int ntiles) {
   const int nb = gridDim.x, xcd = blockIdx.x & 7, l = blockIdx.x >> 3;
   const int q = ntiles >> 3, r = ntiles & 7;
   const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   const int hi = lo + q + (xcd < r ? 1 : 0);
   const int bx = (nb - xcd + 7) >> 3;  // workgroups on this XCD (>= 1: this one)
+  if constexpr (WIN) {  // the zero area: written once, outside every epilogue's LDS use
+    if (threadIdx.x < 64) {
+      u32x4* z = reinterpret_cast<u32x4*>(smem_raw + (2 * kWinRows * kPBK + kPNS * kPBN * kPBK) * 2);
+      z[threadIdx.x] = u32x4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();
+  }
   for (int t = lo + l; t < hi; t += bx) {
-    pipe_tile<ABL, BM>(a, smem_raw, t);
+    pipe_tile<ABL, BM, I8, WIN>(a, smem_raw, t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
 }
+template <int BM, bool WIN>
+constexpr int pipe_smem() {
+  return WIN && kWinSmem > PipeCfg<BM>::Smem ? kWinSmem : PipeCfg<BM>::Smem;
+}
 
-
-// int8 twin of conv_pipe_f16 (same persistent XCD walk)
+template <int ABL, int BM>
+__global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a, int ntiles) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[pipe_smem<BM, false>()];
+  pipe_walk<ABL, BM, false, false>(a, smem_raw, ntiles);
+}
+// window mode (3x3 / s1 / p1, linear rows): see kWinRows
+template <int ABL, int BM>
+__global__ __launch_bounds__(512, 1) void conv_pipew_f16(ConvArgs a, int ntiles) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[pipe_smem<BM, true>()];
+  pipe_walk<ABL, BM, false, true>(a, smem_raw, ntiles);
+}
+// int8 twins (same persistent XCD walk)
 template <int ABL, int BM>
 __global__ __launch_bounds__(512, 1) void conv_pipe_i8(ConvArgs a, int ntiles) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[PipeCfg<BM>::Smem];
-  const int nb = gridDim.x, xcd = blockIdx.x & 7, l = blockIdx.x >> 3;
-  const int q = ntiles >> 3, r = ntiles & 7;
-  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  const int hi = lo + q + (xcd < r ? 1 : 0);
-  const int bx = (nb - xcd + 7) >> 3;
-  for (int t = lo + l; t < hi; t += bx) {
-    pipe_tile<ABL, BM, true>(a, smem_raw, t);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[pipe_smem<BM, false>()];
+  pipe_walk<ABL, BM, true, false>(a, smem_raw, ntiles);
+}
+template <int ABL, int BM>
+__global__ __launch_bounds__(512, 1) void conv_pipew_i8(ConvArgs a, int ntiles) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[pipe_smem<BM, true>()];
+  pipe_walk<ABL, BM, true, true>(a, smem_raw, ntiles);
 }
 
 bool conv_pipe_ok(const ConvArgs& a) {
@@ -567,26 +790,91 @@ static int pipe_bm_nk(const ConvArgs& a, int nk) {
   return best;
 }
 
-template <int BM>
-static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid) {
-  if (a.head_w) {
-    if constexpr (BM >= 128) hipLaunchKernelGGL((conv_pipe_f16<8, BM>), grid, dim3(512), 0, s, a, ntiles);
-  } else if (epi_lean_ok(a)) {
-    hipLaunchKernelGGL((conv_pipe_f16<128, BM>), grid, dim3(512), 0, s, a, ntiles);
-  } else if (epi_lean_ok(a, true)) {
-    hipLaunchKernelGGL((conv_pipe_f16<384, BM>), grid, dim3(512), 0, s, a, ntiles);
-  } else {
-    hipLaunchKernelGGL((conv_pipe_f16<0, BM>), grid, dim3(512), 0, s, a, ntiles);
+static int g_pipe_korder = 1;
+void set_pipe_korder(int v) { g_pipe_korder = v ? 1 : 0; }
+static int g_pipe_korder_get() { return g_pipe_korder; }
+
+// Epilogue instantiation (ABL) of a launch: 8 fused head; lean layers 640 (register
+// epilogue) / 128 (LDS C tile: layers with pool or upsample outputs), +256 with the fused
+// shortcut add; 0 the generic epilogue.
+static int pipe_abl(const ConvArgs& a) {
+  if (a.head_w) return 8;
+  const int reg = !a.e.pool.ptr && !a.e.up.ptr ? 512 : 0;
+  if (epi_lean_ok(a)) return 128 | reg;
+  if (epi_lean_ok(a, true)) return 384 | reg;
+  return 0;
+}
+
+// Window mode eligibility (3x3 / s1 / p1 over a linear-order NHWC input whose window of
+// BM + 2W + 2 rows fits kWinRows; channel-block-outer K order; 256-row tiles: with the
+// 128-row tiles' 16 MFMAs per K-block the window addressing VALU costs more than the
+// A loads it saves, measured +10 % on yolov4-tiny L10 / L14).  rtdm_set_tuning("conv_pipe_win", 0)
+// turns it off (bit-identical either way).
+static int g_pipe_win = 1;
+void set_pipe_win(int v) { g_pipe_win = v ? 1 : 0; }
+static bool pipe_win_ok(const ConvArgs& a, int bm) {
+  return g_pipe_win && bm == 256 && a.ks == 3 && a.stride == 1 && a.pad == 1 && !a.quad && a.pipe_corder &&
+         a.ih == a.oh && a.iw == a.ow && bm + 2 * a.iw + 2 <= kWinRows;
+}
+
+#define RTDM_PIPE_KERNEL(NAME)                                                                  \
+  template <int ABL, int BM>                                                                    \
+  struct NAME##_k {                                                                             \
+    static void go(dim3 g, hipStream_t s, const ConvArgs& a, int nt) {                          \
+      hipLaunchKernelGGL((NAME<ABL, BM>), g, dim3(512), 0, s, a, nt);                          \
+    }                                                                                           \
+  };
+RTDM_PIPE_KERNEL(conv_pipe_f16)
+RTDM_PIPE_KERNEL(conv_pipew_f16)
+RTDM_PIPE_KERNEL(conv_pipe_i8)
+RTDM_PIPE_KERNEL(conv_pipew_i8)
+#undef RTDM_PIPE_KERNEL
+
+template <template <int, int> class K, int BM>
+static void launch_abl(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int nt) {
+  switch (abl) {
+    case 8:
+      if constexpr (BM >= 128) K<8, BM>::go(g, s, a, nt);
+      break;
+    case 128: K<128, BM>::go(g, s, a, nt); break;
+    case 384: K<384, BM>::go(g, s, a, nt); break;
+    case 640: K<640, BM>::go(g, s, a, nt); break;
+    case 896: K<896, BM>::go(g, s, a, nt); break;
+    default: K<0, BM>::go(g, s, a, nt); break;
   }
 }
 
-const char* conv_pipe_name(const ConvArgs& a) {
+template <int BM>
+static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid, bool win) {
+  if constexpr (BM >= 128) {
+    if (win) return launch_abl<conv_pipew_f16_k, BM>(pipe_abl(a), grid, s, a, ntiles);
+  }
+  launch_abl<conv_pipe_f16_k, BM>(pipe_abl(a), grid, s, a, ntiles);
+}
+
+static const char* pipe_name(bool i8, bool win, int abl, int bm) {
+  static char buf[4][2][6][3][32];
+  static bool init = false;
+  static const int abls[6] = {8, 128, 384, 640, 896, 0};
+  static const int bms[3] = {256, 128, 64};
+  if (!init) {
+    for (int q = 0; q < 4; ++q)
+      for (int k = 0; k < 6; ++k)
+        for (int b = 0; b < 3; ++b)
+          snprintf(buf[q][0][k][b], 32, "conv_pipe%s_%s<%d,%d>", (q & 1) ? "w" : "", (q & 2) ? "i8" : "f16", abls[k], bms[b]);
+    init = true;
+  }
+  int k = 0, b = 0;
+  while (k < 5 && abls[k] != abl) ++k;
+  while (b < 2 && bms[b] != bm) ++b;
+  return buf[(i8 ? 2 : 0) | (win ? 1 : 0)][0][k][b];
+}
+
+const char* conv_pipe_name(const ConvArgs& a_in) {
+  ConvArgs a = a_in;
+  a.pipe_corder = g_pipe_korder_get() && a.ks == 3 ? 1 : 0;
   const int bm = pipe_bm(a);
-  if (a.head_w) return bm == 256 ? "conv_pipe_f16<8,256>" : "conv_pipe_f16<8,128>";
-  if (epi_lean_ok(a)) return bm == 256 ? "conv_pipe_f16<128,256>" : bm == 128 ? "conv_pipe_f16<128,128>" : "conv_pipe_f16<128,64>";
-  if (epi_lean_ok(a, true))
-    return bm == 256 ? "conv_pipe_f16<384,256>" : bm == 128 ? "conv_pipe_f16<384,128>" : "conv_pipe_f16<384,64>";
-  return bm == 256 ? "conv_pipe_f16<0,256>" : bm == 128 ? "conv_pipe_f16<0,128>" : "conv_pipe_f16<0,64>";
+  return pipe_name(false, pipe_win_ok(a, bm), pipe_abl(a), bm);
 }
 
 // K order of the implicit GEMM: 0 = tap outer (each tap's whole channel run), 1 = 64-channel
@@ -594,8 +882,6 @@ const char* conv_pipe_name(const ConvArgs& a) {
 // a tap re-reads are the slice's: an L2 working set of 1/(cin/64) of the tap-outer one).
 // rtdm_set_tuning("conv_pipe_korder", v).  Changes the fp32 summation order (not batch
 // invariance): results differ from the other order in the last bits.
-static int g_pipe_korder = 1;
-void set_pipe_korder(int v) { g_pipe_korder = v ? 1 : 0; }
 
 void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
   ConvArgs a = a_in;
@@ -618,14 +904,16 @@ void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
     case 9: hipLaunchKernelGGL((conv_pipe_f16<48, 256>), grid, dim3(512), 0, s, a, ntiles); break;
     case 10: hipLaunchKernelGGL((conv_pipe_f16<96, 256>), grid, dim3(512), 0, s, a, ntiles); break;
     case 11: hipLaunchKernelGGL((conv_pipe_f16<0, 256>), grid, dim3(512), 0, s, a, ntiles); break;
-    default:
+    default: {
+      const bool win = pipe_win_ok(a, bm);
       if (bm == 256)
-        launch_pipe_bm<256>(a, s, ntiles, grid);
+        launch_pipe_bm<256>(a, s, ntiles, grid, win);
       else if (bm == 128)
-        launch_pipe_bm<128>(a, s, ntiles, grid);
+        launch_pipe_bm<128>(a, s, ntiles, grid, win);
       else
-        launch_pipe_bm<64>(a, s, ntiles, grid);
+        launch_pipe_bm<64>(a, s, ntiles, grid, false);
       break;
+    }
   }
 }
 
@@ -642,26 +930,11 @@ bool conv_pipe_i8_ok(const ConvArgs& a) {
   return true;
 }
 
-const char* conv_pipe_i8_name(const ConvArgs& a) {
+const char* conv_pipe_i8_name(const ConvArgs& a_in) {
+  ConvArgs a = a_in;
+  a.pipe_corder = g_pipe_korder && a.ks == 3 ? 1 : 0;
   const int bm = pipe_bm_nk(a, a.kpad / 128);
-  if (a.head_w) return bm == 256 ? "conv_pipe_i8<8,256>" : "conv_pipe_i8<8,128>";
-  if (epi_lean_ok(a)) return bm == 256 ? "conv_pipe_i8<128,256>" : bm == 128 ? "conv_pipe_i8<128,128>" : "conv_pipe_i8<128,64>";
-  if (epi_lean_ok(a, true))
-    return bm == 256 ? "conv_pipe_i8<384,256>" : bm == 128 ? "conv_pipe_i8<384,128>" : "conv_pipe_i8<384,64>";
-  return bm == 256 ? "conv_pipe_i8<0,256>" : bm == 128 ? "conv_pipe_i8<0,128>" : "conv_pipe_i8<0,64>";
-}
-
-template <int BM>
-static void launch_pipe_i8_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid) {
-  if (a.head_w) {
-    if constexpr (BM >= 128) hipLaunchKernelGGL((conv_pipe_i8<8, BM>), grid, dim3(512), 0, s, a, ntiles);
-  } else if (epi_lean_ok(a)) {
-    hipLaunchKernelGGL((conv_pipe_i8<128, BM>), grid, dim3(512), 0, s, a, ntiles);
-  } else if (epi_lean_ok(a, true)) {
-    hipLaunchKernelGGL((conv_pipe_i8<384, BM>), grid, dim3(512), 0, s, a, ntiles);
-  } else {
-    hipLaunchKernelGGL((conv_pipe_i8<0, BM>), grid, dim3(512), 0, s, a, ntiles);
-  }
+  return pipe_name(true, pipe_win_ok(a, bm), pipe_abl(a), bm);
 }
 
 void launch_conv_pipe_i8(const ConvArgs& a_in, hipStream_t s) {
@@ -673,12 +946,21 @@ void launch_conv_pipe_i8(const ConvArgs& a_in, hipStream_t s) {
   RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
   const int ntiles = (int)nt;
   const dim3 grid((unsigned)(ntiles < pipe_cus() ? ntiles : pipe_cus()));
-  if (bm == 256)
-    launch_pipe_i8_bm<256>(a, s, ntiles, grid);
-  else if (bm == 128)
-    launch_pipe_i8_bm<128>(a, s, ntiles, grid);
-  else
-    launch_pipe_i8_bm<64>(a, s, ntiles, grid);
+  const bool win = pipe_win_ok(a, bm);
+  const int abl = pipe_abl(a);
+  if (bm == 256) {
+    if (win)
+      launch_abl<conv_pipew_i8_k, 256>(abl, grid, s, a, ntiles);
+    else
+      launch_abl<conv_pipe_i8_k, 256>(abl, grid, s, a, ntiles);
+  } else if (bm == 128) {
+    if (win)
+      launch_abl<conv_pipew_i8_k, 128>(abl, grid, s, a, ntiles);
+    else
+      launch_abl<conv_pipe_i8_k, 128>(abl, grid, s, a, ntiles);
+  } else {
+    launch_abl<conv_pipe_i8_k, 64>(abl, grid, s, a, ntiles);
+  }
   RTDM_HIP(hipGetLastError());
 }
 

@@ -92,7 +92,7 @@ def test_int8_detector_vs_scheme_model(dev, case, nframes):
         nm = ctypes.create_string_buffer(64)
         L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, None, None, None))
         names.append(nm.value.decode())
-    n_i8 = sum(n.startswith("conv_pipe_i8") for n in names)
+    n_i8 = sum(n.startswith(("conv_pipe_i8", "conv_pipew_i8")) for n in names)
     assert n_i8 >= 8, names  # L8..L28 incl. the fused head conv
 
     ref = DarknetRef(text, stream)

@@ -190,7 +190,7 @@ def test_fp16_io_within_storage_floor(dev, case):
 @pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416"])
 @pytest.mark.parametrize("bm", [128, 64])
 def test_pipe_tile_rows_bit_identical(dev, case, bm):
-    """conv_pipe_f16 with 128- / 64-row tiles (picked for small per-rank batches) gives
+    """conv_pipe with 128- / 64-row tiles (picked for small per-rank batches) gives
     the same io bits as the 256-row tiles: only the tiling changes, never the K order."""
     from rtdm import _lib as L
     from rtdm.synth import synth_frames
@@ -208,28 +208,60 @@ def test_pipe_tile_rows_bit_identical(dev, case, bm):
     assert torch.equal(outs[256], outs[bm])
 
 
-def test_lean_residual_epilogue_bit_identical(dev):
-    """The lean conv_pipe epilogue with the fused shortcut add (Darknet-53 residual
-    blocks, conv_pipe_f16<384,*>) gives the same io bits as the generic epilogue
-    (rtdm_set_tuning("conv_pipe", 11): generic epi_vec8 everywhere, 256-row tiles)."""
+@pytest.mark.parametrize("case", ["yolov3-aider-416@416", "yolov4-tiny-aider-416@608"])
+def test_lean_window_epilogues_bit_identical(dev, case):
+    """The production conv_pipe kernels give the same io bits as the generic one
+    (rtdm_set_tuning("conv_pipe", 11): per-tap A loads, unswapped MFMA operands, fp32 C
+    tile through LDS, epi_vec8 everywhere, 256-row tiles):
+      * window mode (conv_pipew_*: 3x3 / s1 inputs staged in LDS once per 64-channel
+        block, the 9 taps read shifted views, out-of-image taps read a zero area);
+      * the register epilogue (ABL 640 / 896: swapped MFMA operands, so a lane holds 4
+        channels of one pixel; bias / act / affine, the fused shortcut add of the
+        Darknet-53 residual blocks, stores straight from registers);
+      * the lean LDS epilogue of the pooled / upsampled layers (ABL 128)."""
+    import ctypes
     from rtdm import _lib as L
     from rtdm.synth import synth_frames
-    x = torch.from_numpy(synth_frames(2, 416, 416, seed=23)).to(dev)
+    cfg, size = case.split("@")
+    size = int(size)
+    x = torch.from_numpy(synth_frames(2, size, size, seed=23)).to(dev)
     outs = {}
     try:
         for mode in (11, 1):
             L.check(L.lib().rtdm_set_tuning(b"conv_pipe", mode))
-            m, _, _, _ = _detector("yolov3-aider-416", 416)
+            m, _, _, _ = _detector(cfg, size)
             outs[mode] = m(x)[0].cpu()
             if mode == 1:
                 h = m.handle(2)
                 names = set()
-                import ctypes
                 for i in range(L.lib().rtdm_detector_num_steps(h)):
                     nm = ctypes.create_string_buffer(64)
                     L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, None, None, None))
                     names.add(nm.value.decode())
-                assert any(n.startswith("conv_pipe_f16<384,") for n in names), names
+                want = ("<896,",) if cfg.startswith("yolov3") else ("<640,", "conv_pipe_f16<128,")
+                for w in want:
+                    assert any(w in n for n in names), (w, names)
+                assert any(n.startswith("conv_pipew_f16<") for n in names), names
     finally:
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe", 1))
     assert torch.equal(outs[11], outs[1])
+
+
+@pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416"])
+def test_window_mode_bit_identical(dev, case):
+    """conv_pipe window mode on / off (rtdm_set_tuning("conv_pipe_win")) at b3: same io bits
+    (tiles spanning image boundaries, image edges, the last partial tile)."""
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    cfg, size = case.split("@")
+    size = int(size)
+    x = torch.from_numpy(synth_frames(3, size, size, seed=29)).to(dev)
+    outs = {}
+    try:
+        for v in (0, 1):
+            L.check(L.lib().rtdm_set_tuning(b"conv_pipe_win", v))
+            m, _, _, _ = _detector(cfg, size)
+            outs[v] = m(x)[0].cpu()
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_win", 1))
+    assert torch.equal(outs[0], outs[1])
