@@ -363,6 +363,16 @@ def main():
               "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tr["source"] if tr else None,
               "timing": f"hipEvents around each detector launch on its launch stream, {calls.value} eager steps "
                         f"after the timed region"}
+        # the whole implicit-GEMM family (every conv_pipe / conv_pipew instantiation: the
+        # dominant symbol above is one epilogue / tiling variant of it)
+        fam = [k for k in agg if k.startswith(("conv_pipe_", "conv_pipew_"))]
+        if fam:
+            f_ms = sum(agg[k][0] for k in fam)
+            f_flop = sum(agg[k][1] for k in fam)
+            f_ach = f_flop / (f_ms * 1e-3) / 1e12
+            rl["family"] = {"kernels": "conv_pipe*/conv_pipew* (all MFMA implicit-GEMM convs)",
+                            "achieved": round(f_ach, 2), "frac": round(f_ach / peak, 4),
+                            "ms_per_step": round(f_ms / max(1, calls.value), 4)}
         if rank == 0:
             per_step = {f"L{layer}:{name}": round(t / max(1, calls.value), 4)
                         for (name, layer, flop, byt), t in zip(steps, ms)}

@@ -291,15 +291,31 @@ __device__ __forceinline__ float fma_mix_hi(float w, uint32_t x2, float acc) {
   asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "s"(w), "v"(x2), "v"(acc));
   return d;
 }
+// the same with the weight in a VGPR (broadcast from LDS)
+__device__ __forceinline__ float fma_mix_lo_v(float w, uint32_t x2, float acc) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(d) : "v"(w), "v"(x2), "v"(acc));
+  return d;
+}
+__device__ __forceinline__ float fma_mix_hi_v(float w, uint32_t x2, float acc) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(w), "v"(x2), "v"(acc));
+  return d;
+}
+constexpr int kAcffPMaxCin = 128;  // depthwise taps + biases of the whole layer in LDS
 
 template <int CC, int NF, int ABL = 0>  // ABL (diagnostics, wrong outputs): 1 no taps, 2 no GEMM
-__global__ __launch_bounds__(256, 2) void acff_persist(AcffPArgs a) {
+__global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a) {  // NF 2: <= 168 VGPRs, 3 waves / SIMD
   using G = AcffPGeom<CC>;
   constexpr int TH = G::TH, TW = G::TW, HW = G::HW, PS = G::PS, CG = G::CG, KC = G::KC, AS = G::AS;
   constexpr int HALO = G::HALO, PV = G::PV, XS = G::XS;
   __shared__ __attribute__((aligned(16))) _Float16 xs[2 * XS];
   __shared__ __attribute__((aligned(16))) _Float16 At[G::NPIX * AS];
+  // depthwise taps [27][cin] then biases [3][cin]: LDS broadcast reads, pipelined by the
+  // compiler (as wave-uniform scalar loads every tap waited on its own s_load latency)
+  extern __shared__ __attribute__((aligned(16))) float s_dw[];  // dynamic: 30 * cin floats
   const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < 30 * a.cin; i += 256) s_dw[i] = i < 27 * a.cin ? a.dw_wt[i] : a.dw_b[i - 27 * a.cin];
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, g = lane >> 4;
   const int oh = a.h - 2, ow = a.w - 2;
@@ -390,10 +406,16 @@ __global__ __launch_bounds__(256, 2) void acff_persist(AcffPArgs a) {
 #pragma unroll
         for (int br = 0; br < 3; ++br) {
           const int d = br + 1;
-          const cfloat_p bp = (cfloat_p)(a.dw_b + br * a.cin + cbase);
+          const float* bp = s_dw + (27 + br) * a.cin + cbase;
           float s8[8];
+          {
+            const f4 b0 = *(const f4*)bp, b1 = *(const f4*)(bp + 4);
 #pragma unroll
-          for (int jj = 0; jj < 8; ++jj) s8[jj] = bp[jj];
+            for (int jj = 0; jj < 4; ++jj) {
+              s8[jj] = b0[jj];
+              s8[4 + jj] = b1[jj];
+            }
+          }
 #pragma unroll
           for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
@@ -401,11 +423,13 @@ __global__ __launch_bounds__(256, 2) void acff_persist(AcffPArgs a) {
               if constexpr ((ABL & 1) != 0) continue;
               const int hr = py + 3 + (kh - 1) * d, hc = px + 3 + (kw - 1) * d;
               const u32x4 xv = *(const u32x4*)(xb + (hr * HW + hc) * PS + cg * 8);
-              const cfloat_p wp = (cfloat_p)(a.dw_wt + (size_t)(br * 9 + kh * 3 + kw) * a.cin + cbase);
+              const float* wp = s_dw + (br * 9 + kh * 3 + kw) * a.cin + cbase;
+              const f4 w0 = *(const f4*)wp, w1 = *(const f4*)(wp + 4);
+              const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
 #pragma unroll
               for (int jj = 0; jj < 4; ++jj) {
-                s8[2 * jj] = fma_mix_lo(wp[2 * jj], xv[jj], s8[2 * jj]);
-                s8[2 * jj + 1] = fma_mix_hi(wp[2 * jj + 1], xv[jj], s8[2 * jj + 1]);
+                s8[2 * jj] = fma_mix_lo_v(wv[2 * jj], xv[jj], s8[2 * jj]);
+                s8[2 * jj + 1] = fma_mix_hi_v(wv[2 * jj + 1], xv[jj], s8[2 * jj + 1]);
               }
             }
           h8 o;
@@ -505,6 +529,7 @@ void set_acff_persist_mode(int v) { g_acff_persist = v < 0 ? 0 : v; }
 int acff_persist_chunk(int cin, int cout_pad, int oh) {
   if (cout_pad != 64 && cout_pad != 128) return 0;
   if (oh < 24) return 0;  // small maps: 8 x 16 tiles would mostly idle
+  if (cin > kAcffPMaxCin) return 0;
   // 16-channel chunks for every cin: (CC = 32 chunks need ~40 more VGPRs and spill)
   return cin % 16 == 0 ? 16 : 0;
 }
@@ -544,11 +569,12 @@ void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int
   RTDM_REQUIRE(tiles < (1ll << 31), RTDM_E_CAPACITY, "acff_persist: too many tiles");
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const size_t lds = (size_t)30 * cin * sizeof(float);
   auto go = [&](auto kern) {
     int per_cu = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
     const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cus);
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, a);
   };
   const int abl = acff_persist_mode() - 1;  // >1: diagnostic ablations
   if (cc == 16) {
