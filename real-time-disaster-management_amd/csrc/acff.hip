@@ -726,6 +726,17 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
       const int d = br + 1;
       const float* wb = wsm + br * 9 * C;
       const float* bb = wsm + 27 * C + br * C;
+      // this branch's 1x1 weight fragments (global, L2-resident), issued before the
+      // depthwise phase so their latency hides under it (C <= 128: 4 k-steps)
+      const _Float16* wrow = st.pw + (size_t)(n_base + fr) * st.kpad + br * C + g * 8;
+      const int nks = C / 32;
+      h8 bpre[4][2];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        if (ks < nks && C <= 128) {
+          bpre[ks][0] = *(const h8*)(wrow + ks * 32);
+          bpre[ks][1] = *(const h8*)(wrow + (size_t)16 * st.kpad + ks * 32);
+        }
       for (int i = tid; i < M * CG; i += kChainThreads) {
         const int m = i / CG, v = i - m * CG;
         const int oy = m / OH, ox = m - oy * OH;
@@ -758,10 +769,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
       }
       __syncthreads();
       // this branch's K slice: k = br*C + [0, C)
-      const _Float16* wrow = st.pw + (size_t)(n_base + fr) * st.kpad + br * C + g * 8;
-      for (int ks = 0; ks < C / 32; ++ks) {
-        const h8 b0 = *(const h8*)(wrow + ks * 32);
-        const h8 b1 = *(const h8*)(wrow + (size_t)16 * st.kpad + ks * 32);
+      auto kstep = [&](int ks, const h8& b0, const h8& b1) {
 #pragma unroll
         for (int tm = 0; tm < 4; ++tm) {
           if (tm < fm && m_base + tm * 16 < M) {
@@ -771,6 +779,14 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
             acc[tm][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b1, acc[tm][1], 0, 0, 0);
           }
         }
+      };
+      if (C <= 128) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          if (ks < nks) kstep(ks, bpre[ks][0], bpre[ks][1]);
+      } else {
+        for (int ks = 0; ks < nks; ++ks)
+          kstep(ks, *(const h8*)(wrow + ks * 32), *(const h8*)(wrow + (size_t)16 * st.kpad + ks * 32));
       }
       __syncthreads();  // the A chunk is rewritten by the next branch
     }

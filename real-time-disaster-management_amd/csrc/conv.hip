@@ -20,6 +20,8 @@
 // (disaster_detection/model/acff.py:49-53, BN applied as a post-activation affine).
 #include "conv_epi.h"
 
+#include <type_traits>
+
 #include <algorithm>
 
 namespace rtdm {
@@ -351,34 +353,65 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
     const uint2* rowk0 = stem_lds + (ly * s + kh0) * cols;
     const uint2* rowk2 = stem_lds + (ly * s + 2) * cols;
     _Float16* pool_row = (_Float16*)e.pool.ptr + ((size_t)n * qh + py) * qw * e.pool.cs + e.pool.co;
-    for (int tx = wid & 1; tx * 4 < qw; tx += 2) {
-      const int qx = tx * 4 + (p >> 2);
-      const int ox = 2 * (qx < qw ? qx : qw - 1) + (d & 1);
-      const int lx = ox * s - pad + 1;
-      const uint2 b00 = rowk0[lx + 2 * pr0], b01 = rowk0[lx + 2 * pr0 + 1];
-      uint2 b10 = rowk2[lx + 2 * (g & 1)], b11 = rowk2[lx + 2 * (g & 1) + 1];
-      if (g >= 2) b10 = b11 = make_uint2(0u, 0u);
-      const h8 bf0 = __builtin_bit_cast(h8, (u32x4{b00.x, b00.y, b01.x, b01.y}));
-      const h8 bf1 = __builtin_bit_cast(h8, (u32x4{b10.x, b10.y, b11.x, b11.y}));
-      const int oq = tx * 4 + g;  // pooled x of this lane's output quad
+    // Darknet stem (no BN affine after the fold, LeakyReLU / linear): LeakyReLU as
+    // max(x, slope x) (0 < slope < 1; 1 = linear), no per-value branches
+    const bool lean = !e.scale && act != ACT_SWISH && (act != ACT_LEAKY || (slope > 0.f && slope <= 1.f));
+    const float slp = act == ACT_LEAKY ? slope : 1.f;
+    // two 4-quad tiles per iteration (tx, tx + 2): two independent LDS -> MFMA -> epilogue
+    // chains per wave instead of one latency-bound chain; the loop is unswitched on `lean`
+    auto run = [&](auto lean_c) {
+    constexpr bool LEAN = decltype(lean_c)::value;
+    for (int tx0 = wid & 1; tx0 * 4 < qw; tx0 += 4) {
+      h8 bf0[2], bf1[2];
+      int oq[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int tx = tx0 + 2 * u;
+        const int qx = tx * 4 + (p >> 2);
+        const int ox = 2 * (qx < qw ? qx : qw - 1) + (d & 1);
+        const int lx = ox * s - pad + 1;
+        const uint2 b00 = rowk0[lx + 2 * pr0], b01 = rowk0[lx + 2 * pr0 + 1];
+        uint2 b10 = rowk2[lx + 2 * (g & 1)], b11 = rowk2[lx + 2 * (g & 1) + 1];
+        if (g >= 2) b10 = b11 = make_uint2(0u, 0u);
+        bf0[u] = __builtin_bit_cast(h8, (u32x4{b00.x, b00.y, b01.x, b01.y}));
+        bf1[u] = __builtin_bit_cast(h8, (u32x4{b10.x, b10.y, b11.x, b11.y}));
+        oq[u] = tx * 4 + g;  // pooled x of this lane's output quad
+      }
 #pragma unroll
       for (int t = 0; t < NTN; ++t) {
-        f4 acc;
-        if constexpr ((ABL & 4) != 0) {
-          acc = f4{(float)bf0[0], (float)bf0[1], (float)bf1[2], (float)bf1[3]};
-        } else {
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf0, wa[t][0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1, wa[t][1], acc, 0, 0, 0);
+        f4 acc[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if constexpr ((ABL & 4) != 0) {
+            acc[u] = f4{(float)bf0[u][0], (float)bf0[u][1], (float)bf1[u][2], (float)bf1[u][3]};
+          } else {
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf0[u], wa[t][0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1[u], wa[t][1], acc[u], 0, 0, 0);
+          }
         }
-        // bias, LeakyReLU/linear and the positive 1/255 scale are monotone non-decreasing
-        // (and so is their fp32 rounding): pool first, then one epilogue per quad
-        const float m = e.scale || act == ACT_SWISH
-                            ? fmaxf(fmaxf(epi(acc[0], t, 0), epi(acc[1], t, 0)), fmaxf(epi(acc[2], t, 0), epi(acc[3], t, 0)))
-                            : epi(fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])), t, 0);
         const int c = 16 * t + p;
-        if (oq < qw && c < a.cout && (!(ABL & 2) || m == 12345.f)) pool_row[(size_t)oq * e.pool.cs + c] = (_Float16)m;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          // bias, LeakyReLU/linear and the positive 1/255 scale are monotone non-decreasing
+          // (and so is their fp32 rounding): pool first, then one epilogue per quad
+          float m;
+          if constexpr (LEAN) {
+            const float x = fmaxf(fmaxf(acc[u][0], acc[u][1]), fmaxf(acc[u][2], acc[u][3])) * in_scale + bias[t][0];
+            m = fmaxf(x, x * slp) + 0.f;  // + 0: epi's "* 1 + 0" affine (-0 -> +0), bit-identical
+          } else {
+            m = e.scale || act == ACT_SWISH
+                    ? fmaxf(fmaxf(epi(acc[u][0], t, 0), epi(acc[u][1], t, 0)), fmaxf(epi(acc[u][2], t, 0), epi(acc[u][3], t, 0)))
+                    : epi(fmaxf(fmaxf(acc[u][0], acc[u][1]), fmaxf(acc[u][2], acc[u][3])), t, 0);
+          }
+          if (oq[u] < qw && c < a.cout && (!(ABL & 2) || m == 12345.f)) pool_row[(size_t)oq[u] * e.pool.cs + c] = (_Float16)m;
+        }
       }
     }
+    };
+    if (lean)
+      run(std::true_type{});
+    else
+      run(std::false_type{});
   } else {
     const int tiles_x = (a.ow + 15) >> 4;
     const int ntiles = tiles_x * ROWS;
@@ -1049,37 +1082,46 @@ __global__ __launch_bounds__(256) void conv3_pool_small(ConvArgs a) {
     for (int r = 0; r < 4; ++r) bias[t][r] = a.e.bias ? a.e.bias[co0 + 16 * t + 4 * g + r] : 0.f;
 
   const _Float16* __restrict__ in = (const _Float16*)a.in + a.in_co;
+  // per-thread halo slots, fixed across tiles: (row, column) of the 16-byte vector k and
+  // its LDS offset (the prefetch addressing was ~30 VALU per vector when recomputed)
+  int hr[PV], hc[PV], hoff[PV], soff[PV];
+#pragma unroll
+  for (int k = 0; k < PV; ++k) {
+    const int i = tid + 256 * k;
+    const int pix = i / CG, v = i - pix * CG;
+    hr[k] = i < HALO ? pix / HW : -(1 << 20);  // out of range: never loaded
+    hc[k] = pix - (pix / HW) * HW;
+    hoff[k] = v * 8;
+    soff[k] = pix * PS + v * 8;
+  }
+  const int img = a.ih * a.iw * a.in_cs;  // halfs per image (< 2^31: planner limits)
   u32x4 pre[PV];
   auto prefetch = [&](int tile) {
     const int tx = tile % tiles_x, t1 = tile / tiles_x;
     const int ty = t1 % tiles_y, n = t1 / tiles_y;
+    const _Float16* base = in + (size_t)n * img;
+    const int y0 = ty * TH - 1, x0 = tx * TW - 1;
 #pragma unroll
     for (int k = 0; k < PV; ++k) {
-      const int i = tid + 256 * k;
-      const int pix = i / CG, v = i - pix * CG;
-      const int r = pix / HW, c = pix - r * HW;
-      const int y = ty * TH - 1 + r, x = tx * TW - 1 + c;
+      const int y = y0 + hr[k], x = x0 + hc[k];
       u32x4 d = {0u, 0u, 0u, 0u};
-      if (i < HALO && (unsigned)y < (unsigned)a.ih && (unsigned)x < (unsigned)a.iw)
-        d = *(const u32x4*)(in + ((size_t)(n * a.ih + y) * a.iw + x) * a.in_cs + v * 8);
+      if ((unsigned)y < (unsigned)a.ih && (unsigned)x < (unsigned)a.iw)
+        d = *(const u32x4*)(base + (y * a.iw + x) * a.in_cs + hoff[k]);
       pre[k] = d;
     }
   };
   const Epilogue& e = a.e;
   const int qh = a.oh >> 1, qw = a.ow >> 1;
+  // LeakyReLU as max(x, slope x) (0 < slope < 1; slope 1 = linear): same values, no branch
+  const float slope = e.act == ACT_LEAKY ? e.slope : 1.f;
   int buf = 0;
   int tile = blockIdx.x;
   if (tile < ntiles) prefetch(tile);
   for (; tile < ntiles; tile += gridDim.x) {
     _Float16* xb_w = xs + buf * XS;
 #pragma unroll
-    for (int k = 0; k < PV; ++k) {
-      const int i = tid + 256 * k;
-      if (i < HALO) {
-        const int pix = i / CG, v = i - pix * CG;
-        *(u32x4*)(xb_w + pix * PS + v * 8) = pre[k];
-      }
-    }
+    for (int k = 0; k < PV; ++k)
+      if (tid + 256 * k < HALO) *(u32x4*)(xb_w + soff[k]) = pre[k];
     __syncthreads();
     const int tx = tile % tiles_x, t1 = tile / tiles_x;
     const int ty = t1 % tiles_y, n = t1 / tiles_y;
@@ -1101,27 +1143,28 @@ __global__ __launch_bounds__(256) void conv3_pool_small(ConvArgs a) {
           acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][t], b, acc[j][t], 0, 0, 0);
       }
     }
-    // pooled epilogue: lane = pixel column ox0 + p, rows j; channels co0 + 16t + 4g + r
+    // pooled epilogue: lane = pixel column ox0 + p, rows j; channels co0 + 16t + 4g + r.
+    // One pooled-row pointer per tile; rows j step by qw pixels.
     const int px = (tx * TW + p) >> 1;
+    const int py0 = (ty * TH + wr * WROWS) >> 1;
+    _Float16* const prow = (_Float16*)e.pool.ptr + e.pool.co + co0 + 4 * g +
+                           ((size_t)(n * qh + py0) * qw + px) * e.pool.cs;
+    const bool lane_st = (p & 1) == 0 && px < qw;
 #pragma unroll
-    for (int t = 0; t < WCH; ++t) {
-      const int c0 = co0 + 16 * t + 4 * g;
+    for (int j = 0; j < WROWS; j += 2) {
+      const bool st = lane_st && py0 + j / 2 < qh;
 #pragma unroll
-      for (int j = 0; j < WROWS; j += 2) {
+      for (int t = 0; t < WCH; ++t) {
         float m[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float t2 = fmaxf(acc[j][t][r], acc[j + 1][t][r]);
-          float x = fmaxf(t2, dpp_xor1(t2)) + bias[t][r];
-          if (e.act == ACT_LEAKY) x = x > 0.f ? x : x * e.slope;
-          m[r] = x;
+          const float x = fmaxf(t2, dpp_xor1(t2)) + bias[t][r];
+          m[r] = fmaxf(x, x * slope);
         }
-        const int py = (ty * TH + wr * WROWS + j) >> 1;
-        if ((p & 1) == 0 && py < qh && px < qw) {
-          const size_t pp = ((size_t)n * qh + py) * qw + px;
-          *(uint2*)((_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0) =
+        if (st)
+          *(uint2*)(prow + (size_t)(j / 2) * qw * e.pool.cs + 16 * t) =
               make_uint2(pack_h2(m[0], m[1]), pack_h2(m[2], m[3]));
-        }
       }
     }
     buf ^= 1;
@@ -1135,6 +1178,8 @@ static bool pool_small_ok(const ConvArgs& a) {
   if (!a.e.pool.ptr || a.e.full.ptr || a.e.up.ptr || a.e.res.ptr || a.e.io || a.e.scale || a.e.act == ACT_SWISH)
     return false;
   if ((a.e.pool.cs | a.e.pool.co) & 3) return false;
+  if (a.e.act == ACT_LEAKY && !(a.e.slope > 0.f && a.e.slope <= 1.f)) return false;  // max(x, slope x)
+  if ((int64_t)a.ih * a.iw * a.in_cs >= (1ll << 31)) return false;                  // 32-bit image offsets
   return a.kpad >= 32 * ((9 * a.cin / 8 + 3) / 4);  // weights read up to k = 32 * NKS
 }
 

@@ -1021,6 +1021,7 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
     conv_set_rows(a);
     a.e.bias = (const float*)64;
     a.e.act = st.act;
+    a.e.slope = st.slope;  // kernel choice depends on it (pool_small_ok)
     if (st.pc.s_off != SIZE_MAX) {
       a.e.scale = (const float*)64;
       a.e.shift = (const float*)64;

@@ -227,6 +227,7 @@ def test_lean_window_epilogues_bit_identical(dev, case):
     x = torch.from_numpy(synth_frames(2, size, size, seed=23)).to(dev)
     outs = {}
     try:
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 256))  # window mode runs on 256-row tiles
         for mode in (11, 1):
             L.check(L.lib().rtdm_set_tuning(b"conv_pipe", mode))
             m, _, _, _ = _detector(cfg, size)
@@ -244,6 +245,7 @@ def test_lean_window_epilogues_bit_identical(dev, case):
                 assert any(n.startswith("conv_pipew_f16<") for n in names), names
     finally:
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe", 1))
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
     assert torch.equal(outs[11], outs[1])
 
 
@@ -255,13 +257,23 @@ def test_window_mode_bit_identical(dev, case):
     from rtdm.synth import synth_frames
     cfg, size = case.split("@")
     size = int(size)
+    import ctypes
     x = torch.from_numpy(synth_frames(3, size, size, seed=29)).to(dev)
     outs = {}
     try:
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 256))  # window mode runs on 256-row tiles
         for v in (0, 1):
             L.check(L.lib().rtdm_set_tuning(b"conv_pipe_win", v))
             m, _, _, _ = _detector(cfg, size)
             outs[v] = m(x)[0].cpu()
+            h = m.handle(3)
+            names = set()
+            for i in range(L.lib().rtdm_detector_num_steps(h)):
+                nm = ctypes.create_string_buffer(64)
+                L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, None, None, None))
+                names.add(nm.value.decode())
+            assert any(n.startswith("conv_pipew_") for n in names) == bool(v), names
     finally:
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe_win", 1))
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
     assert torch.equal(outs[0], outs[1])
