@@ -686,6 +686,7 @@ struct AcffChainArgs {
   const float* fcb;
   float* logits;
   float* probs;
+  int abl;  // diagnostics (wrong outputs): 1 no depthwise, 2 no 1x1 MFMA, 4 no tail
 };
 
 __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
@@ -707,10 +708,47 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
   }
   int cur = 0;
   const int fr = lane & 15, g = lane >> 4;
+  // depthwise taps + biases of a stage -> wsm.  Stage 0 here; stage si + 1's are loaded into
+  // registers while stage si runs and stored once its last depthwise phase is done (each
+  // stage used to start by waiting on these global loads).
+  constexpr int kWPre = (30 * 128 + kChainThreads - 1) / kChainThreads;  // cin <= 128
+  auto wload = [&](const AcffChainStage& st, float (&pre)[kWPre]) {
+#pragma unroll
+    for (int k = 0; k < kWPre; ++k) {
+      const int i = tid + k * kChainThreads;
+      pre[k] = i < 27 * st.cin ? st.dw_wt[i] : (i < 30 * st.cin ? st.dw_b[i - 27 * st.cin] : 0.f);
+    }
+  };
+  auto wstore = [&](const AcffChainStage& st, const float (&pre)[kWPre]) {
+#pragma unroll
+    for (int k = 0; k < kWPre; ++k) {
+      const int i = tid + k * kChainThreads;
+      if (i < 30 * st.cin) wsm[i] = pre[k];
+    }
+  };
+  if (a.nst > 0) {
+    float pre0[kWPre];
+    wload(a.st[0], pre0);
+    wstore(a.st[0], pre0);
+  }
   for (int si = 0; si < a.nst; ++si) {
     const AcffChainStage& st = a.st[si];
     const int H = st.h, OH = H - 2, M = OH * OH, C = st.cin, CG = C >> 3, AS = C + 8;
-    for (int i = tid; i < 30 * C; i += kChainThreads) wsm[i] = i < 27 * C ? st.dw_wt[i] : st.dw_b[i - 27 * C];
+    float wpre[kWPre];
+    if (si + 1 < a.nst) wload(a.st[si + 1], wpre);
+    // this lane's epilogue constants (2 channels), loaded now so the epilogue does not wait
+    float e_b[2], e_s[2], e_t[2];
+    {
+      const int wn0 = st.cout_pad >> 5, wni0 = wid - (wid / wn0) * wn0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = wni0 * 32 + j * 16 + fr;
+        const bool cv = c < st.cout;
+        e_b[j] = cv ? st.bias[c] : 0.f;
+        e_s[j] = cv && st.scale ? st.scale[c] : 1.f;
+        e_t[j] = cv && st.scale ? st.shift[c] : 0.f;
+      }
+    }
     __syncthreads();  // input map + dw weights ready; the previous stage's A reads are done
     const _Float16* X = buf[cur];
     _Float16* Y = buf[cur ^ 1];
@@ -737,7 +775,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
           bpre[ks][0] = *(const h8*)(wrow + ks * 32);
           bpre[ks][1] = *(const h8*)(wrow + (size_t)16 * st.kpad + ks * 32);
         }
-      for (int i = tid; i < M * CG; i += kChainThreads) {
+      for (int i = tid; i < ((a.abl & 1) ? 0 : M * CG); i += kChainThreads) {
         const int m = i / CG, v = i - m * CG;
         const int oy = m / OH, ox = m - oy * OH;
         float t[8];
@@ -780,7 +818,8 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
           }
         }
       };
-      if (C <= 128) {
+      if (a.abl & 2) {
+      } else if (C <= 128) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
           if (ks < nks) kstep(ks, bpre[ks][0], bpre[ks][1]);
@@ -788,6 +827,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
         for (int ks = 0; ks < nks; ++ks)
           kstep(ks, *(const h8*)(wrow + ks * 32), *(const h8*)(wrow + (size_t)16 * st.kpad + ks * 32));
       }
+      if (br == 2 && si + 1 < a.nst) wstore(a.st[si + 1], wpre);  // this stage's taps are no longer read
       __syncthreads();  // the A chunk is rewritten by the next branch
     }
     // epilogue: bias -> LeakyReLU -> BN affine -> fp16 map Y [M][cout]
@@ -795,9 +835,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     for (int j = 0; j < 2; ++j) {
       const int c = n_base + j * 16 + fr;
       if (c >= st.cout) continue;
-      const float bc = st.bias[c];
-      const float sc = st.scale ? st.scale[c] : 1.f;
-      const float sh = st.scale ? st.shift[c] : 0.f;
+      const float bc = e_b[j], sc = e_s[j], sh = e_t[j];
 #pragma unroll
       for (int tm = 0; tm < 4; ++tm) {
         if (!(tm < fm)) continue;
@@ -815,26 +853,31 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     cur ^= 1;
   }
   __syncthreads();
+  if (a.abl & 4) return;
   // ---- tail on the last map: [hw][c], c = last cout ----
   const int h = a.nst > 0 ? a.st[a.nst - 1].h - 2 : a.st[0].h, hw = h * h;
   const int c = a.nst > 0 ? a.st[a.nst - 1].cout : a.st[0].cin;
   const _Float16* X = buf[cur];
   float* conv = (float*)At;  // [5][hw]
-  for (int p = wid; p < hw; p += kChainThreads / 64) {
+  // conv2 1x1 (c -> 5): one (output, pixel) pair per thread, weights from LDS, four partial
+  // sums over the channels (was a wave per pixel with shuffle reductions)
+  float* w2s = wsm;  // [5][c], the stage taps are dead
+  for (int i = tid; i < 5 * c; i += kChainThreads) w2s[i] = a.w2[i];
+  __syncthreads();
+  for (int t = tid; t < 5 * hw; t += kChainThreads) {
+    const int o = t / hw, p = t - o * hw;
     const _Float16* x = X + (size_t)p * c;
-    float s5[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int ch = lane; ch < c; ch += 64) {
-      const float xv = (float)x[ch];
+    const float* w = w2s + o * c;
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int ch = 0; ch < c; ch += 8) {
+      const h8 xv = *(const h8*)(x + ch);
+      const f4 w0 = *(const f4*)(w + ch), w1 = *(const f4*)(w + ch + 4);
 #pragma unroll
-      for (int o = 0; o < 5; ++o) s5[o] = fmaf(xv, a.w2[(size_t)o * c + ch], s5[o]);
+      for (int j = 0; j < 4; ++j) s4[j] = fmaf((float)xv[j], w0[j], s4[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s4[j] = fmaf((float)xv[4 + j], w1[j], s4[j]);
     }
-#pragma unroll
-    for (int o = 0; o < 5; ++o) {
-      float v = s5[o];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-      if (lane == 0) conv[o * hw + p] = v;
-    }
+    conv[o * hw + p] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   }
   __syncthreads();
   float* feat = conv + 5 * hw;  // [5*ph*pw]
@@ -908,6 +951,10 @@ bool acff_chain_ok(const AcffChainPlan& p) {
   }
   const int oh = p.h[p.nst - 1] - 2;
   if (oh * oh > 64 * 16) return false;
+  int cmax = 0;
+  for (int i = 0; i < p.nst; ++i) cmax = std::max(cmax, p.cin[i]);
+  const int clast = p.cout[p.nst - 1];
+  if (cmax > 128 || clast % 8 != 0 || 5 * clast > 30 * cmax) return false;  // register prefetch, tail in wsm
   return acff_chain_lds(p) <= 160 * 1024;
 }
 
@@ -925,6 +972,7 @@ void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in
   a.in_cs = in_cs;
   a.in_co = in_co;
   a.nst = acff_chain_mode() == 2 ? 0 : p.nst;  // 2: tail only (diagnostics; stages skipped -> wrong)
+  a.abl = acff_chain_mode() >= 8 ? (acff_chain_mode() - 8) & 7 : 0;  // 8 + bits: ablations (diagnostics)
   for (int i = 0; i < p.nst; ++i) {
     AcffChainStage& t = a.st[i];
     t.dw_wt = dw_wt[i];
