@@ -675,6 +675,8 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       for (int j = 0; j < 8; ++j) v[r][j] = Cs[(q * 4 + r) * kPCstr + gg * 8 + j];
     if constexpr ((ABL & 128) != 0)
       epi_vec8_lean<(ABL & 256) != 0>(a, m0, c0, v, lb, ls, lh);
+    else if constexpr ((ABL & 1024) != 0)
+      epi_vec8_io(a, m0, c0, v);  // stand-alone YOLO head: decode -> io only
     else
       epi_vec8(a, m0, c0, v);
   }
@@ -794,11 +796,13 @@ static int g_pipe_korder = 1;
 void set_pipe_korder(int v) { g_pipe_korder = v ? 1 : 0; }
 static int g_pipe_korder_get() { return g_pipe_korder; }
 
-// Epilogue instantiation (ABL) of a launch: 8 fused head; lean layers 640 (register
+// Epilogue instantiation (ABL) of a launch: 8 fused head; 1024 stand-alone YOLO head
+// (decode into io only, epi_vec8_io); lean layers 640 (register
 // epilogue) / 128 (LDS C tile: layers with pool or upsample outputs), +256 with the fused
 // shortcut add; 0 the generic epilogue.
 static int pipe_abl(const ConvArgs& a) {
   if (a.head_w) return 8;
+  if (epi_io_ok(a)) return 1024;
   const int reg = !a.e.pool.ptr && !a.e.up.ptr ? 512 : 0;
   if (epi_lean_ok(a)) return 128 | reg;
   if (epi_lean_ok(a, true)) return 384 | reg;
@@ -840,6 +844,7 @@ static void launch_abl(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int nt
     case 384: K<384, BM>::go(g, s, a, nt); break;
     case 640: K<640, BM>::go(g, s, a, nt); break;
     case 896: K<896, BM>::go(g, s, a, nt); break;
+    case 1024: K<1024, BM>::go(g, s, a, nt); break;
     default: K<0, BM>::go(g, s, a, nt); break;
   }
 }
@@ -853,19 +858,19 @@ static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 gr
 }
 
 static const char* pipe_name(bool i8, bool win, int abl, int bm) {
-  static char buf[4][2][6][3][32];
+  static char buf[4][2][7][3][32];
   static bool init = false;
-  static const int abls[6] = {8, 128, 384, 640, 896, 0};
+  static const int abls[7] = {8, 128, 384, 640, 896, 1024, 0};
   static const int bms[3] = {256, 128, 64};
   if (!init) {
     for (int q = 0; q < 4; ++q)
-      for (int k = 0; k < 6; ++k)
+      for (int k = 0; k < 7; ++k)
         for (int b = 0; b < 3; ++b)
           snprintf(buf[q][0][k][b], 32, "conv_pipe%s_%s<%d,%d>", (q & 1) ? "w" : "", (q & 2) ? "i8" : "f16", abls[k], bms[b]);
     init = true;
   }
   int k = 0, b = 0;
-  while (k < 5 && abls[k] != abl) ++k;
+  while (k < 6 && abls[k] != abl) ++k;
   while (b < 2 && bms[b] != bm) ++b;
   return buf[(i8 ? 2 : 0) | (win ? 1 : 0)][0][k][b];
 }

@@ -727,6 +727,13 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     }
     const int filters = st.cout, size = st.ks;
     const bool stem = f16 && st.in_t < 0 && st.cin == 3 && size == 3 && (st.stride == 1 || st.stride == 2) && st.pad <= 1;
+    // stand-alone YOLO head convs (1x1 -> 3|4 x (5 + nc), decode epilogue) whose input
+    // conv_pipe takes: padded to one 128-channel N tile so they run on conv_pipe (io
+    // epilogue) instead of the small-tile conv_mfma (b8 L15: 27 -> ~6 us)
+    const int pad_to = use_mfma && st.yolo >= 0 && !st.head && !st.acff && filters <= 128 && st.cin % 64 == 0 &&
+                               (size == 1 || size == 3)
+                           ? 128
+                           : 0;
     if (weights) {
       std::vector<double> sc(filters, 1.0);
       std::vector<float> b(filters);
@@ -739,7 +746,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         }
       }
       st.pc = pack_conv(blob, st.acff ? st.a_W.data() : st.w_W, filters, st.cin, size, st.bn ? sc.data() : nullptr,
-                        use_mfma);
+                        use_mfma, pad_to);
       st.pc.b_off = blob.add_f32(b);
       if (st.acff) {  // BatchNorm2d after the LeakyReLU (acff.py order), eps 1e-5
         std::vector<float> as(filters), at(filters);
@@ -801,7 +808,7 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       st.pc.ks = size;
       st.pc.mfma = use_mfma;
       st.pc.kpad = (int)round_up((int64_t)size * size * st.cin, 64);
-      st.pc.cout_pad = cout_pad_for(filters);
+      st.pc.cout_pad = pad_to > 0 ? pad_to : cout_pad_for(filters);
       if (stem) st.pc.stem_off = 0;  // planning only: marks the stem kernel for step_info
     }
     st.w_beta = st.w_gamma = st.w_mean = st.w_var = st.w_bias = st.w_W = nullptr;

@@ -61,14 +61,15 @@ inline size_t pack_stem(Blob& blob, const float* w, int cout, const double* osca
 // w: OIHW fp32 [cout][cin][ks][ks]; oscale: optional per-out-channel multiplier
 // (folded BN).  K index = (kh*ks + kw)*cin + c so each tap is a contiguous NHWC
 // channel slice.
-inline PackedConv pack_conv(Blob& blob, const float* w, int cout, int cin, int ks, const double* oscale, bool mfma) {
+inline PackedConv pack_conv(Blob& blob, const float* w, int cout, int cin, int ks, const double* oscale, bool mfma,
+                            int cout_pad = 0) {
   PackedConv p;
   p.cout = cout;
   p.cin = cin;
   p.ks = ks;
   p.mfma = mfma;
   p.kpad = (int)round_up((int64_t)ks * ks * cin, 64);
-  p.cout_pad = cout_pad_for(cout);
+  p.cout_pad = cout_pad > 0 ? cout_pad : cout_pad_for(cout);
   const size_t nel = (size_t)p.cout_pad * p.kpad;
   if (mfma) {
     std::vector<_Float16> h(nel, (_Float16)0.f);
