@@ -33,11 +33,14 @@ namespace rtdm {
 namespace {
 constexpr int kPBN = 128, kPBK = 64, kPNS = 3;
 constexpr int kPCstr = kPBN + 4;
+// NS: LDS stages (the ring code takes any NS >= 3; deeper rings for the 128- / 64-row
+// tiles, 4 x 32 KB / 6 x 24 KB, measured no faster at b8: r02an).
 template <int BM>
 struct PipeCfg {
   static constexpr int WM = BM == 256 ? 4 : 2, WN = 8 / WM;
+  static constexpr int NS = 3;
   static constexpr int Stage = (BM + kPBN) * kPBK;  // halfs per stage
-  static constexpr int Smem = kPNS * Stage * 2 > BM * kPCstr * 4 ? kPNS * Stage * 2 : BM * kPCstr * 4;
+  static constexpr int Smem = NS * Stage * 2 > BM * kPCstr * 4 ? NS * Stage * 2 : BM * kPCstr * 4;
 };
 
 // Window mode (3x3 / stride 1 / pad 1, linear row order): per 64-channel block the tile's
@@ -58,6 +61,8 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
     asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
   else if constexpr (N == 12)
     asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 8)
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
   else
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
@@ -202,6 +207,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   constexpr int NA = WIN ? 1 : BM * BK * 2 / (NT * 16);  // A buffer->LDS ops per thread per stage
   constexpr int NB = BN * BK * 2 / (NT * 16);          // B ops
   constexpr int VM = NA + NB;
+  constexpr int NSt = WIN ? kPNS : PipeCfg<BM>::NS;  // LDS ring stages (window mode: the 3-stage B ring)
+  constexpr int WAITN = (NSt - 2) * VM;               // ops of the stages younger than kb+1
+  static_assert(WAITN == 3 || WAITN == 6 || WAITN == 8 || WAITN == 12, "wait literal");
   static_assert(!WIN || BM >= 128, "window mode: 256- / 128-row tiles");
   static_assert(VM == 6 || VM == 4 || VM == 3, "wait literal");
   _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
@@ -370,7 +378,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       st_i = 0;
       ++st_o;
     }
-    st_buf = st_buf == kPNS - 1 ? 0 : st_buf + 1;
+    st_buf = st_buf == NSt - 1 ? 0 : st_buf + 1;
   };
 
   const int fr = lane & 15, g = lane >> 4;
@@ -475,11 +483,12 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     for (int j = 0; 64 * j < wr; ++j) win_op(j, 0, true);
     win_addr();
   }
-  stage();
-  if (nk > 1) {
-    stage();
-    wait_vm_lgkm0<VM>();
+  if (nk >= NSt - 1) {
+#pragma unroll
+    for (int i = 0; i < NSt - 1; ++i) stage();
+    wait_vm_lgkm0<WAITN>();
   } else {
+    for (int i = 0; i < nk; ++i) stage();
     wait_vm_lgkm0<0>();
   }
   __builtin_amdgcn_s_barrier();
@@ -487,15 +496,15 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   read0(0);
 
   // Cluster A (half 0 of kb): MFMAs on fa0/fb0, interleaved with the reads of half 1
-  // (fa1/fb1) and the buffer->LDS loads of kb+2.  Cluster B (half 1): MFMAs on
+  // (fa1/fb1) and the buffer->LDS loads of kb+NSt-1.  Cluster B (half 1): MFMAs on
   // fa1/fb1, interleaved with the reads of half 0 of kb+1 (after the barrier that
   // publishes kb+1).  The loop is peeled so the steady-state body is one basic
-  // block (interleave groups do not cross branches): STG = loads of kb+2 go out,
+  // block (interleave groups do not cross branches): STG = loads of kb+NSt-1 go out,
   // NXT = kb+1 exists (wait for it, barrier, read its half 0).
   int cur = 0;
   auto body = [&](auto stg, auto nxt_c) {
     constexpr bool STG = decltype(stg)::value, NXT = decltype(nxt_c)::value;
-    const int nxt = cur == kPNS - 1 ? 0 : cur + 1;
+    const int nxt = cur == NSt - 1 ? 0 : cur + 1;
     if constexpr (!(ABL & 2)) read1(cur);
     if constexpr (STG && !(ABL & 1)) stage();
 #pragma unroll
@@ -530,7 +539,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       // in every wave before any wave restages it (kb+3, issued after this barrier)
       if constexpr (!(ABL & 4)) {
         if constexpr (STG)
-          wait_vm_lgkm0<VM>();
+          wait_vm_lgkm0<WAITN>();
         else
           wait_vm_lgkm0<0>();
         __builtin_amdgcn_s_barrier();
@@ -551,8 +560,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   using T_ = std::true_type;
   using F_ = std::false_type;
   if constexpr (!(ABL & 32)) {
-    for (int kb = 0; kb + 2 < nk; ++kb) body(T_{}, T_{});
-    if (nk >= 2) body(F_{}, T_{});
+    int kb = 0;
+    for (; kb + NSt - 1 < nk; ++kb) body(T_{}, T_{});  // stages kb + NSt - 1
+    for (; kb + 1 < nk; ++kb) body(F_{}, T_{});        // tail: nothing left to stage (waits vmcnt(0))
     body(F_{}, F_{});
   }
   if constexpr (REG) {
