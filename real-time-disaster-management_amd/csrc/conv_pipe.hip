@@ -209,7 +209,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   constexpr int VM = NA + NB;
   constexpr int NSt = WIN ? kPNS : PipeCfg<BM>::NS;  // LDS ring stages (window mode: the 3-stage B ring)
   constexpr int WAITN = (NSt - 2) * VM;               // ops of the stages younger than kb+1
-  static_assert(WAITN == 3 || WAITN == 6 || WAITN == 8 || WAITN == 12, "wait literal");
+  static_assert(WAITN == 3 || WAITN == 4 || WAITN == 6 || WAITN == 8 || WAITN == 12, "wait literal");
   static_assert(!WIN || BM >= 128, "window mode: 256- / 128-row tiles");
   static_assert(VM == 6 || VM == 4 || VM == 3, "wait literal");
   _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
