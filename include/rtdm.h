@@ -67,11 +67,13 @@ typedef enum rtdm_status {
 typedef enum rtdm_dtype {
   RTDM_F32 = 0, /* fp32 activations/weights, fp32 FMA (parity mode)            */
   RTDM_F16 = 1, /* fp16 activations/weights, fp32 accumulation on MFMA          */
-  RTDM_I8 = 2   /* detector only: fp16 activations in HBM; every conv with Cin % 128 == 0
-                   runs on int8 MFMA (conv_pipe_i8: v_mfma_i32_16x16x64_i8) over a
-                   per-channel int8 copy of its input, per-channel activation scales
-                   folded into per-output-channel int8 weights (rtdm_detector_calibrate);
-                   the reference's README --quant int8 (config 5)                      */
+  RTDM_I8 = 2   /* fp16 activations in HBM, int8 MFMA in the hot GEMMs, per-channel
+                   activation scales folded into per-output-channel int8 weights.
+                   detector: every conv with Cin % 128 == 0 runs on conv_pipe_i8
+                   (v_mfma_i32_16x16x64_i8) over an int8 copy of its input
+                   (rtdm_detector_calibrate); the reference's README --quant int8
+                   (config 5).  classifier: the ACFF 1x1 fusion GEMMs of the persistent
+                   and chained stages (rtdm_classifier_calibrate).                     */
 } rtdm_dtype;
 
 typedef enum rtdm_model_kind {
@@ -136,12 +138,25 @@ rtdm_status rtdm_classifier_create(int kind, int dtype, const rtdm_param* params
 rtdm_status rtdm_classifier_destroy(rtdm_classifier h);
 /* Input side length the model expects (140 or 240). */
 int rtdm_classifier_input_size(rtdm_classifier h);
+/* Human-readable plan: one line per ACFF block (geometry, kernel, pool, reducer,
+ * int8); returns bytes needed including the NUL when buf is too small.            */
+int64_t rtdm_classifier_describe(rtdm_classifier h, char* buf, int64_t buf_len);
 /* x: see rtdm_input_kind.  For FRAME_U8, in_h/in_w are the frame size; for the
  * NCHW kinds they must equal the model input size.
  * logits: [n,5] fc output (pre-softmax) or NULL; probs: [n,5] softmax (the value
  * the reference nn.Module returns) or NULL.                                      */
 rtdm_status rtdm_classify(rtdm_classifier h, const void* x, int x_kind, int n, int in_h, int in_w,
                           float* logits, float* probs, void* stream);
+/* int8 calibration of an RTDM_I8 classifier (activations stay fp16; the ACFF 1x1
+ * fusion GEMMs of the persistent and chained stages run on int8 MFMA): runs the
+ * network in fp16 on x (kinds as rtdm_classify) recording every int8 stage's
+ * per-concat-channel |x|max (max over all calls since the last reset != 0), then
+ * folds s_k = |x|max_k / 127 into the fusion weights and quantises them per output
+ * channel, as rtdm_detector_calibrate.  Synchronises the stream.  rtdm_classify on an
+ * uncalibrated RTDM_I8 handle returns RTDM_E_INVALID.  The reference has no int8
+ * classifier; this is the §8 int8 row for ErNET.                */
+rtdm_status rtdm_classifier_calibrate(rtdm_classifier h, const void* x, int x_kind, int n, int in_h, int in_w,
+                                      int reset, void* stream);
 
 /* ---- detector -------------------------------------------------------------- */
 /* cfg_text: contents of a Darknet .cfg (victim_localization/yolov3/cfg/NAME.cfg),

@@ -1,4 +1,12 @@
-"""int8 quantisation model of the detector's RTDM_I8 path (TEST INFRASTRUCTURE ONLY).
+"""int8 quantisation models of the RTDM_I8 paths (TEST INFRASTRUCTURE ONLY).
+
+Classifier (cls_calibrate / cls_int8_hook, on oracle.classifier.forward's fusion hook):
+the ACFF 1x1 fusion GEMM of the blocks the C++ planner marks int8 (classifier.cpp;
+rtdm_classifier_describe lists them) takes the depthwise concat quantised per concat
+channel, s_k = |x|max_k / 127 over the calibration frames, and the fusion weights times
+s_k quantised symmetric per output channel — the detector scheme below on the concat.
+
+Detector:
 
 The reference has no numeric int8 path (opaque TensorRT engines and
 entropy-calibration caches, tensorrt_inference/yolo/calibrator.py:87-153), so the int8
@@ -47,4 +55,28 @@ def int8_hook(amax):
         sw = wp.abs().flatten(1).amax(1).clamp_min(1e-30) / 127.0
         wq = torch.round(wp / sw.view(-1, 1, 1, 1)).clamp(-127, 127)
         return xq, wq * sw.view(-1, 1, 1, 1), b
+    return hook
+
+
+def cls_calibrate(kind, sd, x, blocks):
+    """Per-concat-channel |x|max of the int8 blocks' fusion inputs on inputs x ([N,3,S,S])."""
+    from oracle import classifier as OC
+    amax = {}
+
+    def hook(p, cat, w, b):
+        if p in blocks:
+            m = cat.abs().amax(dim=(0, 2, 3))
+            amax[p] = torch.maximum(amax[p], m) if p in amax else m
+        return cat, w, b
+
+    OC.forward(kind, sd, x, hook)
+    return amax
+
+
+def cls_int8_hook(amax):
+    """oracle.classifier fusion hook applying the classifier RTDM_I8 quantisation."""
+    inner = int8_hook(amax)
+
+    def hook(p, cat, w, b):
+        return inner(p, cat, w, b)
     return hook

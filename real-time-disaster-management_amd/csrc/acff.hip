@@ -26,6 +26,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace rtdm {
 
@@ -261,6 +262,15 @@ struct AcffPArgs {
   float slope;
   _Float16* out;
   int out_cs, pool;
+  // int8 1x1 fusion (RTDM_I8 classifiers, BASELINE config 5): the depthwise concat is
+  // quantised per concat channel (x * inv_s[branch][c], symmetric, +-127) into an int8 A
+  // tile; the per-channel activation scales are folded into per-output-channel int8
+  // weights pw8 [cout_pad][nch * 64] (k = chunk*64 + branch*CC + c), exact int32 sums
+  // dequantised by deq[o].
+  const int8_t* pw8;
+  const float* deq;
+  const float* inv_s;  // [3][cin]
+  unsigned* amax;      // calibration (fp16 path): |x|max of every concat channel [3][cin]
 };
 
 // Wave-uniform reads through the constant address space become scalar loads
@@ -304,18 +314,25 @@ __device__ __forceinline__ float fma_mix_hi_v(float w, uint32_t x2, float acc) {
 }
 constexpr int kAcffPMaxCin = 128;  // depthwise taps + biases of the whole layer in LDS
 
-template <int CC, int NF, int ABL = 0>  // ABL (diagnostics, wrong outputs): 1 no taps, 2 no GEMM
+// MODE: 0 fp16, 1 int8 1x1 fusion, 2 fp16 + calibration (records the concat's |x|max)
+template <int CC, int NF, int ABL = 0, int MODE = 0>  // ABL (diagnostics, wrong outputs): 1 no taps, 2 no GEMM
 __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a) {  // NF 2: <= 168 VGPRs, 3 waves / SIMD
+  constexpr bool I8 = MODE == 1, CAL = MODE == 2;
   using G = AcffPGeom<CC>;
   constexpr int TH = G::TH, TW = G::TW, HW = G::HW, PS = G::PS, CG = G::CG, KC = G::KC, AS = G::AS;
   constexpr int HALO = G::HALO, PV = G::PV, XS = G::XS;
+  constexpr int KC8 = (3 * CC + 63) / 64 * 64, AS8 = KC8 + 16;  // int8 A tile: K per chunk, row bytes
+  static_assert(!I8 || G::NPIX * AS8 <= G::NPIX * AS * 2, "int8 A tile reuses the fp16 one");
   __shared__ __attribute__((aligned(16))) _Float16 xs[2 * XS];
   __shared__ __attribute__((aligned(16))) _Float16 At[G::NPIX * AS];
-  // depthwise taps [27][cin] then biases [3][cin]: LDS broadcast reads, pipelined by the
-  // compiler (as wave-uniform scalar loads every tap waited on its own s_load latency)
-  extern __shared__ __attribute__((aligned(16))) float s_dw[];  // dynamic: 30 * cin floats
+  int8_t* const At8 = reinterpret_cast<int8_t*>(At);
+  // depthwise taps [27][cin], biases [3][cin] (int8: + inverse activation scales [3][cin]):
+  // LDS broadcast reads, pipelined by the compiler (as wave-uniform scalar loads every tap
+  // waited on its own s_load latency)
+  extern __shared__ __attribute__((aligned(16))) float s_dw[];  // dynamic: (I8 ? 33 : 30) * cin floats
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int i = tid; i < 30 * a.cin; i += 256) s_dw[i] = i < 27 * a.cin ? a.dw_wt[i] : a.dw_b[i - 27 * a.cin];
+  for (int i = tid; i < (I8 ? 33 : 30) * a.cin; i += 256)
+    s_dw[i] = i < 27 * a.cin ? a.dw_wt[i] : i < 30 * a.cin ? a.dw_b[i - 27 * a.cin] : a.inv_s[i - 30 * a.cin];
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, g = lane >> 4;
   const int oh = a.h - 2, ow = a.w - 2;
@@ -323,7 +340,10 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
   const int ntiles = a.n * tiles_x * tiles_y;
   const int nch = a.cin / CC;
   const int ktot = nch * KC;
-  if (KC > 3 * CC) {  // zero K padding of the A tile (never overwritten)
+  if constexpr (I8) {  // zero K padding of the int8 A tile (never overwritten)
+    constexpr int padw = KC8 - 3 * CC;
+    for (int i = tid; i < G::NPIX * padw; i += 256) At8[(i / padw) * AS8 + 3 * CC + i % padw] = 0;
+  } else if (KC > 3 * CC) {  // zero K padding of the A tile (never overwritten)
     constexpr int padw = KC - 3 * CC;
     for (int i = tid; i < G::NPIX * padw; i += 256) At[(i / padw) * AS + 3 * CC + i % padw] = (_Float16)0.f;
   }
@@ -357,35 +377,48 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
     }
   };
   const int wm = wid >> 1, wn = wid & 1;
-  f4 acc[4][NF];
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  using AccT = std::conditional_t<I8, i32x4, f4>;
+  AccT acc[4][NF];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int jn = 0; jn < NF; ++jn) acc[i][jn] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int jn = 0; jn < NF; ++jn) acc[i][jn] = AccT{0, 0, 0, 0};
   h8 bf[KC / 32][NF];
+  i32x4 bf8[KC8 / 64][NF];
   int bf_ch = -1;
+  const int ktot8 = nch * KC8;
   // 1x1 weight fragments of item j's chunk (global, L2-resident; once when nch == 1).
   // Issued BEFORE the halo prefetch of j+2: vmcnt retires in order, so waiting for
   // these never waits for the prefetch.
   auto load_bf = [&](int j) {
     const int ch = j % nch;
     if (ch == bf_ch) return;
+    if constexpr (I8) {
 #pragma unroll
-    for (int ks = 0; ks < KC / 32; ++ks)
+      for (int ks = 0; ks < KC8 / 64; ++ks)
 #pragma unroll
-      for (int tn = 0; tn < NF; ++tn)
-        bf[ks][tn] = *(const h8*)(a.pw + (size_t)(wn * NF * 16 + tn * 16 + fr) * ktot + ch * KC + ks * 32 + g * 8);
+        for (int tn = 0; tn < NF; ++tn)
+          bf8[ks][tn] = *(const i32x4*)(a.pw8 + (size_t)(wn * NF * 16 + tn * 16 + fr) * ktot8 + ch * KC8 + ks * 64 + g * 16);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < KC / 32; ++ks)
+#pragma unroll
+        for (int tn = 0; tn < NF; ++tn)
+          bf[ks][tn] = *(const h8*)(a.pw + (size_t)(wn * NF * 16 + tn * 16 + fr) * ktot + ch * KC + ks * 32 + g * 8);
+    }
     bf_ch = ch;
   };
   // epilogue constants of this lane's channels, hoisted out of the item loop (a load
   // in the loop would wait for the in-flight prefetch)
-  float e_b[NF], e_s[NF], e_t[NF];
+  float e_b[NF], e_s[NF], e_t[NF], e_d[NF];
   bool e_ok[NF];
 #pragma unroll
   for (int tn = 0; tn < NF; ++tn) {
     const int c = wn * NF * 16 + tn * 16 + fr;
     const bool cv = c < a.cout;
     e_ok[tn] = cv;
+    e_d[tn] = I8 && cv ? a.deq[c] : 1.f;
     e_b[tn] = cv ? a.bias[c] : 0.f;
     e_s[tn] = (cv && a.scale) ? a.scale[c] : 1.f;
     e_t[tn] = (cv && a.scale) ? a.shift[c] : 0.f;
@@ -393,7 +426,15 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
 
   auto process = [&](int j, const _Float16* xb) {
     const int tile = item_tile(j), ch = j % nch;
-    // ---- depthwise branches -> A tile (fp16) ----
+    int cal_ok = 0;  // calibration: this lane's pixel lies inside the output map
+    if constexpr (CAL) {
+      const int tx = tile % tiles_x, ty = (tile / tiles_x) % tiles_y;
+      const int m = lane, q = m >> 2, dq = m & 3;  // pixel of lane (pixel block 0 / 1 differ by 4 rows)
+      const int py = 2 * (q >> 3) + (dq >> 1), px = 2 * (q & 7) + (dq & 1);
+      cal_ok = (ty * TH + py < oh ? 1 : 0) | (ty * TH + py + 4 < oh ? 2 : 0);
+      if (tx * TW + px >= ow) cal_ok = 0;
+    }
+    // ---- depthwise branches -> A tile (fp16, or int8 quantised per concat channel) ----
 #pragma unroll
     for (int u0 = 0; u0 < 2 * CG; u0 += 4) {
       const int u = u0 + wid;
@@ -432,25 +473,63 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
                 s8[2 * jj + 1] = fma_mix_hi_v(wv[2 * jj + 1], xv[jj], s8[2 * jj + 1]);
               }
             }
-          h8 o;
+          if constexpr (I8) {
+            const float* ip = s_dw + (30 + br) * a.cin + cbase;
+            uint32_t lo = 0, hi = 0;
 #pragma unroll
-          for (int jj = 0; jj < 8; ++jj) o[jj] = (_Float16)s8[jj];
-          *(h8*)(At + m * AS + br * CC + cg * 8) = o;
+            for (int jj = 0; jj < 8; ++jj) {
+              int v = (int)rintf(s8[jj] * ip[jj]);
+              v = v < -127 ? -127 : (v > 127 ? 127 : v);
+              if (jj < 4)
+                lo |= ((uint32_t)v & 255u) << (8 * jj);
+              else
+                hi |= ((uint32_t)v & 255u) << (8 * (jj - 4));
+            }
+            *(uint2*)(At8 + m * AS8 + br * CC + cg * 8) = make_uint2(lo, hi);
+          } else {
+            h8 o;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) o[jj] = (_Float16)s8[jj];
+            *(h8*)(At + m * AS + br * CC + cg * 8) = o;
+            if constexpr (CAL) {  // calibration: per concat channel |x|max over the wave's valid pixels
+#pragma unroll
+              for (int jj = 0; jj < 8; ++jj) {
+                float v = ((cal_ok >> pb) & 1) ? fabsf(s8[jj]) : 0.f;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+                if (lane == 0 && v > 0.f) atomicMax(a.amax + br * a.cin + cbase + jj, __float_as_uint(v));
+              }
+            }
+          }
         }
       }
     }
     __syncthreads();
     // ---- 1x1 GEMM over this chunk: [128 px x KC] x [KC x cout_pad] ----
+    if constexpr (I8) {
 #pragma unroll
-    for (int ks = 0; ks < ((ABL & 2) ? 0 : KC / 32); ++ks) {
-      h8 af[4];
+      for (int ks = 0; ks < ((ABL & 2) ? 0 : KC8 / 64); ++ks) {
+        i32x4 af[4];
 #pragma unroll
-      for (int tm = 0; tm < 4; ++tm) af[tm] = *(const h8*)(At + (wm * 64 + tm * 16 + fr) * AS + ks * 32 + g * 8);
+        for (int tm = 0; tm < 4; ++tm) af[tm] = *(const i32x4*)(At8 + (wm * 64 + tm * 16 + fr) * AS8 + ks * 64 + g * 16);
 #pragma unroll
-      for (int tm = 0; tm < 4; ++tm)
+        for (int tm = 0; tm < 4; ++tm)
 #pragma unroll
-        for (int tn = 0; tn < NF; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[tm], bf[ks][tn], acc[tm][tn], 0, 0, 0);
+          for (int tn = 0; tn < NF; ++tn)
+            acc[tm][tn] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[tm], bf8[ks][tn], acc[tm][tn], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < ((ABL & 2) ? 0 : KC / 32); ++ks) {
+        h8 af[4];
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm) af[tm] = *(const h8*)(At + (wm * 64 + tm * 16 + fr) * AS + ks * 32 + g * 8);
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < NF; ++tn)
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[tm], bf[ks][tn], acc[tm][tn], 0, 0, 0);
+      }
     }
     if (ch == nch - 1) {
       // ---- epilogue: bias -> LeakyReLU (0 < slope < 1: max(x, slope x)) -> BN affine ->
@@ -469,7 +548,7 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
         for (int tn = 0; tn < NF; ++tn)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float x = acc[tm][tn][r] + e_b[tn];
+            const float x = (I8 ? (float)acc[tm][tn][r] * e_d[tn] : (float)acc[tm][tn][r]) + e_b[tn];
             v[tn][r] = fmaxf(x, x * a.slope) * e_s[tn] + e_t[tn];
           }
         if (a.pool) {
@@ -496,7 +575,7 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int jn = 0; jn < NF; ++jn) acc[i][jn] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int jn = 0; jn < NF; ++jn) acc[i][jn] = AccT{0, 0, 0, 0};
     }
   };
 
@@ -537,7 +616,7 @@ int acff_persist_chunk(int cin, int cout_pad, int oh) {
 void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int w, int cin, int lim_h, int lim_w,
                          const float* dw_wt, const float* dw_b, const void* pwc, int cout, int cout_pad,
                          const float* bias, const float* scale, const float* shift, float slope, void* out, int out_cs,
-                         int pool, hipStream_t s) {
+                         int pool, hipStream_t s, const AcffI8* q) {
   const int cc = acff_persist_chunk(cin, cout_pad, h - 2);
   RTDM_REQUIRE(cc > 0, RTDM_E_INVALID, "acff_persist: unsupported shape");
   RTDM_REQUIRE((in_cs % 8) == 0 && (in_co % 8) == 0, RTDM_E_INVALID, "acff_persist: input view not 16-byte aligned");
@@ -564,12 +643,17 @@ void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int
   a.out = (_Float16*)out;
   a.out_cs = out_cs;
   a.pool = pool;
+  const bool i8 = q && q->w8;
+  a.pw8 = i8 ? (const int8_t*)q->w8 : nullptr;
+  a.deq = i8 ? q->deq : nullptr;
+  a.inv_s = i8 ? q->inv_s : nullptr;
+  a.amax = q && !i8 ? q->amax : nullptr;
   const int64_t tiles = (int64_t)n * ((lim_h + 7) / 8) * ((lim_w + 15) / 16);
   if (tiles <= 0) return;
   RTDM_REQUIRE(tiles < (1ll << 31), RTDM_E_CAPACITY, "acff_persist: too many tiles");
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const size_t lds = (size_t)30 * cin * sizeof(float);
+  const size_t lds = (size_t)(i8 ? 33 : 30) * cin * sizeof(float);
   auto go = [&](auto kern) {
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
@@ -578,7 +662,9 @@ void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int
   };
   const int abl = acff_persist_mode() - 1;  // >1: diagnostic ablations
   if (cc == 16) {
-    if (abl == 1) cout_pad == 64 ? go(acff_persist<16, 2, 1>) : go(acff_persist<16, 4, 1>);
+    if (i8) cout_pad == 64 ? go(acff_persist<16, 2, 0, 1>) : go(acff_persist<16, 4, 0, 1>);
+    else if (a.amax) cout_pad == 64 ? go(acff_persist<16, 2, 0, 2>) : go(acff_persist<16, 4, 0, 2>);
+    else if (abl == 1) cout_pad == 64 ? go(acff_persist<16, 2, 1>) : go(acff_persist<16, 4, 1>);
     else if (abl == 2) cout_pad == 64 ? go(acff_persist<16, 2, 2>) : go(acff_persist<16, 4, 2>);
     else cout_pad == 64 ? go(acff_persist<16, 2>) : go(acff_persist<16, 4>);
   }
@@ -665,6 +751,10 @@ struct AcffChainStage {
   const float* dw_wt;   // [3][9][cin]
   const float* dw_b;    // [3][cin]
   const _Float16* pw;   // [cout_pad][kpad], k = branch*cin + c
+  const int8_t* pw8;    // int8: [cout_pad][3 cin], k = branch*cin + c (AcffI8)
+  const float* deq;
+  const float* inv_s;   // [3][cin]
+  unsigned* amax;       // calibration (fp16 run)
   const float* bias;
   const float* scale;
   const float* shift;
@@ -689,14 +779,19 @@ struct AcffChainArgs {
   int abl;  // diagnostics (wrong outputs): 1 no depthwise, 2 no 1x1 MFMA, 4 no tail
 };
 
+template <int MODE>  // 0 fp16, 1 int8 1x1 fusion, 2 fp16 + calibration
 __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
+  constexpr bool I8 = MODE == 1, CAL = MODE == 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char chain_lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int img = blockIdx.x;
   _Float16* buf[2] = {(_Float16*)chain_lds, (_Float16*)(chain_lds + a.act_bytes)};
   _Float16* At = (_Float16*)(chain_lds + 2 * a.act_bytes);
-  float* wsm = (float*)(chain_lds + 2 * a.act_bytes + a.a_bytes);  // [3][9][C] then bias [3][C]
+  int8_t* const At8 = (int8_t*)At;  // int8 A chunk [M][C + 16] bytes (inside the fp16 one)
+  float* wsm = (float*)(chain_lds + 2 * a.act_bytes + a.a_bytes);  // [3][9][C], bias [3][C] (int8: inv_s [3][C])
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  using AccT = std::conditional_t<I8, i32x4, f4>;
 
   {  // input map of stage 0: [h*h][cin] fp16 from the NHWC view
     const int h = a.st[0].h, C = a.st[0].cin, CG = C >> 3;
@@ -711,19 +806,23 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
   // depthwise taps + biases of a stage -> wsm.  Stage 0 here; stage si + 1's are loaded into
   // registers while stage si runs and stored once its last depthwise phase is done (each
   // stage used to start by waiting on these global loads).
-  constexpr int kWPre = (30 * 128 + kChainThreads - 1) / kChainThreads;  // cin <= 128
+  constexpr int NW = I8 ? 33 : 30;  // floats per channel in wsm
+  constexpr int kWPre = (NW * 128 + kChainThreads - 1) / kChainThreads;  // cin <= 128
   auto wload = [&](const AcffChainStage& st, float (&pre)[kWPre]) {
 #pragma unroll
     for (int k = 0; k < kWPre; ++k) {
       const int i = tid + k * kChainThreads;
-      pre[k] = i < 27 * st.cin ? st.dw_wt[i] : (i < 30 * st.cin ? st.dw_b[i - 27 * st.cin] : 0.f);
+      pre[k] = i < 27 * st.cin   ? st.dw_wt[i]
+               : i < 30 * st.cin ? st.dw_b[i - 27 * st.cin]
+               : (I8 && i < 33 * st.cin) ? st.inv_s[i - 30 * st.cin]
+                                          : 0.f;
     }
   };
   auto wstore = [&](const AcffChainStage& st, const float (&pre)[kWPre]) {
 #pragma unroll
     for (int k = 0; k < kWPre; ++k) {
       const int i = tid + k * kChainThreads;
-      if (i < 30 * st.cin) wsm[i] = pre[k];
+      if (i < NW * st.cin) wsm[i] = pre[k];
     }
   };
   if (a.nst > 0) {
@@ -737,13 +836,14 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     float wpre[kWPre];
     if (si + 1 < a.nst) wload(a.st[si + 1], wpre);
     // this lane's epilogue constants (2 channels), loaded now so the epilogue does not wait
-    float e_b[2], e_s[2], e_t[2];
+    float e_b[2], e_s[2], e_t[2], e_d[2];
     {
       const int wn0 = st.cout_pad >> 5, wni0 = wid - (wid / wn0) * wn0;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = wni0 * 32 + j * 16 + fr;
         const bool cv = c < st.cout;
+        e_d[j] = I8 && cv ? st.deq[c] : 1.f;
         e_b[j] = cv ? st.bias[c] : 0.f;
         e_s[j] = cv && st.scale ? st.scale[c] : 1.f;
         e_t[j] = cv && st.scale ? st.shift[c] : 0.f;
@@ -757,9 +857,10 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     const int mtiles = (M + 15) >> 4;
     const int fm = (mtiles + wm - 1) / wm;  // <= 4 (plan-time check)
     const int m_base = wmi * fm * 16, n_base = wni * 32;
-    f4 acc[4][2];
+    AccT acc[4][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = AccT{0, 0, 0, 0};
+    const int AS8 = C + 16;
     for (int br = 0; br < 3; ++br) {
       const int d = br + 1;
       const float* wb = wsm + br * 9 * C;
@@ -768,13 +869,24 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
       // depthwise phase so their latency hides under it (C <= 128: 4 k-steps)
       const _Float16* wrow = st.pw + (size_t)(n_base + fr) * st.kpad + br * C + g * 8;
       const int nks = C / 32;
-      h8 bpre[4][2];
+      h8 bpre[I8 ? 1 : 4][2];
+      i32x4 bpre8[I8 ? 2 : 1][2];
+      if constexpr (I8) {  // k-steps of 64: C / 64 <= 2
+        const int8_t* w8row = st.pw8 + (size_t)(n_base + fr) * 3 * C + br * C + g * 16;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-        if (ks < nks && C <= 128) {
-          bpre[ks][0] = *(const h8*)(wrow + ks * 32);
-          bpre[ks][1] = *(const h8*)(wrow + (size_t)16 * st.kpad + ks * 32);
-        }
+        for (int ks = 0; ks < 2; ++ks)
+          if (ks < C / 64) {
+            bpre8[ks][0] = *(const i32x4*)(w8row + ks * 64);
+            bpre8[ks][1] = *(const i32x4*)(w8row + (size_t)16 * 3 * C + ks * 64);
+          }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          if (ks < nks && C <= 128) {
+            bpre[ks][0] = *(const h8*)(wrow + ks * 32);
+            bpre[ks][1] = *(const h8*)(wrow + (size_t)16 * st.kpad + ks * 32);
+          }
+      }
       for (int i = tid; i < ((a.abl & 1) ? 0 : M * CG); i += kChainThreads) {
         const int m = i / CG, v = i - m * CG;
         const int oy = m / OH, ox = m - oy * OH;
@@ -800,25 +912,64 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
             t[6] = fmaf(w1.z, (float)xv[6], t[6]);
             t[7] = fmaf(w1.w, (float)xv[7], t[7]);
           }
-        h8 o;
+        if constexpr (I8) {
+          const float* ip = wsm + 30 * C + br * C + v * 8;
+          uint32_t lo = 0, hi = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (_Float16)t[j];
-        *(h8*)(At + (size_t)m * AS + v * 8) = o;
+          for (int j = 0; j < 8; ++j) {
+            int q = (int)rintf(t[j] * ip[j]);
+            q = q < -127 ? -127 : (q > 127 ? 127 : q);
+            if (j < 4)
+              lo |= ((uint32_t)q & 255u) << (8 * j);
+            else
+              hi |= ((uint32_t)q & 255u) << (8 * (j - 4));
+          }
+          *(uint2*)(At8 + (size_t)m * AS8 + v * 8) = make_uint2(lo, hi);
+        } else {
+          h8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (_Float16)t[j];
+          *(h8*)(At + (size_t)m * AS + v * 8) = o;
+          if constexpr (CAL) {  // calibration: |x|max per concat channel
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (t[j] != 0.f) atomicMax(st.amax + br * C + v * 8 + j, __float_as_uint(fabsf(t[j])));
+          }
+        }
       }
       __syncthreads();
       // this branch's K slice: k = br*C + [0, C)
+      auto kstep8 = [&](int ks, const i32x4& b0, const i32x4& b1) {
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm) {
+          if (tm < fm && m_base + tm * 16 < M) {
+            const int row = m_base + tm * 16 + fr;
+            const i32x4 av = *(const i32x4*)(At8 + (size_t)(row < M ? row : M - 1) * AS8 + ks * 64 + g * 16);
+            if constexpr (I8) {
+              acc[tm][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, b0, acc[tm][0], 0, 0, 0);
+              acc[tm][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, b1, acc[tm][1], 0, 0, 0);
+            }
+          }
+        }
+      };
       auto kstep = [&](int ks, const h8& b0, const h8& b1) {
 #pragma unroll
         for (int tm = 0; tm < 4; ++tm) {
           if (tm < fm && m_base + tm * 16 < M) {
             const int row = m_base + tm * 16 + fr;
             const h8 av = *(const h8*)(At + (size_t)(row < M ? row : M - 1) * AS + ks * 32 + g * 8);
-            acc[tm][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b0, acc[tm][0], 0, 0, 0);
-            acc[tm][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b1, acc[tm][1], 0, 0, 0);
+            if constexpr (!I8) {
+              acc[tm][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b0, acc[tm][0], 0, 0, 0);
+              acc[tm][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b1, acc[tm][1], 0, 0, 0);
+            }
           }
         }
       };
       if (a.abl & 2) {
+      } else if constexpr (I8) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          if (ks < C / 64) kstep8(ks, bpre8[ks][0], bpre8[ks][1]);
       } else if (C <= 128) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
@@ -835,7 +986,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     for (int j = 0; j < 2; ++j) {
       const int c = n_base + j * 16 + fr;
       if (c >= st.cout) continue;
-      const float bc = e_b[j], sc = e_s[j], sh = e_t[j];
+      const float bc = e_b[j], sc = e_s[j], sh = e_t[j], dq = e_d[j];
 #pragma unroll
       for (int tm = 0; tm < 4; ++tm) {
         if (!(tm < fm)) continue;
@@ -843,7 +994,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
         for (int r = 0; r < 4; ++r) {
           const int m = m_base + tm * 16 + g * 4 + r;
           if (m < M) {
-            float x = acc[tm][j][r] + bc;
+            float x = (I8 ? (float)acc[tm][j][r] * dq : (float)acc[tm][j][r]) + bc;
             x = x > 0.f ? x : x * a.slope;
             Y[(size_t)m * st.cout + c] = (_Float16)fmaf(x, sc, sh);
           }
@@ -935,7 +1086,7 @@ size_t acff_chain_lds(const AcffChainPlan& p) {
   const int oh = p.h[p.nst - 1] - 2;
   ab = std::max(ab, (size_t)(5 * oh * oh + 5 * 16 + 8) * 4);  // the tail reuses the A chunk
   ab = (size_t)round_up((int64_t)ab, 16);
-  return 2 * act + ab + (size_t)30 * cmax * 4;
+  return 2 * act + ab + (size_t)33 * cmax * 4;  // wsm: taps, biases (+ int8 inverse scales)
 }
 
 bool acff_chain_ok(const AcffChainPlan& p) {
@@ -962,7 +1113,7 @@ void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in
                        const float* const* dw_b, const void* const* pw, const float* const* bias,
                        const float* const* scale, const float* const* shift, float slope, const float* w2,
                        int pool_pad, int ph, int pwid, const float* fcw, const float* fcb, float* logits, float* probs,
-                       hipStream_t s) {
+                       hipStream_t s, const AcffI8* q) {
   RTDM_REQUIRE(acff_chain_ok(p), RTDM_E_INVALID, "acff_chain: unsupported plan");
   RTDM_REQUIRE((in_cs % 8) == 0 && (in_co % 8) == 0, RTDM_E_INVALID, "acff_chain: input view not 16-byte aligned");
   RTDM_REQUIRE(ph * pwid <= 16, RTDM_E_UNSUPPORTED, "acff_chain: pooled tail too large");
@@ -986,7 +1137,18 @@ void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in
     t.cout_pad = p.cout_pad[i];
     t.kpad = p.kpad[i];
     t.h = p.h[i];
+    const bool i8 = q && q[i].w8;
+    t.pw8 = i8 ? (const int8_t*)q[i].w8 : nullptr;
+    t.deq = i8 ? q[i].deq : nullptr;
+    t.inv_s = i8 ? q[i].inv_s : nullptr;
+    t.amax = q && !i8 ? q[i].amax : nullptr;
   }
+  const bool i8 = q && q[0].w8;
+  for (int i = 0; i < p.nst; ++i)
+    RTDM_REQUIRE(!q || (q[i].w8 != nullptr) == i8, RTDM_E_INVALID, "acff_chain: int8 on some stages only");
+  if (i8)
+    for (int i = 0; i < p.nst; ++i)
+      RTDM_REQUIRE(p.cin[i] % 64 == 0, RTDM_E_UNSUPPORTED, "acff_chain: int8 needs cin % 64 == 0");
   a.slope = slope;
   size_t act = 0, ab = 0;
   for (int i = 0; i < p.nst; ++i) {
@@ -1008,7 +1170,12 @@ void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in
   a.logits = logits;
   a.probs = probs;
   const size_t lds = acff_chain_lds(p);
-  hipLaunchKernelGGL(acff_chain, dim3(n), dim3(kChainThreads), lds, s, a);
+  if (i8)
+    hipLaunchKernelGGL(acff_chain<1>, dim3(n), dim3(kChainThreads), lds, s, a);
+  else if (q && q[0].amax)
+    hipLaunchKernelGGL(acff_chain<2>, dim3(n), dim3(kChainThreads), lds, s, a);
+  else
+    hipLaunchKernelGGL(acff_chain<0>, dim3(n), dim3(kChainThreads), lds, s, a);
   RTDM_HIP(hipGetLastError());
 }
 

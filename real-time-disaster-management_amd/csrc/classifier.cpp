@@ -8,6 +8,8 @@
 //   -> tail (1x1 ->5, AvgPool 5, NCHW flatten, Linear, Softmax).
 // RedConv's conv_red1 is folded into the stem (linear o linear); conv_red2
 // absorbs acff2's BN affine.
+#include <cmath>
+#include <cstring>
 #include <map>
 
 #include "weights.h"
@@ -34,6 +36,13 @@ struct AcffStage {
   size_t red_buf = 0;
   int red_h = 0, red_w = 0;
   size_t mid_buf = 0;  // ACFF output before the reducer (when red)
+  // int8 1x1 fusion (RTDM_I8 handles: acff_persist and acff_chain stages): blob slots of
+  // the int8 weights (kernel K order), per-output dequantisation, inverse activation
+  // scales [3][cin]; fp32 fusion weights [cout][3 cin] kept for the calibration
+  bool q8 = false;
+  size_t w8_off = 0, deq_off = 0, inv_off = 0;
+  int amax_off = 0;
+  std::vector<float> wf;
 };
 
 }  // namespace rtdm
@@ -56,6 +65,12 @@ struct rtdm_classifier_s {
   // stages [chain_start, end) + tail run as one acff_chain launch (-1: none)
   int chain_start = -1;
   rtdm::AcffChainPlan chain;
+  // RTDM_I8: fp16 activations everywhere, int8 1x1 fusion GEMMs in the persistent and
+  // chained ACFF stages once calibrated (rtdm_classifier_calibrate); calibrating = the
+  // fp16 forward recording every int8 stage's concat |x|max into amax
+  bool int8 = false, calibrated = false, calibrating = false;
+  rtdm::DevBuf amax;
+  int q_channels = 0;
 };
 
 namespace rtdm {
@@ -191,6 +206,7 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
     bn_affine(pm.get(p + ".batch_norm.weight", sp.cout), pm.get(p + ".batch_norm.bias", sp.cout),
               pm.get(p + ".batch_norm.running_mean", sp.cout), pm.get(p + ".batch_norm.running_var", sp.cout), sp.cout,
               1e-5, bs, bt);
+    if (h.int8) st.wf.assign(fw, fw + (size_t)sp.cout * 3 * sp.cin);
     st.pw = pack_conv(blob, fw, sp.cout, 3 * sp.cin, 1, nullptr, f16);
     st.pw.b_off = blob.add(fb, sizeof(float) * sp.cout);
     st.fused = f16 && acff_fused_ok(sp.cin, st.pw.cout_pad, st.pw.kpad);
@@ -294,6 +310,28 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
       }
     }
   }
+  if (h.int8) {  // int8 slots for the persistent stages and (all or none of) the chained ones
+    bool chain_q = h.chain_start >= 0;
+    for (int i = std::max(0, h.chain_start); chain_q && i < (int)h.stages.size(); ++i)
+      chain_q = h.stages[i].cin % 64 == 0;
+    for (int i = 0; i < (int)h.stages.size(); ++i) {
+      AcffStage& st = h.stages[i];
+      const bool in_chain = h.chain_start >= 0 && i >= h.chain_start;
+      if (!(st.persist_cc || (in_chain && chain_q))) {
+        st.wf.clear();
+        continue;
+      }
+      const int cp = st.pw.cout_pad;
+      const size_t kq = st.persist_cc ? (size_t)(st.cin / st.persist_cc) * 64 : (size_t)3 * st.cin;
+      st.q8 = true;
+      st.w8_off = blob.add(nullptr, (size_t)cp * kq);
+      st.deq_off = blob.add(nullptr, (size_t)cp * sizeof(float));
+      st.inv_off = blob.add(nullptr, (size_t)3 * st.cin * sizeof(float));
+      st.amax_off = h.q_channels;
+      h.q_channels += 3 * st.cin;
+    }
+    h.amax.alloc((size_t)std::max(1, h.q_channels) * sizeof(unsigned));
+  }
   h.per_image = off;
   h.blob.upload(blob);
   h.arena.alloc(h.per_image * esize(h.dtype) * h.max_batch);
@@ -303,6 +341,8 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
                            float* probs, hipStream_t s) {
   RTDM_REQUIRE(n >= 0 && n <= h.max_batch, RTDM_E_CAPACITY,
                "classify: batch " + std::to_string(n) + " exceeds max_batch " + std::to_string(h.max_batch));
+  RTDM_REQUIRE(!h.int8 || h.calibrated || h.calibrating || h.q_channels == 0, RTDM_E_INVALID,
+               "classify: int8 classifier not calibrated (rtdm_classifier_calibrate)");
   if (n == 0) return;
   RTDM_REQUIRE(x, RTDM_E_INVALID, "classify: NULL input");
   const size_t es = esize(h.dtype);
@@ -362,6 +402,18 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
 
   View cur{buf(h.stem_buf), h.stem_cout, 0};
   const bool chain = h.chain_start >= 0 && acff_chain_mode();
+  // int8 / calibration arguments of a stage (nullptr: the plain fp16 kernels)
+  auto q8 = [&](const AcffStage& st, AcffI8& q) -> const AcffI8* {
+    if (!st.q8) return nullptr;
+    if (h.calibrating) {
+      q.amax = h.amax.as<unsigned>() + st.amax_off;
+      return &q;
+    }
+    q.w8 = h.blob.at<void>(st.w8_off);
+    q.deq = h.blob.at<float>(st.deq_off);
+    q.inv_s = h.blob.at<float>(st.inv_off);
+    return &q;
+  };
   for (size_t si = 0; si < h.stages.size(); ++si) {
     if (chain && (int)si == h.chain_start) break;
     const AcffStage& st = h.stages[si];
@@ -371,10 +423,12 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       const float* sh = st.affine ? h.blob.at<float>(st.pw.t_off) : nullptr;
       const bool pool_here = st.pool && !st.red_pool;
       void* dst = st.red && st.red_pool ? buf(st.mid_buf) : buf(st.out_buf);
-      if (st.persist_cc && acff_persist_mode())
+      AcffI8 qa;
+      if (st.persist_cc && (acff_persist_mode() || st.q8))
         launch_acff_persist(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_wt),
                             h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pwc_off), st.cout, st.pw.cout_pad,
-                            h.blob.at<float>(st.pw.b_off), sc, sh, 0.01f, dst, st.cout, pool_here ? 1 : 0, s);
+                            h.blob.at<float>(st.pw.b_off), sc, sh, 0.01f, dst, st.cout, pool_here ? 1 : 0, s,
+                            q8(st, qa));
       else
       launch_acff_fused(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_wt),
                         h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pw.w_off), st.pw.kpad, st.cout, st.pw.cout_pad,
@@ -505,8 +559,11 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       cur = View{buf(st.red_buf), st.redw.cout, 0};
     }
   }
+  RTDM_REQUIRE(!h.int8 || chain || h.chain_start < 0, RTDM_E_INVALID, "classify: int8 handle needs acff_chain mode");
   if (chain) {
     const int k = h.chain.nst;
+    AcffI8 qs[4];
+    bool any_q = false;
     const float* dw_wt[4];
     const float* dw_b[4];
     const void* pw[4];
@@ -521,10 +578,11 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       bias[i] = h.blob.at<float>(st.pw.b_off);
       sc[i] = h.blob.at<float>(st.pw.s_off);
       sh[i] = h.blob.at<float>(st.pw.t_off);
+      any_q = q8(st, qs[i]) != nullptr || any_q;
     }
     launch_acff_chain(h.chain, cur.ptr, cur.cs, cur.co, n, dw_wt, dw_b, pw, bias, sc, sh, 0.01f,
                       h.blob.at<float>(h.tail_w2), h.tail_pool_pad, h.tail_ph, h.tail_pw, h.blob.at<float>(h.tail_fcw),
-                      h.blob.at<float>(h.tail_fcb), logits, probs, s);
+                      h.blob.at<float>(h.tail_fcb), logits, probs, s, any_q ? qs : nullptr);
     return;
   }
   launch_cls_tail(cur.ptr, n, h.tail_h, h.tail_h, h.tail_c, h.blob.at<float>(h.tail_w2), h.tail_pool_pad, h.tail_ph,
@@ -543,12 +601,14 @@ rtdm_status rtdm_classifier_create(int kind, int dtype, const rtdm_param* params
     RTDM_REQUIRE(out, RTDM_E_INVALID, "classifier_create: NULL out");
     *out = nullptr;
     RTDM_REQUIRE(kind >= RTDM_SQUEEZE_ERNET && kind <= RTDM_ERNET, RTDM_E_INVALID, "classifier_create: bad kind");
-    RTDM_REQUIRE(dtype == RTDM_F32 || dtype == RTDM_F16, RTDM_E_INVALID, "classifier_create: bad dtype");
+    RTDM_REQUIRE(dtype == RTDM_F32 || dtype == RTDM_F16 || dtype == RTDM_I8, RTDM_E_INVALID,
+                 "classifier_create: bad dtype");
     RTDM_REQUIRE(max_batch > 0, RTDM_E_INVALID, "classifier_create: max_batch must be > 0");
     RTDM_REQUIRE(params && n_params > 0, RTDM_E_INVALID, "classifier_create: no parameters");
     auto h = std::make_unique<rtdm_classifier_s>();
     h->kind = kind;
-    h->dtype = dtype;
+    h->int8 = dtype == RTDM_I8;
+    h->dtype = h->int8 ? RTDM_F16 : dtype;  // int8 handles keep fp16 activations
     h->S = kind == RTDM_ERNET ? 240 : 140;
     h->max_batch = max_batch;
     RTDM_HIP(hipGetDevice(&h->dev));
@@ -563,6 +623,98 @@ rtdm_status rtdm_classifier_destroy(rtdm_classifier h) {
 }
 
 int rtdm_classifier_input_size(rtdm_classifier h) { return h ? h->S : 0; }
+
+int64_t rtdm_classifier_describe(rtdm_classifier h, char* buf, int64_t buf_len) {
+  if (!h) return 0;
+  std::string s = "classifier S " + std::to_string(h->S) + " dtype " +
+                  (h->int8 ? "i8" : h->dtype == RTDM_F16 ? "f16" : "f32") + " max_batch " +
+                  std::to_string(h->max_batch) + "\n";
+  const bool chain = h->chain_start >= 0 && acff_chain_mode();
+  for (int i = 0; i < (int)h->stages.size(); ++i) {
+    const AcffStage& st = h->stages[i];
+    const char* k = chain && i >= h->chain_start                     ? "acff_chain"
+                    : st.persist_cc && (acff_persist_mode() || st.q8) ? "acff_persist"
+                    : st.fused                                        ? "acff_fused"
+                                                                      : "dw3+gemm";
+    s += "acff" + std::to_string(i + 1) + " cin " + std::to_string(st.cin) + " cout " + std::to_string(st.cout) +
+         " in " + std::to_string(st.h) + "x" + std::to_string(st.w) + " kernel " + k + " pool " +
+         std::to_string(st.pool ? 1 : 0) + " red " + std::to_string(st.red ? 1 : 0) + " int8 " +
+         std::to_string(st.q8 ? 1 : 0) + "\n";
+  }
+  const int64_t need = (int64_t)s.size() + 1;
+  if (buf && buf_len >= need) std::memcpy(buf, s.c_str(), need);
+  return need;
+}
+
+rtdm_status rtdm_classifier_calibrate(rtdm_classifier h, const void* x, int x_kind, int n, int in_h, int in_w,
+                                      int reset, void* stream) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "classifier_calibrate: NULL handle");
+    RTDM_REQUIRE(h->int8, RTDM_E_INVALID, "classifier_calibrate: handle is not RTDM_I8");
+    if (h->q_channels == 0) {
+      h->calibrated = true;
+      return;
+    }
+    RTDM_REQUIRE(acff_chain_mode() == 1 || h->chain_start < 0, RTDM_E_INVALID, "classifier_calibrate: acff_chain mode");
+    const hipStream_t s = (hipStream_t)stream;
+    if (reset) RTDM_HIP(hipMemsetAsync(h->amax.p, 0, (size_t)h->q_channels * sizeof(unsigned), s));
+    if (n > 0) {
+      DevBuf out;
+      out.alloc((size_t)n * 10 * sizeof(float));
+      h->calibrating = true;  // fp16 forward, |x|max of every int8 stage's depthwise concat
+      try {
+        run_classifier(*h, x, x_kind, n, in_h, in_w, out.as<float>(), out.as<float>() + (size_t)n * 5, s);
+      } catch (...) {
+        h->calibrating = false;
+        throw;
+      }
+      h->calibrating = false;
+    }
+    // per int8 stage, per concat channel k = branch*cin + c: s_k = |x|max_k / 127 folded into
+    // the fusion weights (W'[o][k] = W[o][k] s_k), symmetric per-output-channel int8 of W'
+    // (s_w[o] = max_k |W'[o][k]| / 127, W8 = rint(W' / s_w[o]), deq[o] = s_w[o]) — the
+    // detector's scheme (rtdm_detector_calibrate) on the ACFF concat
+    std::vector<unsigned> am(h->q_channels);
+    RTDM_HIP(hipMemcpyAsync(am.data(), h->amax.p, am.size() * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    RTDM_HIP(hipStreamSynchronize(s));
+    for (const AcffStage& st : h->stages) {
+      if (!st.q8) continue;
+      const int K = 3 * st.cin, cp = st.pw.cout_pad;
+      std::vector<float> sx(K), inv(K);
+      for (int k = 0; k < K; ++k) {
+        float mx;
+        std::memcpy(&mx, &am[st.amax_off + k], sizeof(float));
+        RTDM_REQUIRE(std::isfinite(mx), RTDM_E_INVALID, "classifier_calibrate: non-finite activations");
+        sx[k] = mx > 0.f ? mx / 127.f : 1.f;
+        inv[k] = 1.f / sx[k];
+      }
+      const int cc = st.persist_cc, nch = cc ? st.cin / cc : 1;
+      const size_t kq = cc ? (size_t)nch * 64 : (size_t)K;
+      std::vector<int8_t> w8((size_t)cp * kq, 0);
+      std::vector<float> dq(cp, 0.f);
+      for (int o = 0; o < st.cout; ++o) {
+        const float* row = &st.wf[(size_t)o * K];
+        double mx = 0.0;
+        for (int k = 0; k < K; ++k) mx = std::max(mx, std::fabs((double)row[k] * sx[k]));
+        const double sw = mx > 0.0 ? mx / 127.0 : 1.0;
+        dq[o] = (float)sw;
+        for (int k = 0; k < K; ++k) {
+          const long q = std::max(-127L, std::min(127L, std::lround((double)row[k] * sx[k] / sw)));
+          size_t dst = (size_t)k;  // chain: k = branch*cin + c
+          if (cc) {                // persist: chunk*64 + branch*cc + c_local
+            const int br = k / st.cin, c = k - br * st.cin;
+            dst = (size_t)(c / cc) * 64 + br * cc + c % cc;
+          }
+          w8[(size_t)o * kq + dst] = (int8_t)q;
+        }
+      }
+      RTDM_HIP(hipMemcpy(h->blob.at<void>(st.w8_off), w8.data(), w8.size(), hipMemcpyHostToDevice));
+      RTDM_HIP(hipMemcpy(h->blob.at<void>(st.deq_off), dq.data(), dq.size() * sizeof(float), hipMemcpyHostToDevice));
+      RTDM_HIP(hipMemcpy(h->blob.at<void>(st.inv_off), inv.data(), inv.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+    h->calibrated = true;
+  });
+}
 
 rtdm_status rtdm_classify(rtdm_classifier h, const void* x, int x_kind, int n, int in_h, int in_w, float* logits,
                           float* probs, void* stream) {

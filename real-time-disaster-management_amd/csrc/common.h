@@ -247,13 +247,23 @@ void launch_acff_fused(const void* in, int in_cs, int in_co, int n, int h, int w
                        const float* dw_wt /*[3][9][cin]*/, const float* dw_b /*[3][cin]*/, const void* pw, int kpad,
                        int cout, int cout_pad, const float* bias, const float* scale, const float* shift, float slope,
                        void* out, int out_cs, int pool, hipStream_t s);
+// int8 1x1 fusion of an ACFF stage (RTDM_I8 classifiers): w8 non-null runs the int8 GEMM
+// (the concat quantised per channel with inv_s [3][cin], per-output-channel int8 weights in
+// the kernel's K order, dequantised by deq); w8 null and amax non-null records the fp16
+// run's |x|max of every concat channel (calibration).
+struct AcffI8 {
+  const void* w8 = nullptr;
+  const float* deq = nullptr;
+  const float* inv_s = nullptr;
+  unsigned* amax = nullptr;
+};
 // acff.hip: persistent ACFF for the large maps (channel chunk from acff_persist_chunk;
-// pwc = 1x1 weights in (chunk, branch, channel) K order)
+// pwc = 1x1 weights in (chunk, branch, channel) K order; int8: k = chunk*64 + branch*CC + c)
 int acff_persist_chunk(int cin, int cout_pad, int oh);
 void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int w, int cin, int lim_h, int lim_w,
                          const float* dw_wt, const float* dw_b, const void* pwc, int cout, int cout_pad,
                          const float* bias, const float* scale, const float* shift, float slope, void* out, int out_cs,
-                         int pool, hipStream_t s);
+                         int pool, hipStream_t s, const AcffI8* q = nullptr);
 // acff.hip: the classifier's non-pooled small-map ACFF suffix + tail in one launch
 struct AcffChainPlan {
   int nst = 0;
@@ -265,7 +275,7 @@ void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in
                        const float* const* dw_b, const void* const* pw, const float* const* bias,
                        const float* const* scale, const float* const* shift, float slope, const float* w2,
                        int pool_pad, int ph, int pwid, const float* fcw, const float* fcb, float* logits, float* probs,
-                       hipStream_t s);
+                       hipStream_t s, const AcffI8* q = nullptr /* [nst]; int8: k = branch*cin + c */);
 int acff_chain_mode();  // 1 = use acff_chain when the plan allows (default), 0 = per-stage kernels + tail
 void set_acff_chain_mode(int v);
 int acff_persist_mode();

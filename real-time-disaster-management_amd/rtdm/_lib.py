@@ -60,11 +60,13 @@ SIGNATURES = {
     "rtdm_classifier_destroy": (c_int, [c_void_p]),
     "rtdm_classifier_input_size": (c_int, [c_void_p]),
     "rtdm_classify": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "rtdm_classifier_calibrate": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "rtdm_detector_create": (c_int, [c_char_p, c_int, c_int, c_int, POINTER(c_float), c_int64, c_int,
                                      POINTER(c_void_p)]),
     "rtdm_detector_destroy": (c_int, [c_void_p]),
     "rtdm_detector_get_info": (c_int, [c_void_p, POINTER(rtdm_detector_info)]),
     "rtdm_detector_describe": (c_int64, [c_void_p, c_char_p, c_int64]),
+    "rtdm_classifier_describe": (c_int64, [c_void_p, c_char_p, c_int64]),
     "rtdm_detector_num_steps": (c_int, [c_void_p]),
     "rtdm_detector_step_info": (c_int, [c_void_p, c_int, c_char_p, c_int, POINTER(c_int), POINTER(c_double),
                                         POINTER(c_double)]),

@@ -42,6 +42,7 @@ class _ACFFClassifier(torch.nn.Module):
         self._handle = None
         self._handle_key = None
         self._dtype = L.RTDM_F32
+        self._calib = None
         self.logits = None  # fc output of the last forward (pre-softmax)
 
     # ---------------------------------------------------------------- weights --
@@ -73,6 +74,33 @@ class _ACFFClassifier(torch.nn.Module):
         self._dtype = L.RTDM_F32
         self._release()
         return self
+
+    def int8(self, calib: torch.Tensor):
+        """int8 ACFF fusion GEMMs (the §8 int8 row for ErNET; the reference classifier has no
+        int8 mode): activations stay fp16, the 1x1 fusion convs of the persistent and chained
+        ACFF stages run on int8 MFMA with per-concat-channel activation scales calibrated on
+        `calib` (uint8 frames [N,H,W,3] or [N,3,S,S] inputs on the GPU, kept for handles
+        created later) folded into per-output-channel int8 weights."""
+        if not calib.is_cuda:
+            raise RuntimeError("calibration frames must be on the GPU")
+        self._calib = calib.contiguous()
+        self._dtype = L.RTDM_I8
+        self._release()
+        return self
+
+    def _calibrate(self, h):
+        x = self._calib
+        if x.dtype == torch.uint8:
+            kind, hh, ww = L.RTDM_INPUT_FRAME_U8, x.shape[1], x.shape[2]
+        else:
+            kind = L.RTDM_INPUT_NCHW_F32 if x.dtype == torch.float32 else L.RTDM_INPUT_NCHW_F16
+            hh, ww = x.shape[2], x.shape[3]
+        cap = self._handle_key[1]
+        with torch.cuda.device(x.device):
+            for i in range(0, x.shape[0], cap):
+                c = x[i:i + cap]
+                L.check(L.lib().rtdm_classifier_calibrate(h, L.ptr(c), kind, c.shape[0], hh, ww,
+                                                          1 if i == 0 else 0, L.stream_ptr()))
 
     def _release(self):
         if self._handle is not None:
@@ -109,7 +137,17 @@ class _ACFFClassifier(torch.nn.Module):
                                                ctypes.byref(h)))
         self._handle = h
         self._handle_key = (key, cap)
+        if self._dtype == L.RTDM_I8:
+            self._calibrate(h)
         return h
+
+    def describe(self, n: int = 1) -> str:
+        """Text dump of the launch plan (one line per ACFF block: kernel, int8) of a handle for n."""
+        h = self._get_handle(n)
+        need = L.lib().rtdm_classifier_describe(h, None, 0)
+        buf = ctypes.create_string_buffer(int(need) + 1)
+        L.lib().rtdm_classifier_describe(h, buf, len(buf))
+        return buf.value.decode()
 
     # ---------------------------------------------------------------- forward --
     def forward(self, x: torch.Tensor) -> torch.Tensor:
