@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--classifier", default="ernet", choices=["ernet", "squeeze-ernet", "squeeze-redconv", "none"],
                     help="none: detection only (BASELINE config 3)")
     ap.add_argument("--dtype", default="f16", choices=["f16", "f32", "i8"],
-                    help="i8: int8-quantised detector (BASELINE config 5; classifier fp16)")
+                    help="i8: int8-quantised detector (BASELINE config 5) and classifier ACFF fusion GEMMs")
     ap.add_argument("--conf", type=float, default=0.3)
     ap.add_argument("--iou", type=float, default=0.4)
     ap.add_argument("--max-det", type=int, default=300)
@@ -148,7 +148,7 @@ def build(args, world, rank):
     if args.dtype in ("f16", "i8"):
         det.half() if args.dtype == "f16" else det.int8(calib)
         if use_cls:
-            cls.half()
+            cls.half() if args.dtype == "f16" else cls.int8(calib)
     pipes = []
     for j in range(args.inflight):
         if j:  # another instance: own device weights, arenas, buffers and streams
@@ -159,7 +159,7 @@ def build(args, world, rank):
             if args.dtype in ("f16", "i8"):
                 det.half() if args.dtype == "f16" else det.int8(calib)
                 if use_cls:
-                    cls.half()
+                    cls.half() if args.dtype == "f16" else cls.int8(calib)
         pipes.append(TwoStagePipeline(cls, det, args.conf, args.iou, args.max_det, overlap=bool(args.overlap),
                                       priority=bool(args.priority), graphs=bool(args.graphs)))
     return pipes, text, stream, sd
