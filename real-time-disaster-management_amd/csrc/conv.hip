@@ -232,6 +232,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_f16(ConvArgs a) {
 constexpr int kStemRows = 4;      // output rows per block, plain stem
 constexpr int kStemRowsPool = 4;  // output rows per block, pooled stem (2 waves per quad row; 8 measured slower)
 __host__ __device__ constexpr int stem_rows(bool pool) { return pool ? kStemRowsPool : kStemRows; }
+// LDS columns past the staged row that the pooled loop's last two tiles may read: quad
+// x <= qw + 10 -> column <= (ow + 21) * s + 4, i.e. 22 * s + pad past the staged columns
+__host__ __device__ constexpr int stem_xcols(bool pool, int s) { return pool ? 22 * s + 2 : 0; }
 
 __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
   const _Float16 ha = (_Float16)a, hb = (_Float16)b;
@@ -251,6 +254,7 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
   const int oy0 = (blockIdx.x - n * bpi) * ROWS;
   const int nrows = (ROWS - 1) * s + 3;
   const int cols = (a.ow - 1) * s - pad + 5;  // LDS column = x + 1, x in [-1, (ow-1)*s - pad + 3]
+  const int ls = cols + stem_xcols(POOL, s);   // LDS row stride (overrun columns: never staged)
   const int iy0 = oy0 * s - pad;
   const int H = a.ih, W = a.iw;
 
@@ -270,7 +274,7 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
       const uint32_t b[12] = {d0 & 255u, (d0 >> 8) & 255u, (d0 >> 16) & 255u, d0 >> 24,
                               d1 & 255u, (d1 >> 8) & 255u, (d1 >> 16) & 255u, d1 >> 24,
                               d2 & 255u, (d2 >> 8) & 255u, (d2 >> 16) & 255u, d2 >> 24};
-      uint2* dst = stem_lds + r * cols + 4 * g + 1;
+      uint2* dst = stem_lds + r * ls + 4 * g + 1;
 #pragma unroll
       for (int p = 0; p < 4; ++p)
         dst[p] = make_uint2(pack_h2((float)b[3 * p], (float)b[3 * p + 1]), pack_h2((float)b[3 * p + 2], 0.f));
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
     const int npad = cols - W;  // LDS column 0 and columns W+1 .. cols-1 are padding
     for (int idx = tid; idx < nrows * npad; idx += 256) {
       const int r = idx / npad, k = idx - r * npad;
-      stem_lds[r * cols + (k == 0 ? 0 : W + k)] = make_uint2(0u, 0u);
+      stem_lds[r * ls + (k == 0 ? 0 : W + k)] = make_uint2(0u, 0u);
     }
   } else {
     for (int idx = tid; idx < nrows * cols; idx += 256) {
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
             v[c] = (float)((const _Float16*)a.in)[((size_t)(n * H + y) * W + x) * a.in_cs + a.in_co + c];
         }
       }
-      stem_lds[idx] = make_uint2(pack_h2(v[0], v[1]), pack_h2(v[2], 0.f));
+      stem_lds[r * ls + lc] = make_uint2(pack_h2(v[0], v[1]), pack_h2(v[2], 0.f));
     }
   }
 
@@ -350,8 +354,13 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
     if (py >= qh) return;
     const int d = p & 3;
     const int ly = 2 * tr + (d >> 1);  // LDS row of kh = 0 (stride 1 / 2 scaled below)
-    const uint2* rowk0 = stem_lds + (ly * s + kh0) * cols;
-    const uint2* rowk2 = stem_lds + (ly * s + 2) * cols;
+    // lane's LDS reads for the wave's first tile (tx = wid & 1); a tile step of 2 is 16*s
+    // columns and the loop step of 4 tiles 32*s.  Pixels past the row (qx >= qw) read the
+    // overrun columns and are never stored.  The second K half's lanes g >= 2 (G = 6, 7)
+    // read kh = 2 pixels again, against zero weights (pack_stem): finite x 0, no masking.
+    const int lx0 = (2 * ((wid & 1) * 4 + (p >> 2)) + (d & 1)) * s - pad + 1;
+    const uint2* rk0 = stem_lds + (ly * s + kh0) * ls + lx0 + 2 * pr0;
+    const uint2* rk2 = stem_lds + (ly * s + 2) * ls + lx0 + 2 * (g & 1);
     _Float16* pool_row = (_Float16*)e.pool.ptr + ((size_t)n * qh + py) * qw * e.pool.cs + e.pool.co;
     // Darknet stem (no BN affine after the fold, LeakyReLU / linear): LeakyReLU as
     // max(x, slope x) (0 < slope < 1; 1 = linear), no per-value branches
@@ -361,18 +370,14 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
     // chains per wave instead of one latency-bound chain; the loop is unswitched on `lean`
     auto run = [&](auto lean_c) {
     constexpr bool LEAN = decltype(lean_c)::value;
-    for (int tx0 = wid & 1; tx0 * 4 < qw; tx0 += 4) {
+    for (int tx0 = wid & 1, off = 0; tx0 * 4 < qw; tx0 += 4, off += 32 * s) {
       h8 bf0[2], bf1[2];
       int oq[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int tx = tx0 + 2 * u;
-        const int qx = tx * 4 + (p >> 2);
-        const int ox = 2 * (qx < qw ? qx : qw - 1) + (d & 1);
-        const int lx = ox * s - pad + 1;
-        const uint2 b00 = rowk0[lx + 2 * pr0], b01 = rowk0[lx + 2 * pr0 + 1];
-        uint2 b10 = rowk2[lx + 2 * (g & 1)], b11 = rowk2[lx + 2 * (g & 1) + 1];
-        if (g >= 2) b10 = b11 = make_uint2(0u, 0u);
+        const int tx = tx0 + 2 * u, o = off + u * 16 * s;
+        const uint2 b00 = rk0[o], b01 = rk0[o + 1];
+        const uint2 b10 = rk2[o], b11 = rk2[o + 1];
         bf0[u] = __builtin_bit_cast(h8, (u32x4{b00.x, b00.y, b01.x, b01.y}));
         bf1[u] = __builtin_bit_cast(h8, (u32x4{b10.x, b10.y, b11.x, b11.y}));
         oq[u] = tx * 4 + g;  // pooled x of this lane's output quad
@@ -422,8 +427,8 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
       const int ox = tx * 16 + p;
       const bool valid = ox < a.ow;
       const int lx = (valid ? ox : a.ow - 1) * s - pad + 1;
-      const uint2* rowk0 = stem_lds + (tr * s + kh0) * cols;
-      const uint2* rowk2 = stem_lds + (tr * s + 2) * cols;
+      const uint2* rowk0 = stem_lds + (tr * s + kh0) * ls;
+      const uint2* rowk2 = stem_lds + (tr * s + 2) * ls;
       const uint2 b00 = rowk0[lx + 2 * pr0], b01 = rowk0[lx + 2 * pr0 + 1];
       uint2 b10 = rowk2[lx + 2 * (g & 1)], b11 = rowk2[lx + 2 * (g & 1) + 1];
       if (g >= 2) b10 = b11 = make_uint2(0u, 0u);
@@ -455,7 +460,7 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
 
 static size_t stem3_lds_bytes(const ConvArgs& a) {
   const int nrows = (stem_rows(a.quad != 0) - 1) * a.stride + 3;
-  const int cols = (a.ow - 1) * a.stride - a.pad + 5;
+  const int cols = (a.ow - 1) * a.stride - a.pad + 5 + stem_xcols(a.quad != 0, a.stride);
   return (size_t)nrows * cols * sizeof(uint2);
 }
 // --------------------------------------------------------------------------

@@ -307,17 +307,32 @@ __device__ __forceinline__ void epi_vec8_lean(const ConvArgs& a, int m0, int c0,
 // YOLO-head variant of epi_vec8: bias -> activation -> optional scale/shift -> decode
 // (or raw) into io, the only output.  Same operations, in the same order, as the io
 // branch of epi_vec8 (bit-identical), without the code of the other branches.
-__device__ __forceinline__ void epi_vec8_io(const ConvArgs& a, int m0, int c0, const float (&v)[4][8]) {
+// Channel constants of the 8 channels c0..c0+7: bias, scale, shift and the anchor of
+// the w/h channels (epi_io_consts; conv_pipe loads them at the tile's start).
+__device__ __forceinline__ void epi_io_consts(const ConvArgs& a, int c0, float (&bias)[8], float (&sc)[8],
+                                              float (&sh)[8], float (&anc)[8]) {
   const Epilogue& e = a.e;
   const int nc = a.cout - c0 < 8 ? a.cout - c0 : 8;
-  float bias[8], sc[8], sh[8];
+  int ai = c0 / e.no, k = c0 - ai * e.no;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const bool cv = j < nc;
     bias[j] = (e.bias && cv) ? e.bias[c0 + j] : 0.f;
     sc[j] = (e.scale && cv) ? e.scale[c0 + j] : 1.f;
     sh[j] = (e.scale && cv) ? e.shift[c0 + j] : 0.f;
+    anc[j] = (cv && !e.raw && (k == 2 || k == 3)) ? e.anchor_vec[2 * ai + (k - 2)] : 0.f;
+    if (++k == e.no) {
+      k = 0;
+      ++ai;
+    }
   }
+}
+
+__device__ __forceinline__ void epi_vec8_io(const ConvArgs& a, int m0, int c0, const float (&v)[4][8],
+                                            const float (&bias)[8], const float (&sc)[8], const float (&sh)[8],
+                                            const float (&anc)[8]) {
+  const Epilogue& e = a.e;
+  const int nc = a.cout - c0 < 8 ? a.cout - c0 : 8;
   int pn, poy, pox;
   row_to_pix(a, m0, pn, poy, pox);
   const size_t plane = (size_t)a.oh * a.ow;
@@ -342,7 +357,7 @@ __device__ __forceinline__ void epi_vec8_io(const ConvArgs& a, int m0, int c0, c
         else if (k < 2)
           o = (__frcp_rn(1.f + __expf(-x)) + (float)(k == 0 ? ox : oy)) * e.ystride;
         else if (k < 4)
-          o = (__expf(x) * e.anchor_vec[2 * ai + (k - 2)]) * e.ystride;
+          o = (__expf(x) * anc[j]) * e.ystride;
         else
           o = __frcp_rn(1.f + __expf(-x));
         e.io[(pix_io + (size_t)ai * plane) * e.no + k] = o;
@@ -353,6 +368,46 @@ __device__ __forceinline__ void epi_vec8_io(const ConvArgs& a, int m0, int c0, c
       }
     }
   }
+}
+
+// epi_vec8_io's arithmetic in place (v <- the io values of its 4 rows x 8 channels);
+// the caller stores them (conv_pipe: coalesced per anchor plane)
+__device__ __forceinline__ void epi_io_decode(const ConvArgs& a, int m0, int c0, float (&v)[4][8],
+                                              const float (&bias)[8], const float (&sc)[8], const float (&sh)[8],
+                                              const float (&anc)[8]) {
+  const Epilogue& e = a.e;
+  int pn, poy, pox;
+  row_to_pix(a, m0, pn, poy, pox);
+  const int ai0 = c0 / e.no, k0 = c0 - ai0 * e.no;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    int n, oy, ox;
+    row_pix4(a, m0, r, pn, poy, pox, n, oy, ox);
+    int k = k0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = v[r][j] + bias[j];
+      if (e.act == ACT_LEAKY) t = t > 0.f ? t : t * e.slope;
+      const float x = t * sc[j] + sh[j];
+      float o;
+      if (e.raw)
+        o = x;
+      else if (k < 2)
+        o = (__frcp_rn(1.f + __expf(-x)) + (float)(k == 0 ? ox : oy)) * e.ystride;
+      else if (k < 4)
+        o = (__expf(x) * anc[j]) * e.ystride;
+      else
+        o = __frcp_rn(1.f + __expf(-x));
+      v[r][j] = o;
+      if (++k == e.no) k = 0;
+    }
+  }
+}
+
+__device__ __forceinline__ void epi_vec8_io(const ConvArgs& a, int m0, int c0, const float (&v)[4][8]) {
+  float bias[8], sc[8], sh[8], anc[8];
+  epi_io_consts(a, c0, bias, sc, sh, anc);
+  epi_vec8_io(a, m0, c0, v, bias, sc, sh, anc);
 }
 
 inline bool epi_io_ok(const ConvArgs& a) {

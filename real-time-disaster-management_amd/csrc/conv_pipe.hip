@@ -233,7 +233,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // the K-loop.  Register epilogue: the 4 channels (4g..4g+3 of each 16-column block)
   // of this lane's accumulators.  Fused head: the FN columns of this lane's accumulators.
   constexpr int CG = BN / 8;
-  float lb[8], ls[8], lh[8];
+  float lb[8], ls[8], lh[8], la[8];
   f4 rb[REG ? FN : 1];
   if constexpr (REG) {
 #pragma unroll
@@ -250,6 +250,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       ls[j] = cv && a.e.scale ? a.e.scale[c0 + j] : 1.f;
       lh[j] = cv && a.e.scale ? a.e.shift[c0 + j] : 0.f;
     }
+  } else if constexpr ((ABL & 1024) != 0) {  // stand-alone head: + the w/h anchors
+    const int c0 = n_base + (tid % CG) * 8;
+    if (c0 < a.cout) epi_io_consts(a, c0, lb, ls, lh, la);
   }
   float dq[FN];  // int8: per-output-channel dequantisation of this lane's accumulator columns
   f4 dq4[REG && I8 ? FN : 1];
@@ -670,6 +673,44 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   __syncthreads();
   constexpr int UNITS = (BM / 4) * CG;
   static_assert(NT % CG == 0, "channel group per thread");
+  if constexpr ((ABL & 1024) != 0) {
+    if (!a.quad) {  // (head convs are never quad-ordered; the per-unit stores below stay for them)
+      // stand-alone YOLO head: decode in place in the C tile (same operations as
+      // epi_vec8_io), then write io anchor plane by anchor plane: a plane's rows of
+      // consecutive pixels are one contiguous run of io, stored by consecutive lanes
+      // (the per-unit stores were 4-byte scatters, one io row per lane)
+      for (int u = tid; u < UNITS; u += NT) {
+        const int q = u / CG, gg = u - (u / CG) * CG;
+        const int m0 = m_base + q * 4, c0 = n_base + gg * 8;
+        if (m0 >= a.M || c0 >= a.cout) continue;
+        float v[4][8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[r][j] = Cs[(q * 4 + r) * kPCstr + gg * 8 + j];
+        epi_io_decode(a, m0, c0, v, lb, ls, lh, la);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) Cs[(q * 4 + r) * kPCstr + gg * 8 + j] = v[r][j];
+      }
+      __syncthreads();
+      const Epilogue& e = a.e;
+      const int no = e.no, plane = a.oh * a.ow;
+      const int rows = a.M - m_base < BM ? a.M - m_base : BM;
+      const int nch = a.cout - n_base < BN ? a.cout - n_base : BN;
+      const int per_a = rows * no;
+      for (int ai = 0; ai * no < nch; ++ai) {
+        const size_t aoff = (size_t)(n_base / no + ai) * plane;
+        for (int f = tid; f < per_a; f += NT) {
+          const int r = f / no, k = f - r * no;
+          const int m = m_base + r, n = m / plane, p = m - n * plane;
+          e.io[((size_t)n * e.io_rows + e.io_off + p + aoff) * no + k] = Cs[r * kPCstr + ai * no + k];
+        }
+      }
+      return;
+    }
+  }
   for (int u = tid; u < UNITS; u += NT) {
     const int q = u / CG, gg = u - (u / CG) * CG;
     if constexpr ((ABL & 64) != 0) {
@@ -686,7 +727,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     if constexpr ((ABL & 128) != 0)
       epi_vec8_lean<(ABL & 256) != 0>(a, m0, c0, v, lb, ls, lh);
     else if constexpr ((ABL & 1024) != 0)
-      epi_vec8_io(a, m0, c0, v);  // stand-alone YOLO head: decode -> io only
+      epi_vec8_io(a, m0, c0, v, lb, ls, lh, la);  // stand-alone YOLO head: decode -> io only
     else
       epi_vec8(a, m0, c0, v);
   }

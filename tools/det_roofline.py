@@ -29,6 +29,9 @@ ap.add_argument("--bm", type=int, default=0, help="force conv_pipe tile rows (25
 args = ap.parse_args()
 L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", args.bm))
 L.check(L.lib().rtdm_set_tuning(b"conv_pipe_korder", int(os.environ.get("KORDER", "1"))))
+for kv in filter(None, os.environ.get("TUNE", "").split(",")):  # TUNE="key=v,key=v" (diagnostics)
+    k, v = kv.split("=")
+    L.check(L.lib().rtdm_set_tuning(k.encode(), int(v)))
 text = open(os.path.join(ROOT, "real-time-disaster-management_amd", "rtdm", "cfg", args.cfg + ".cfg")).read()
 d = Darknet(text, (args.img, args.img))
 cal = load_calibration(args.cfg)
