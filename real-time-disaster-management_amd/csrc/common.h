@@ -285,7 +285,7 @@ void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, 
 void launch_upsample(View iv, int n, int h, int w, int c, int f, View ov, int dtype, hipStream_t s);
 // F.interpolate(mode="nearest", size=(oh, ow)): src = min(floor(dst * (in / out)), in - 1)
 // out = a + b (fp32 sum, rounded once), NHWC views of one shape
-void launch_add(View a, View b, int n, int h, int w, int c, View ov, int dtype, hipStream_t s);
+void launch_add(View a, View b, int n, int h, int w, int c, int cb, View ov, int dtype, hipStream_t s);
 void launch_resize_nearest(View iv, int n, int h, int w, int c, View ov, int oh, int ow, int dtype, hipStream_t s);
 void launch_copy_slice(View iv, int n, int h, int w, int c, View ov, int dtype, hipStream_t s);
 void launch_cls_tail(const void* in, int n, int h, int w, int c, const float* w2 /*[5][c]*/, int pool_pad,

@@ -401,7 +401,11 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
           cur_h = s.oh * 2;
           cur_w = s.ow * 2;
         } else if (nx.type == "shortcut" && only_next && nx.ints("from").size() == 1 &&
-                   resolve_ref(i + 1, nx.ints("from")[0]) != i && !nx.has("weights_type")) {
+                   resolve_ref(i + 1, nx.ints("from")[0]) != i && !nx.has("weights_type") &&
+                   h.layer_tensor[resolve_ref(i + 1, nx.ints("from")[0])] >= 0 &&
+                   h.tensors[h.layer_tensor[resolve_ref(i + 1, nx.ints("from")[0])]].c == filters) {
+          // same-channel shortcut fused as the residual epilogue; a channel mismatch runs the
+          // unfused ST_ADD below (weightedFeatureFusion's slicing)
           const int src = resolve_ref(i + 1, nx.ints("from")[0]);
           const int st = h.layer_tensor[src];
           RTDM_REQUIRE(st >= 0, RTDM_E_UNSUPPORTED, "cfg: shortcut source not materialisable");
@@ -654,12 +658,14 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         cur_w = ww;
       }
     } else if (t == "shortcut") {
-      // unfused weightedFeatureFusion (models.py:135-155), unweighted, same shapes
+      // unfused weightedFeatureFusion (models.py:135-155), unweighted; channel counts may differ
+      // (dc > 0: the residual is added into the first ac channels; dc < 0: only its first nc
+      // channels are read), spatial shapes must agree
       RTDM_REQUIRE(!d.has("weights_type") && d.ints("from").size() == 1 && cur_t >= 0, RTDM_E_UNSUPPORTED,
                    "cfg: unsupported shortcut at layer " + std::to_string(i));
       const int rt = h.layer_tensor[resolve_ref(i, d.ints("from")[0])];
-      RTDM_REQUIRE(rt >= 0 && h.tensors[rt].c == cur_c && h.tensors[rt].h == cur_h && h.tensors[rt].w == cur_w,
-                   RTDM_E_UNSUPPORTED, "cfg: shortcut with channel/shape mismatch unsupported (layer " + std::to_string(i) + ")");
+      RTDM_REQUIRE(rt >= 0 && h.tensors[rt].h == cur_h && h.tensors[rt].w == cur_w, RTDM_E_UNSUPPORTED,
+                   "cfg: shortcut with spatial shape mismatch unsupported (layer " + std::to_string(i) + ")");
       Step ad;
       ad.kind = ST_ADD;
       ad.layer = i;
@@ -977,8 +983,8 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       launch_dw3_sum(iv.ptr, iv.cs, iv.co, n, st.ih, st.iw, st.cin, h.blob.at<float>(st.dw_w_off),
                      h.blob.at<float>(st.dw_b_off), ov.ptr, h.dtype, s);
     } else if (st.kind == ST_ADD) {
-      launch_add(tensor_view(h, st.in_t), tensor_view(h, st.res_t), n, st.ih, st.iw, st.cin, tensor_view(h, st.out_t),
-                 h.dtype, s);
+      launch_add(tensor_view(h, st.in_t), tensor_view(h, st.res_t), n, st.ih, st.iw, st.cin,
+                 std::min(st.cin, h.tensors[st.res_t].c), tensor_view(h, st.out_t), h.dtype, s);
     } else if (st.kind == ST_RESIZE) {
       launch_resize_nearest(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, tensor_view(h, st.out_t), st.oh, st.ow,
                             h.dtype, s);

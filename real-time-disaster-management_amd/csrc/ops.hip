@@ -466,30 +466,33 @@ void launch_upsample(View iv, int n, int h, int w, int c, int f, View ov, int dt
   RTDM_HIP(hipGetLastError());
 }
 
-// Unfused [shortcut] (weightedFeatureFusion.forward, models.py:135-155, same shapes).
+// Unfused [shortcut] (weightedFeatureFusion.forward, models.py:135-155): out has the current
+// map's c channels; the first cb of them get the residual added (cb = min(c, residual
+// channels): dc > 0 adds into x[:, :ac], dc < 0 reads only a[:, :nc]); the rest are copied.
 template <typename T>
 __global__ __launch_bounds__(256) void add_kernel(const T* __restrict__ a, int a_cs, int a_co, const T* __restrict__ b,
-                                                  int b_cs, int b_co, int64_t pix, int c, T* __restrict__ out,
+                                                  int b_cs, int b_co, int64_t pix, int c, int cb, T* __restrict__ out,
                                                   int o_cs, int o_co) {
   const int64_t total = pix * c;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int ch = (int)(idx % c);
     const int64_t p = idx / c;
-    out[p * o_cs + o_co + ch] = (T)((float)a[p * a_cs + a_co + ch] + (float)b[p * b_cs + b_co + ch]);
+    const T x = a[p * a_cs + a_co + ch];
+    out[p * o_cs + o_co + ch] = ch < cb ? (T)((float)x + (float)b[p * b_cs + b_co + ch]) : x;
   }
 }
 
-void launch_add(View a, View b, int n, int h, int w, int c, View ov, int dtype, hipStream_t s) {
+void launch_add(View a, View b, int n, int h, int w, int c, int cb, View ov, int dtype, hipStream_t s) {
   const int64_t pix = (int64_t)n * h * w;
   if (pix * c <= 0) return;
   const int g = grid_for(pix * c, 256);
   if (dtype == RTDM_F16)
     hipLaunchKernelGGL(add_kernel<_Float16>, dim3(g), dim3(256), 0, s, (const _Float16*)a.ptr, a.cs, a.co,
-                       (const _Float16*)b.ptr, b.cs, b.co, pix, c, (_Float16*)ov.ptr, ov.cs, ov.co);
+                       (const _Float16*)b.ptr, b.cs, b.co, pix, c, cb, (_Float16*)ov.ptr, ov.cs, ov.co);
   else
     hipLaunchKernelGGL(add_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)a.ptr, a.cs, a.co,
-                       (const float*)b.ptr, b.cs, b.co, pix, c, (float*)ov.ptr, ov.cs, ov.co);
+                       (const float*)b.ptr, b.cs, b.co, pix, c, cb, (float*)ov.ptr, ov.cs, ov.co);
   RTDM_HIP(hipGetLastError());
 }
 

@@ -95,6 +95,76 @@ def test_planner_fusions_yolov3_shortcuts():
     assert len(re.findall(r"res=conv|res=\w+\d+\[", plan)) == 23  # every shortcut fused as a residual epilogue
 
 
+_SHORTCUT_MISMATCH = """[net]
+width=32
+height=32
+channels=3
+
+[convolutional]
+batch_normalize=1
+filters=8
+size=3
+stride=1
+pad=1
+activation=leaky
+
+[convolutional]
+batch_normalize=1
+filters=16
+size=1
+stride=1
+pad=1
+activation=leaky
+
+[shortcut]
+from=-2
+activation=linear
+
+[convolutional]
+batch_normalize=1
+filters=8
+size=3
+stride=1
+pad=1
+activation=leaky
+
+[shortcut]
+from=-2
+activation=linear
+
+[convolutional]
+size=1
+stride=1
+pad=1
+filters=14
+activation=linear
+
+[yolo]
+mask=0,1
+anchors=10,14, 23,27
+classes=2
+num=2
+"""
+
+
+def test_planner_shortcut_channel_mismatch():
+    """weightedFeatureFusion with dc > 0 (16-channel map + 8-channel residual) and dc < 0
+    (8-channel map + 16-channel residual), models.py:146-154: planned as unfused adds whose
+    output keeps the current map's channels (the GPU parity test runs it vs the oracle)."""
+    from rtdm import _lib as L
+    h = ctypes.c_void_p()
+    L.check(L.lib().rtdm_detector_create(_SHORTCUT_MISMATCH.encode(), 32, 32, 1, None, 0, 2, ctypes.byref(h)))
+    try:
+        n = L.lib().rtdm_detector_describe(h, None, 0)
+        buf = ctypes.create_string_buffer(int(n))
+        L.lib().rtdm_detector_describe(h, buf, n)
+        plan = buf.value.decode()
+    finally:
+        L.lib().rtdm_detector_destroy(h)
+    assert plan.count("shortcut add") == 2, plan
+    assert "res=-" in plan and not re.search(r"res=[^-]", plan), plan
+
+
 def test_error_paths_return_status_not_abort():
     from rtdm import _lib as L
     lib = L.lib()

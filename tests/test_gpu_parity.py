@@ -485,6 +485,26 @@ def test_acff_route_resize_shortcut_small(dev, half):
     _check_io(io.cpu().numpy(), ref.numpy(), half)
 
 
+@pytest.mark.parametrize("half", [False, True])
+def test_shortcut_channel_mismatch(dev, half):
+    """[shortcut] between maps of different channel counts (weightedFeatureFusion dc > 0 and
+    dc < 0, models.py:146-154) on the unfused add path, against the oracle's slicing."""
+    from test_abi import _SHORTCUT_MISMATCH as cfg
+    from oracle.darknet import DarknetRef
+    from rtdm.darknet import Darknet
+    from rtdm.synth import synth_darknet_weights, synth_frames
+    w = synth_darknet_weights(cfg, seed=7)
+    m = Darknet(cfg, (32, 32))
+    m.load_weight_stream(w)
+    if half:
+        m.half()
+    frames = synth_frames(3, 32, 32, seed=4)
+    io, _ = m(torch.from_numpy(frames).to(dev))
+    ref = DarknetRef(cfg, w).forward(torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0)
+    assert io.shape == ref.shape
+    _check_io(io.cpu().numpy(), ref.numpy(), half)
+
+
 # -------------------------------------------------------------------- NMS --
 def _nms_compare(io, conf, iou, multi_label=True, agnostic=False, classes=None):
     from oracle import nms as ON
