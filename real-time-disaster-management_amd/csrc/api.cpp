@@ -39,6 +39,8 @@ rtdm_status rtdm_set_tuning(const char* key, int value) {
       set_pipe_bm(value);
     else if (!strcmp(key, "conv_pipe_win"))
       set_pipe_win(value);
+    else if (!strcmp(key, "head1x1"))
+      set_head1x1(value);
     else if (!strcmp(key, "fuse_head"))
       set_fuse_head(value);
     else if (!strcmp(key, "two_streams"))

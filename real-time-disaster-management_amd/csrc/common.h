@@ -191,6 +191,11 @@ void launch_quantize(View v, int n, int h, int w, int c, const float* inv_scale,
 // conv_pipe.hip: pipelined 256x128 implicit GEMM for Cin % 64 == 0 layers
 bool conv_pipe_ok(const ConvArgs& a);
 void launch_conv_pipe(const ConvArgs& a, hipStream_t s);
+// head.hip: stand-alone YOLO head (1x1, Cin % 128 == 0, <= 32 outputs, decode into io)
+bool head1x1_ok(const ConvArgs& a);
+void launch_head1x1(const ConvArgs& a, hipStream_t s);
+const char* head1x1_name(const ConvArgs& a);
+void set_head1x1(int v);  // conv.hip: 0 = stand-alone heads on conv_pipe (A/B)
 int conv_pipe_mode();
 int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 / 128 / 64)
 void set_pipe_bm(int v);                  // 0 = cost model, else forced

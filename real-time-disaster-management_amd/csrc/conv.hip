@@ -1314,6 +1314,11 @@ int conv_pipe_mode() {
 }
 void set_conv_pipe_mode(int v) { g_conv_pipe = v < 0 ? 0 : v; }
 
+// Stand-alone YOLO head convs on head1x1_f16 (head.hip); 0 = conv_pipe's decode epilogue
+// (rtdm_set_tuning("head1x1", v), for A/B runs; bit-identical either way).
+static int g_head1x1 = 1;
+void set_head1x1(int v) { g_head1x1 = v ? 1 : 0; }
+
 static bool use_pipe(const ConvArgs& a, int dtype) {
   return dtype == RTDM_F16 && (conv_pipe_mode() > 0 || a.head_w) && conv_pipe_ok(a);
 }
@@ -1331,6 +1336,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     const int bn = direct_cfg(a.cout_pad).bn;
     return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
   }
+  if (dtype == RTDM_F16 && g_head1x1 && head1x1_ok(a)) return head1x1_name(a);
   if (use_pipe(a, dtype)) return conv_pipe_name(a);
   if (dtype == RTDM_F16 && glds_ok(a)) {
     static const char* names[2][2] = {{"conv_glds_f16<128,2>", "conv_glds_f16<128,3>"},
@@ -1375,6 +1381,8 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     launch_pool_small(a, s);
   } else if (dtype == RTDM_F16 && direct_ok(a)) {
     launch_direct(a, s);
+  } else if (dtype == RTDM_F16 && g_head1x1 && head1x1_ok(a)) {
+    launch_head1x1(a, s);
   } else if (use_pipe(a, dtype)) {
     launch_conv_pipe(a, s);
   } else if (dtype == RTDM_F16 && glds_ok(a)) {

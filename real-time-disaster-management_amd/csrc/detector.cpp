@@ -1055,7 +1055,9 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
       a.head_e.bias = (const float*)64;
     } else if (st.yolo >= 0) {
       a.e.io = (float*)64;
+      a.e.no = h.heads[st.yolo].no;
     }
+    if (st.pc.mfma) a.w = (const void*)64;
     if (st.q >= 0) {
       a.in_cs = st.cin;
       a.in_co = 0;

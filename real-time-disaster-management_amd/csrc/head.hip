@@ -1,0 +1,159 @@
+// Stand-alone YOLO head conv: the 1x1 conv (Cin % 128 == 0, <= 32 outputs) in front of a
+// [yolo] layer whose producer cannot carry it as a fused head (Cin > 128: yolov4-tiny L15 /
+// L22, the three yolov3 / yolov3-spp heads), plus the YOLOLayer inference decode into io
+// (victim_localization/yolov3/models.py:23-44 conv, :204-258 YOLOLayer, create_grids
+// :422-436).
+//
+// conv_pipe's tile (128 output channels, LDS ring, C tile through LDS, barriers) spent
+// most of a head launch in per-tile latency: 28 real columns of 128, 2-8 K-blocks, then
+// three barrier-separated epilogue phases.  Here each wave owns 16 * FM rows and all 32
+// (padded) head channels and needs no LDS and no barrier: A fragments (8 input channels
+// of one pixel per lane) and B fragments (8 K of one head channel) come straight from
+// global memory (the weights, 32 x Cin fp16, stay in L1/L2), two 128-deep K chunks in
+// flight, v_mfma_f32_16x16x32_f16 in the same K order as conv_pipe (bit-identical
+// accumulators), and the decode runs on the accumulators in registers with the same
+// per-element operations as epi_io_decode.
+#include "conv_epi.h"
+
+namespace rtdm {
+
+namespace {
+constexpr int kHeadCh = 4;  // 32-deep K steps per chunk (128 K)
+}
+
+template <int FM>
+__global__ __launch_bounds__(256) void head1x1_f16(ConvArgs a) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  const int m_base = (blockIdx.x * 4 + wid) * (16 * FM);
+  if (m_base >= a.M) return;
+  const Epilogue& e = a.e;
+
+  // per-lane operand rows: A = pixel m_base + 16 tm + fr (clamped; its outputs are not
+  // stored), K slice 8g..8g+7 of each 32-deep step; B = head channel 16 tn + fr
+  const _Float16* ap[FM];
+#pragma unroll
+  for (int tm = 0; tm < FM; ++tm) {
+    int m = m_base + tm * 16 + fr;
+    m = m < a.M ? m : a.M - 1;
+    ap[tm] = (const _Float16*)a.in + (size_t)m * a.in_cs + a.in_co + 8 * g;
+  }
+  const _Float16* bp[2];
+#pragma unroll
+  for (int tn = 0; tn < 2; ++tn) bp[tn] = (const _Float16*)a.w + (size_t)(tn * 16 + fr) * a.kpad + 8 * g;
+
+  f4 acc[FM][2];
+#pragma unroll
+  for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = f4{0.f, 0.f, 0.f, 0.f};
+
+  h8 a0[kHeadCh][FM], b0[kHeadCh][2], a1[kHeadCh][FM], b1[kHeadCh][2];
+  auto load = [&](int k0, h8(&A)[kHeadCh][FM], h8(&B)[kHeadCh][2]) {
+#pragma unroll
+    for (int s = 0; s < kHeadCh; ++s) {
+#pragma unroll
+      for (int tm = 0; tm < FM; ++tm) A[s][tm] = *(const h8*)(ap[tm] + k0 + 32 * s);
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) B[s][tn] = *(const h8*)(bp[tn] + k0 + 32 * s);
+    }
+  };
+  auto mma = [&](const h8(&A)[kHeadCh][FM], const h8(&B)[kHeadCh][2]) {
+#pragma unroll
+    for (int s = 0; s < kHeadCh; ++s)
+#pragma unroll
+      for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s][tm], B[s][tn], acc[tm][tn], 0, 0, 0);
+  };
+  const int K = a.cin, CK = 32 * kHeadCh;
+  load(0, a0, b0);
+  int k0 = 0;
+  for (; k0 + 2 * CK <= K; k0 += 2 * CK) {
+    load(k0 + CK, a1, b1);
+    mma(a0, b0);
+    if (k0 + 2 * CK < K) load(k0 + 2 * CK, a0, b0);
+    mma(a1, b1);
+  }
+  if (k0 < K) mma(a0, b0);  // odd chunk count: the last chunk was loaded into a0/b0
+
+  // ---- decode (epi_io_decode's per-element operations) and io stores.  Accumulator
+  //      acc[tm][tn][j] = row m_base + 16 tm + 4 g + j, head channel 16 tn + fr. ----
+  float bias[2], sc[2], sh[2], anc[2];
+  int kk[2], ai[2];
+  bool cv[2];
+#pragma unroll
+  for (int tn = 0; tn < 2; ++tn) {
+    const int c = tn * 16 + fr;
+    cv[tn] = c < a.cout;
+    ai[tn] = c / e.no;
+    kk[tn] = c - ai[tn] * e.no;
+    bias[tn] = (e.bias && cv[tn]) ? e.bias[c] : 0.f;
+    sc[tn] = (e.scale && cv[tn]) ? e.scale[c] : 1.f;
+    sh[tn] = (e.scale && cv[tn]) ? e.shift[c] : 0.f;
+    anc[tn] = (cv[tn] && !e.raw && (kk[tn] == 2 || kk[tn] == 3)) ? e.anchor_vec[2 * ai[tn] + (kk[tn] - 2)] : 0.f;
+  }
+  const size_t plane = (size_t)a.oh * a.ow;
+#pragma unroll
+  for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m_base + tm * 16 + 4 * g + j;
+      if (m >= a.M) continue;
+      int n, oy, ox;
+      row_to_pix(a, m, n, oy, ox);
+      const size_t pix_io = (size_t)n * e.io_rows + e.io_off + (size_t)oy * a.ow + ox;
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) {
+        if (!cv[tn]) continue;
+        float t = acc[tm][tn][j] + bias[tn];
+        if (e.act == ACT_LEAKY) t = t > 0.f ? t : t * e.slope;
+        const float x = t * sc[tn] + sh[tn];
+        const int k = kk[tn];
+        float o;
+        if (e.raw)
+          o = x;
+        else if (k < 2)
+          o = (__frcp_rn(1.f + __expf(-x)) + (float)(k == 0 ? ox : oy)) * e.ystride;
+        else if (k < 4)
+          o = (__expf(x) * anc[tn]) * e.ystride;
+        else
+          o = __frcp_rn(1.f + __expf(-x));
+        e.io[(pix_io + (size_t)ai[tn] * plane) * e.no + k] = o;
+      }
+    }
+}
+
+bool head1x1_ok(const ConvArgs& a) {
+  return a.ks == 1 && a.stride == 1 && a.pad == 0 && !a.quad && a.in_kind == IN_NHWC && !a.w_f32 && a.w &&
+         !a.head_w && epi_io_ok(a) && a.cout >= 1 && a.cout <= 32 && a.cout_pad >= 32 && a.cin % 128 == 0 &&
+         a.kpad >= a.cin && (a.in_cs | a.in_co) % 8 == 0 && a.kpad % 8 == 0 && a.ih == a.oh && a.iw == a.ow &&
+         a.e.no > 0;
+}
+
+static int head_fm(const ConvArgs& a) {
+  static int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
+  return (a.M + 127) / 128 >= 2 * cus ? 2 : 1;  // 2 fragments per wave once the grid is >= 2 per CU
+}
+
+const char* head1x1_name(const ConvArgs& a) { return head_fm(a) == 2 ? "head1x1_f16<2>" : "head1x1_f16<1>"; }
+
+void launch_head1x1(const ConvArgs& a, hipStream_t s) {
+  RTDM_REQUIRE(head1x1_ok(a), RTDM_E_INVALID, "head1x1: unsupported layer");
+  const int fm = head_fm(a);
+  const int64_t blocks = ((int64_t)a.M + 64 * fm - 1) / (64 * fm);
+  RTDM_REQUIRE(blocks < (1ll << 31), RTDM_E_CAPACITY, "head1x1: grid too large");
+  if (fm == 2)
+    hipLaunchKernelGGL((head1x1_f16<2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((head1x1_f16<1>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  RTDM_HIP(hipGetLastError());
+}
+
+}  // namespace rtdm

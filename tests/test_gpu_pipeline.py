@@ -277,3 +277,33 @@ def test_window_mode_bit_identical(dev, case):
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe_win", 1))
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416", "yolov3-spp-aider@608"])
+def test_head1x1_bit_identical(dev, case):
+    """Stand-alone YOLO head convs on head1x1_f16 (register-resident, no LDS) against
+    conv_pipe's decode epilogue (rtdm_set_tuning("head1x1", 0)) at b3: same io bits (same
+    MFMA K order, same per-element decode)."""
+    import ctypes
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    cfg, size = case.split("@")
+    size = int(size)
+    x = torch.from_numpy(synth_frames(3, size, size, seed=31)).to(dev)
+    outs = {}
+    try:
+        for v in (0, 1):
+            L.check(L.lib().rtdm_set_tuning(b"head1x1", v))
+            m, _, _, _ = _detector(cfg, size)
+            outs[v] = m(x)[0].cpu()
+            h = m.handle(3)
+            names = []
+            for i in range(L.lib().rtdm_detector_num_steps(h)):
+                nm = ctypes.create_string_buffer(64)
+                L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, None, None, None))
+                names.append(nm.value.decode())
+            n_head = sum(n.startswith("head1x1_f16") for n in names)
+            assert n_head == (0 if v == 0 else (2 if cfg.startswith("yolov4") else 3)), names
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"head1x1", 1))
+    assert torch.equal(outs[0], outs[1])
