@@ -41,6 +41,8 @@ rtdm_status rtdm_set_tuning(const char* key, int value) {
       set_pipe_win(value);
     else if (!strcmp(key, "head1x1"))
       set_head1x1(value);
+    else if (!strcmp(key, "dw3_tile"))
+      set_dw3_tile(value);
     else if (!strcmp(key, "fuse_head"))
       set_fuse_head(value);
     else if (!strcmp(key, "two_streams"))

@@ -245,6 +245,7 @@ void launch_dw3_acff(const void* in, int in_cs, int in_co, int n, int h, int w, 
 void launch_dw3_sum(const void* in, int in_cs, int in_co, int n, int h, int w, int c, const float* wts,
                     const float* bsum, void* out, int dtype, hipStream_t s);
 bool dw3_sum_vec_ok(int c, int in_cs, int in_co, int dtype);
+void set_dw3_tile(int v);  // ops.hip: YOLO-ACFF depthwise on the LDS-tiled kernel (1) or the vector one (0)
 bool dw3_sum_tile_ok(int c, int in_cs, int in_co, int dtype);
 // acff.hip: fused ACFF block (dw3 -> concat -> 1x1 -> LeakyReLU -> BN affine -> opt. 2x2 pool), fp16
 bool acff_fused_ok(int cin, int cout_pad, int kpad);

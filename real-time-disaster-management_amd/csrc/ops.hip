@@ -200,20 +200,52 @@ __global__ __launch_bounds__(256) void dw3_sum_kernel(const T* __restrict__ in, 
 }
 
 // LDS-tiled fp16 form of dw3_sum_kernel for C % 64 == 0: a block stages an 8 x 32 output
-// tile's input window (14 x 38 pixels: radius 3 around the tap centre) of one 64-channel
-// slice into LDS once (68 KB, zero outside the image = the branches' zero padding), then
-// each thread computes 4 neighbouring pixels x 8 channels, reading every tap's weights
-// once per 4 pixels.  The 27 shifted reads per output come from LDS (conflict-free
-// 16-byte reads: 8 pixels x 8 channel vectors = 1 KB contiguous per wave-instruction)
-// instead of L1/L2.  Same sum order as dw3_sum_kernel (bias, branch, kh, kw).
-constexpr int kDwTH = 8, kDwTW = 32, kDwCS = 64;
+// tile's input window (14 x 38 pixels: radius 3 around the tap centre; row stride 39 so
+// vertically adjacent pixels fall in opposite LDS bank halves) of one 64-channel slice
+// into LDS once (70 KB, zero outside the image = the branches' zero padding).  Each thread
+// owns 8 neighbouring output pixels of one row x 8 channels and walks, per (branch, kernel
+// row), the 8 + 2d input pixels that row segment reads: each is read from LDS and
+// converted to fp32 ONCE and feeds its up to 3 taps (kw) in registers (the per-tap form
+// converted every operand for every tap: 1.5 VALU per MAC, here ~1).  Same sum order per
+// output as dw3_sum_kernel (bias, branch, kh, kw): bit-identical.
+constexpr int kDwTH = 8, kDwTW = 32, kDwCS = 64, kDwIWS = kDwTW + 7;
+template <int D>
+__device__ __forceinline__ void dw3_row(const uint4* __restrict__ s_row, const float* __restrict__ wp,
+                                        float (&acc)[8][8]) {
+  // s_row: this thread's channel group at the segment's first input pixel (x0 + 3 - D)
+  float w[3][8];
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[kw][j] = wp[kw * kDwCS + j];
+#pragma unroll
+  for (int i = 0; i < 8 + 2 * D; ++i) {
+    const uint4 raw = s_row[i * (kDwCS / 8)];
+    const uint32_t u[4] = {raw.x, raw.y, raw.z, raw.w};
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[2 * j] = (float)__builtin_bit_cast(_Float16, (uint16_t)(u[j] & 0xffffu));
+      x[2 * j + 1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(u[j] >> 16));
+    }
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int p = i - kw * D;  // output pixel this input pixel feeds through tap kw
+      if (p >= 0 && p < 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[p][j] = fmaf(w[kw][j], x[j], acc[p][j]);
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256, 2) void dw3_sum_tile_kernel(const _Float16* __restrict__ in, int in_cs, int in_co,
                                                            int n, int h, int w, int c, const float* __restrict__ wts,
                                                            const float* __restrict__ bsum,
                                                            _Float16* __restrict__ out) {
   typedef _Float16 h8t __attribute__((ext_vector_type(8)));
-  constexpr int IH = kDwTH + 6, IW = kDwTW + 6, G = kDwCS / 8, QW = kDwTW / 4;
-  __shared__ h8t s_in[IH * IW * G];
+  constexpr int IH = kDwTH + 6, IW = kDwTW + 6, G = kDwCS / 8;
+  __shared__ uint4 s_in[(IH * kDwIWS * G + 63) / 64 * 64];  // whole 64-vector DMA rows
   __shared__ float s_w[28 * kDwCS];
   const int oh = h - 2, ow = w - 2;
   const int tx = (ow + kDwTW - 1) / kDwTW, ty = (oh + kDwTH - 1) / kDwTH, tc = c / kDwCS;
@@ -229,64 +261,67 @@ __global__ __launch_bounds__(256, 2) void dw3_sum_tile_kernel(const _Float16* __
     const int t = i / kDwCS, j = i - t * kDwCS;
     s_w[i] = t < 27 ? wts[t * c + c0 + j] : bsum[c0 + j];
   }
-  const _Float16* src = in + (size_t)b * h * w * in_cs + in_co + c0;
-  for (int i = threadIdx.x; i < IH * IW * G; i += 256) {
-    const int g = i % G, px = i / G;
-    const int gy = oy0 - 2 + px / IW, gx = ox0 - 2 + px % IW;
-    h8t v = {};
-    if ((unsigned)gy < (unsigned)h && (unsigned)gx < (unsigned)w) v = *(const h8t*)(src + ((size_t)gy * w + gx) * in_cs + g * 8);
-    s_in[i] = v;
+  // input window -> LDS by LDS-DMA (buffer_load ... lds): every 16-byte vector of the
+  // window in flight at once (a register-staged loop waited on each load in turn); a lane
+  // whose pixel lies outside the image (or in the stride's pad column) loads from an
+  // out-of-range offset, which returns zeros
+  {
+    typedef __attribute__((address_space(3))) void* lds_p;
+    const _Float16* src = in + (size_t)b * h * w * in_cs + in_co + c0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)src, 0, (int)((((int64_t)h * w - 1) * in_cs + kDwCS) * 2), 0x00020000);
+    constexpr int NV = IH * kDwIWS * G;  // 16-byte vectors of the LDS image
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int k = wid; k * 64 < NV; k += 4) {
+      const int e = k * 64 + lane;
+      const int g = e & 7, px = e >> 3;
+      const int ry = px / kDwIWS, rx = px - ry * kDwIWS;
+      const int gy = oy0 - 2 + ry, gx = ox0 - 2 + rx;
+      const bool ok = e < NV && rx < IW && (unsigned)gy < (unsigned)h && (unsigned)gx < (unsigned)w;
+      const int vo = ok ? ((gy * w + gx) * in_cs + g * 8) * 2 : (int)0x80000000;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_p)(s_in + k * 64), 16, vo, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  for (int it = threadIdx.x; it < kDwTH * QW * G; it += 256) {
-    const int g = it % G, q = it / G;
-    const int y = q / QW, x0 = (q % QW) * 4;
-    float acc[4][8];
+  // thread -> (channel group g, output row y, 8-pixel segment): lanes 8 apart take
+  // adjacent rows (opposite bank halves), 4 segments per row
+  const int g = threadIdx.x & 7, q = threadIdx.x >> 3;
+  const int y = q & 7, x0 = (q >> 3) * 8;
+  float acc[8][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float bj = s_w[27 * kDwCS + g * 8 + j];
+  for (int j = 0; j < 8; ++j) {
+    const float bj = s_w[27 * kDwCS + g * 8 + j];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) acc[p][j] = bj;
-    }
-    // one (branch, kernel row) per iteration: 3 taps x 4 pixels of operands live at a time
-    // (fully unrolled, the compiler hoisted all 108 LDS reads: 512 registers, 1 wave/SIMD)
+    for (int p = 0; p < 8; ++p) acc[p][j] = bj;
+  }
+  // (branch, kernel row) in the reference's order; kw inside dw3_row
 #pragma unroll 1
-    for (int bk = 0; bk < 9; ++bk) {
-      const int br = bk / 3, kh = bk - br * 3, d = br + 1;
-      {
-        const int ly = y + 3 + (kh - 1) * d;
+  for (int kh = 0; kh < 3; ++kh)
+    dw3_row<1>(s_in + ((y + 3 + (kh - 1)) * kDwIWS + x0 + 2) * G + g, s_w + (0 * 9 + kh * 3) * kDwCS + g * 8, acc);
+#pragma unroll 1
+  for (int kh = 0; kh < 3; ++kh)
+    dw3_row<2>(s_in + ((y + 3 + (kh - 1) * 2) * kDwIWS + x0 + 1) * G + g, s_w + (1 * 9 + kh * 3) * kDwCS + g * 8, acc);
+#pragma unroll 1
+  for (int kh = 0; kh < 3; ++kh)
+    dw3_row<3>(s_in + ((y + 3 + (kh - 1) * 3) * kDwIWS + x0) * G + g, s_w + (2 * 9 + kh * 3) * kDwCS + g * 8, acc);
+  const int oy = oy0 + y;
+  if (oy >= oh) return;
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const int lx = x0 + 3 + (kw - 1) * d;
-          const float* wp = s_w + (bk * 3 + kw) * kDwCS + g * 8;
-          float wv[8];
+  for (int p = 0; p < 8; ++p) {
+    const int ox = ox0 + x0 + p;
+    if (ox >= ow) break;
+    h8t o;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) wv[j] = wp[j];
-#pragma unroll
-          for (int p = 0; p < 4; ++p) {
-            const h8t xv = s_in[(ly * IW + lx + p) * G + g];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[p][j] = fmaf(wv[j], (float)xv[j], acc[p][j]);
-          }
-        }
-      }
-    }
-    const int oy = oy0 + y;
-    if (oy >= oh) continue;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int ox = ox0 + x0 + p;
-      if (ox >= ow) break;
-      h8t o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (_Float16)acc[p][j];
-      *(h8t*)(out + (((size_t)b * oh + oy) * ow + ox) * c + c0 + g * 8) = o;
-    }
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)acc[p][j];
+    *(h8t*)(out + (((size_t)b * oh + oy) * ow + ox) * c + c0 + g * 8) = o;
   }
 }
 
+static int g_dw3_tile = 1;  // 0: the per-pixel vector kernel (same sum order, for A/B and tests)
+void set_dw3_tile(int v) { g_dw3_tile = v ? 1 : 0; }
 bool dw3_sum_tile_ok(int c, int in_cs, int in_co, int dtype) {
-  return dtype == RTDM_F16 && c % kDwCS == 0 && in_cs % 8 == 0 && in_co % 8 == 0;
+  return g_dw3_tile && dtype == RTDM_F16 && c % kDwCS == 0 && in_cs % 8 == 0 && in_co % 8 == 0;
 }
 
 bool dw3_sum_vec_ok(int c, int in_cs, int in_co, int dtype) {

@@ -307,3 +307,22 @@ def test_head1x1_bit_identical(dev, case):
     finally:
         L.check(L.lib().rtdm_set_tuning(b"head1x1", 1))
     assert torch.equal(outs[0], outs[1])
+
+
+def test_dw3_tile_bit_identical(dev):
+    """YOLO-ACFF additive depthwise stage (the three dilated branches summed, models.py:
+    296-302): the LDS-tiled kernel (row segments, each input pixel converted once and fed to
+    its taps from registers) against the per-pixel vector kernel with the same per-output
+    sum order (rtdm_set_tuning("dw3_tile", 0)) on yolov3-acffx@416 at b2: same io bits."""
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    x = torch.from_numpy(synth_frames(2, 416, 416, seed=43)).to(dev)
+    outs = {}
+    try:
+        for v in (0, 1):
+            L.check(L.lib().rtdm_set_tuning(b"dw3_tile", v))
+            m, _, _, _ = _detector("yolov3-acffx", 416)
+            outs[v] = m(x)[0].cpu()
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"dw3_tile", 1))
+    assert torch.equal(outs[0], outs[1])
