@@ -39,6 +39,8 @@ rtdm_status rtdm_set_tuning(const char* key, int value) {
       set_pipe_bm(value);
     else if (!strcmp(key, "conv_pipe_win"))
       set_pipe_win(value);
+    else if (!strcmp(key, "conv_pipe_pf"))
+      set_pipe_pf(value);
     else if (!strcmp(key, "head1x1"))
       set_head1x1(value);
     else if (!strcmp(key, "dw3_tile"))

@@ -51,6 +51,12 @@ constexpr int kWinRows = 440;
 constexpr int kWinSmem = (2 * kWinRows * kPBK + kPNS * kPBN * kPBK + 8 * kPBK) * 2;
 static_assert(kWinSmem <= 163840, "window LDS");
 
+// s_waitcnt vmcnt(N) lgkmcnt(0), any N < 64 (gfx9 encoding: vmcnt bits 3:0 and 15:14)
+template <int N>
+__device__ __forceinline__ void wait_vmn_lgkm0() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+}
 template <int N>
 __device__ __forceinline__ void wait_vm_lgkm0() {
   if constexpr (N == 6)
@@ -103,7 +109,16 @@ __device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v
 // Register epilogue of a lean conv_pipe tile (D^T accumulators: acc[tm][tn][r] = output
 // channel n_base + wn*BN/WN + tn*16 + 4g + r of GEMM row m_base + wm*BM/WM + tm*16 + fr).
 // Same per-element operations, in the same order, as epi_vec8_lean.
-template <bool RES, int FM, int FN, int WM, int WN, int BM, typename AccT, int NDQ>
+// FIXED (cross-tile prefetch, see pipe_walk): the full-map output only (no pool / upsample,
+// no BN affine),
+// every store (and residual load) issued by every wave as a buffer op whose offset is out of
+// range for invalid lanes, so the epilogue issues exactly pipe_epi_ops() vector-memory ops and
+// the next tile can wait on its prefetched stage with an exact vmcnt.
+template <bool RES, int FM, int FN>
+__host__ __device__ constexpr int pipe_epi_ops() {
+  return FM * FN * (RES ? 2 : 1);
+}
+template <bool RES, int FM, int FN, int WM, int WN, int BM, bool FIXED = false, typename AccT, int NDQ>
 __device__ __forceinline__ void pipe_epi_regs(const ConvArgs& a, int m_base, int n_base, int wm, int wn, int lane,
                                               const AccT (&acc)[FM][FN], const f4 (&rb)[FN], const f4 (&dq4)[NDQ]) {
   constexpr bool I8 = !std::is_same_v<AccT, f4>;
@@ -113,6 +128,56 @@ __device__ __forceinline__ void pipe_epi_regs(const ConvArgs& a, int m_base, int
   const bool leaky = e.act == ACT_LEAKY;
   const float slope = e.slope;
   typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  typedef int i2 __attribute__((ext_vector_type(2)));
+  if constexpr (FIXED) {
+    // byte offsets < 2^31 - 16 (pipe_pf_ok); 0x7FFFFFF8 is past num_records: no-op store / zero load
+    const __amdgpu_buffer_rsrc_t rs_o =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((_Float16*)e.full.ptr + e.full.co), 0, 0x7FFFFFF0, 0x00020000);
+    __amdgpu_buffer_rsrc_t rs_r = rs_o;
+    if constexpr (RES)
+      rs_r = __builtin_amdgcn_make_buffer_rsrc((void*)((const _Float16*)e.res.ptr + e.res.co), 0, 0x7FFFFFF0,
+                                               0x00020000);
+#pragma unroll
+    for (int tm = 0; tm < FM; ++tm) {
+      const int m = m_base + wm * (BM / WM) + tm * 16 + fr;
+      const bool mv = m < a.M;
+      int n = 0, oy = 0, ox = 0;
+      if (mv) row_to_pix(a, m, n, oy, ox);
+      const int pix = (n * a.oh + oy) * a.ow + ox;
+#pragma unroll
+      for (int tn = 0; tn < FN; ++tn) {
+        const int c0 = n_base + wn * (BN / WN) + tn * 16 + 4 * g;
+        const bool ok = mv && c0 < a.cout;
+        f4 t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if constexpr (I8)
+            t[r] = (float)acc[tm][tn][r] * dq4[NDQ == FN ? tn : 0][r];
+          else
+            t[r] = acc[tm][tn][r];
+          t[r] = t[r] + rb[tn][r];
+          t[r] = leaky ? (t[r] > 0.f ? t[r] : t[r] * slope) : t[r];
+        }
+        if constexpr (RES) {
+          const int ro = ok ? (pix * e.res.cs + c0) * 2 : 0x7FFFFFF8;
+          const h4 rv = __builtin_bit_cast(h4, __builtin_amdgcn_raw_buffer_load_b64(rs_r, ro, 0, 0));
+          // the unconditional add would contract with the LeakyReLU product into
+          // fma(t, slope, r) (fp-contract=fast); the other epilogues round t * slope first
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            asm volatile("" : "+v"(t[r]));
+            t[r] += (float)rv[r];
+          }
+        }
+        h4 hv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hv[r] = (_Float16)t[r];
+        const int oo = ok ? (pix * e.full.cs + c0) * 2 : 0x7FFFFFF8;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i2, hv), rs_o, oo, 0, 0);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int tm = 0; tm < FM; ++tm) {
     const int m = m_base + wm * (BM / WM) + tm * 16 + fr;
@@ -197,7 +262,8 @@ __device__ __forceinline__ void pipe_epi_regs(const ConvArgs& a, int m_base, int
 // the next channel block's window, or a dummy zero load into the zero area, so every
 // stage issues the same op count for the counted waits).
 template <int ABL, int BM, bool I8 = false, bool WIN = false>
-__device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem_raw, int bid) {
+__device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem_raw, int bid, bool pf, int next,
+                                          bool pre) {
   constexpr int WM = PipeCfg<BM>::WM, WN = PipeCfg<BM>::WN;
   constexpr int BN = kPBN, BK = kPBK;              // LDS row: BK halfs = 128 bytes
   constexpr int ES = I8 ? 1 : 2, BKE = I8 ? 128 : 64;  // element bytes, K-elements per K-block
@@ -229,6 +295,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // per 16x16 block, with the 2x2 pool as two DPP max steps over quad-order rows: no
   // fp32 C tile through LDS and no barrier between the K-loop and the stores.
   constexpr bool REG = (ABL & 512) != 0;
+  constexpr bool RES_ = (ABL & 256) != 0;
+  // cross-tile prefetch (pf, register epilogue only: the LDS ring is free during it)
+  constexpr bool PF = REG;
   // Epilogue channel constants, loaded at the tile's start so their latency hides under
   // the K-loop.  Register epilogue: the 4 channels (4g..4g+3 of each 16-column block)
   // of this lane's accumulators.  Fused head: the FN columns of this lane's accumulators.
@@ -236,10 +305,12 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   float lb[8], ls[8], lh[8], la[8];
   f4 rb[REG ? FN : 1];
   if constexpr (REG) {
+    const __amdgpu_buffer_rsrc_t rs_bias = __builtin_amdgcn_make_buffer_rsrc((void*)a.e.bias, 0, a.cout * 4, 0x00020000);
 #pragma unroll
     for (int tn = 0; tn < FN; ++tn) {
       const int c0 = n_base + wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
-      rb[tn] = c0 < a.cout ? *(const f4*)(a.e.bias + c0) : f4{0.f, 0.f, 0.f, 0.f};
+      // buffer load: out-of-range channels (c0 >= cout) load zeros
+      rb[tn] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs_bias, c0 * 4, 0, 0));
     }
   } else if constexpr ((ABL & 128) != 0) {
     const int c0 = n_base + (tid % CG) * 8;
@@ -283,28 +354,49 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 
   // ---- per-lane staging state.  A op j of wave w fills tile rows 8(NA w + j) + lane/8,
   //      B op j rows 8(NB w + j) + lane/8; LDS slot lane%8 of a row holds k-vector
-  //      slot ^ ((row >> 1) & 7) (the read side applies the same involution). ----
+  //      slot ^ ((row >> 1) & 7) (the read side applies the same involution).
+  //      Per-tile part (PipeGeo): A row offsets / tap masks, the window origin, the weight
+  //      panel; built for this tile and, for the cross-tile prefetch, for the next one. ----
   const int slot = lane & 7;
-  int voff_a[WIN ? 1 : NA];
-  uint32_t vmask[WIN ? 1 : NA];
+  struct Geo {
+    int m_base, koff_n;                // koff_n: byte offset of the tile's weight panel
+    int voff_a[WIN ? 1 : NA];
+    uint32_t vmask[WIN ? 1 : NA];
+    int wp0, wv0;                      // window mode: first window row's pixel / source offset
+  };
+  const int wrow0 = 8 * wid + (lane >> 3);
+  auto make_geo = [&](int tile) {
+    Geo G;
+    const int tmt = tile / ntn;
+    G.m_base = tmt * BM;
+    G.koff_n = (tile - tmt * ntn) * BN * a.kpad * ES;
 #pragma unroll
-  for (int j = 0; j < (WIN ? 0 : NA); ++j) {
-    const int r = 8 * (NA * wid + j) + (lane >> 3);
-    const int kofs = 16 * (slot ^ ((r >> 1) & 7));  // bytes
-    const int m = m_base + r;
-    int n = 0, oy = 0, ox = 0;
-    if (m < a.M) row_to_pix(a, m, n, oy, ox);
-    const int iy0 = m < a.M ? oy * a.stride - a.pad : -(1 << 28);
-    const int ix0 = ox * a.stride - a.pad;
-    voff_a[j] = m < a.M ? (n * a.ih * a.iw + iy0 * a.iw + ix0) * a.in_cs * ES + kofs : 0;
-    uint32_t msk = 0;
-    for (int t = 0; t < a.ks * a.ks; ++t) {
-      const int kh = a.ks == 3 ? (t * 11) >> 5 : 0, kw = t - kh * a.ks;
-      const int iy = iy0 + kh, ix = ix0 + kw;
-      if ((unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw) msk |= 1u << t;
+    for (int j = 0; j < (WIN ? 0 : NA); ++j) {
+      const int r = 8 * (NA * wid + j) + (lane >> 3);
+      const int kofs = 16 * (slot ^ ((r >> 1) & 7));  // bytes
+      const int m = G.m_base + r;
+      int n = 0, oy = 0, ox = 0;
+      if (m < a.M) row_to_pix(a, m, n, oy, ox);
+      const int iy0 = m < a.M ? oy * a.stride - a.pad : -(1 << 28);
+      const int ix0 = ox * a.stride - a.pad;
+      G.voff_a[j] = m < a.M ? (n * a.ih * a.iw + iy0 * a.iw + ix0) * a.in_cs * ES + kofs : 0;
+      uint32_t msk = 0;
+      for (int t = 0; t < a.ks * a.ks; ++t) {
+        const int kh = a.ks == 3 ? (t * 11) >> 5 : 0, kw = t - kh * a.ks;
+        const int iy = iy0 + kh, ix = ix0 + kw;
+        if ((unsigned)iy < (unsigned)a.ih && (unsigned)ix < (unsigned)a.iw) msk |= 1u << t;
+      }
+      G.vmask[j] = msk;
     }
-    vmask[j] = msk;
-  }
+    if constexpr (WIN) {
+      G.wp0 = G.m_base - a.iw - 1 + wrow0;
+      G.wv0 = G.wp0 * a.in_cs * ES + 16 * (slot ^ ((wrow0 >> 1) & 7));  // + 64j rows keeps the swizzle
+    } else {
+      G.wp0 = G.wv0 = 0;
+    }
+    return G;
+  };
+  const Geo G0 = make_geo(bid);
   int voff_b[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
@@ -314,8 +406,8 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   const char* in = (const char*)a.in + (size_t)a.in_co * ES;
   const int64_t in_bytes = ((int64_t)a.n * a.ih * a.iw * a.in_cs - a.in_co) * ES;
   const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((const char*)(I8 ? a.w8 : a.w) + (size_t)n_base * a.kpad * ES), 0, BN * a.kpad * ES, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)(I8 ? a.w8 : a.w), 0,
+                                                                        a.cout_pad * a.kpad * ES, 0x00020000);
   const int nk = a.kpad / BKE;
   const int cpt = a.cin / BKE;  // K-blocks per tap
   const int ntap = a.ks * a.ks;
@@ -338,50 +430,59 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // (branch-free: a divergent branch here would split the loop body, and the MFMA /
   // DS-read / VMEM interleave groups do not cross basic blocks)
   // per-lane row of slice 0 (this wave's 8 rows, lane / 8) and its source offset
-  const int wrow0 = 8 * wid + (lane >> 3);
-  const int wp0 = m_base - a.iw - 1 + wrow0;
-  const int wv0 = wp0 * a.in_cs * ES + 16 * (slot ^ ((wrow0 >> 1) & 7));  // + 64j rows keeps the swizzle
-  auto win_op = [&](int j, int cw, bool live) {
+  auto win_op = [&](const Geo& G, int j, int cw, bool live) {
     const int r0 = 64 * j + 8 * wid;  // this wave's 8 rows
     const bool real = live & (r0 < kWinRows);
     _Float16* dst = real ? smem + ((cw & 1) * kWinRows + r0) * BK : zarea;
-    const int p = wp0 + 64 * j;
-    const int vraw = wv0 + (64 * j * a.in_cs + cw * BKE) * ES;
+    const int p = G.wp0 + 64 * j;
+    const int vraw = G.wv0 + (64 * j * a.in_cs + cw * BKE) * ES;
     const bool ok = real & (wrow0 < wr - 64 * j) & ((unsigned)p < (unsigned)npix);
     const int vo = vraw | (int)((uint32_t)!ok << 31);  // >= 2^31: out of range, loads 0
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)dst, 16, vo, 0, 0, 0);
   };
 
-  // Issue the VM buffer->LDS ops of the next K-block (cursor st_*) into stage st_buf.
-  auto stage = [&]() {
-    _Float16* As = smem + st_buf * kPStage;
-    _Float16* Bs = WIN ? Bring + st_buf * kPStage : As + BM * BK;
-    const int st_tap = __builtin_amdgcn_readfirstlane(corder ? st_i : st_o);
-    const int st_c = __builtin_amdgcn_readfirstlane(corder ? st_o : st_i);
+  // Issue the VM buffer->LDS ops of the next K-block (cursor si / so) of tile G into stage sb.
+  auto stage_g = [&](const Geo& G, int& si, int& so, int& sb) {
+    _Float16* As = smem + sb * kPStage;
+    _Float16* Bs = WIN ? Bring + sb * kPStage : As + BM * BK;
+    const int st_tap = __builtin_amdgcn_readfirstlane(corder ? si : so);
+    const int st_c = __builtin_amdgcn_readfirstlane(corder ? so : si);
     const int kh = a.ks == 3 ? (st_tap * 11) >> 5 : 0, kw = st_tap - kh * a.ks;
     if constexpr (WIN) {
       // K-block s = 9 st_c + st_tap is staged during body s - 2: it carries slice
       // j = st_tap - 2 (taps 2..8 -> slices 0..6) of channel block st_c + 1's window
       const int j = st_tap - 2, cw = st_c + 1;
-      win_op(j < 0 ? 0 : j, cw, j >= 0 && cw < ncb && 64 * j < wr);
+      win_op(G, j < 0 ? 0 : j, cw, j >= 0 && cw < ncb && 64 * j < wr);
     } else {
       const int tapoff = ((kh * a.iw + kw) * a.in_cs + st_c * BKE) * ES;
 #pragma unroll
       for (int j = 0; j < NA; ++j) {
-        const int vo = ((vmask[j] >> st_tap) & 1u) ? voff_a[j] + tapoff : (int)0x80000000;
+        const int vo = ((G.vmask[j] >> st_tap) & 1u) ? G.voff_a[j] + tapoff : (int)0x80000000;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(As + 8 * (NA * wid + j) * BK), 16, vo, 0, 0, 0);
       }
     }
-    const int koff = (st_tap * a.cin + st_c * BKE) * ES;  // weight column of this K-block (tap-major packing)
+    // weight column of this K-block (tap-major packing) in the tile's panel
+    const int koff = G.koff_n + (st_tap * a.cin + st_c * BKE) * ES;
 #pragma unroll
     for (int j = 0; j < NB; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j], koff,
                                                0, 0);
-    if (++st_i == ni) {
-      st_i = 0;
-      ++st_o;
+    if (++si == ni) {
+      si = 0;
+      ++so;
     }
-    st_buf = st_buf == NSt - 1 ? 0 : st_buf + 1;
+    sb = sb == NSt - 1 ? 0 : sb + 1;
+  };
+  auto stage = [&]() { stage_g(G0, st_i, st_o, st_buf); };
+  // prologue loads of tile G (window mode: channel block 0's whole window, then K-blocks
+  // 0 .. NSt-2), from a fresh cursor; returns nothing, the caller waits
+  auto prologue_issue = [&](const Geo& G) {
+    int si = 0, so = 0, sb = 0;
+    if constexpr (WIN) {
+      for (int j = 0; 64 * j < wr; ++j) win_op(G, j, 0, true);
+    }
+#pragma unroll
+    for (int i = 0; i < NSt - 1; ++i) stage_g(G, si, so, sb);
   };
 
   const int fr = lane & 15, g = lane >> 4;
@@ -482,15 +583,31 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 
   // prologue: (window mode: channel block 0's whole window,) K-blocks 0 and 1 in flight,
   // wait for 0
-  if constexpr (WIN) {
-    for (int j = 0; 64 * j < wr; ++j) win_op(j, 0, true);
-    win_addr();
-  }
-  if (nk >= NSt - 1) {
+  // (cross-tile prefetch: the previous tile of this workgroup issued them before its
+  // epilogue, whose exactly EPI vector-memory ops are younger than K-block NSt-2)
+  if constexpr (WIN) win_addr();
+  // the tile cursor past the prologue's NSt-1 K-blocks (issued here or by the previous tile)
+  auto skip_prologue = [&]() {
 #pragma unroll
-    for (int i = 0; i < NSt - 1; ++i) stage();
+    for (int i = 0; i < NSt - 1; ++i) {
+      if (++st_i == ni) {
+        st_i = 0;
+        ++st_o;
+      }
+      st_buf = st_buf == NSt - 1 ? 0 : st_buf + 1;
+    }
+  };
+  if (PF && pre) {
+    skip_prologue();
+    wait_vmn_lgkm0<WAITN + pipe_epi_ops<RES_, FM, FN>()>();
+  } else if (nk >= NSt - 1) {
+    prologue_issue(G0);
+    skip_prologue();
     wait_vm_lgkm0<WAITN>();
   } else {
+    if constexpr (WIN) {
+      for (int j = 0; 64 * j < wr; ++j) win_op(G0, j, 0, true);
+    }
     for (int i = 0; i < nk; ++i) stage();
     wait_vm_lgkm0<0>();
   }
@@ -569,7 +686,18 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     body(F_{}, F_{});
   }
   if constexpr (REG) {
-    pipe_epi_regs<(ABL & 256) != 0, FM, FN, WM, WN, BM>(a, m_base, n_base, wm, wn, lane, acc, rb, dq4);
+    if (pf) {
+      if (next >= 0) {  // prefetch the next tile's prologue under this tile's epilogue
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave is past its last fragment read
+        __builtin_amdgcn_sched_barrier(0);
+        prologue_issue(make_geo(next));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      pipe_epi_regs<RES_, FM, FN, WM, WN, BM, true>(a, m_base, n_base, wm, wn, lane, acc, rb, dq4);
+    } else {
+      pipe_epi_regs<RES_, FM, FN, WM, WN, BM>(a, m_base, n_base, wm, wn, lane, acc, rb, dq4);
+    }
     return;
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -738,7 +866,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 // next tile's first K-blocks load, instead of every CU storing, then loading, in
 // lockstep rounds.  Between tiles only LDS is fenced (lgkmcnt): the stores stay in flight.
 template <int ABL, int BM, bool I8, bool WIN>
-__device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem_raw, int ntiles) {
+__device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem_raw, int ntiles, bool pf) {
   const int nb = gridDim.x, xcd = blockIdx.x & 7, l = blockIdx.x >> 3;
   const int q = ntiles >> 3, r = ntiles & 7;
   const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
@@ -751,8 +879,11 @@ __device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem
     }
     __syncthreads();
   }
+  bool pre = false;
   for (int t = lo + l; t < hi; t += bx) {
-    pipe_tile<ABL, BM, I8, WIN>(a, smem_raw, t);
+    const int nx = pf && t + bx < hi ? t + bx : -1;
+    pipe_tile<ABL, BM, I8, WIN>(a, smem_raw, t, pf, nx, pre);
+    pre = nx >= 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
@@ -763,26 +894,26 @@ constexpr int pipe_smem() {
 }
 
 template <int ABL, int BM>
-__global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a, int ntiles) {
+__global__ __launch_bounds__(512, 1) void conv_pipe_f16(ConvArgs a, int ntiles, int pf) {
   __shared__ __attribute__((aligned(16))) unsigned char smem_raw[pipe_smem<BM, false>()];
-  pipe_walk<ABL, BM, false, false>(a, smem_raw, ntiles);
+  pipe_walk<ABL, BM, false, false>(a, smem_raw, ntiles, pf != 0);
 }
 // window mode (3x3 / s1 / p1, linear rows): see kWinRows
 template <int ABL, int BM>
-__global__ __launch_bounds__(512, 1) void conv_pipew_f16(ConvArgs a, int ntiles) {
+__global__ __launch_bounds__(512, 1) void conv_pipew_f16(ConvArgs a, int ntiles, int pf) {
   __shared__ __attribute__((aligned(16))) unsigned char smem_raw[pipe_smem<BM, true>()];
-  pipe_walk<ABL, BM, false, true>(a, smem_raw, ntiles);
+  pipe_walk<ABL, BM, false, true>(a, smem_raw, ntiles, pf != 0);
 }
 // int8 twins (same persistent XCD walk)
 template <int ABL, int BM>
-__global__ __launch_bounds__(512, 1) void conv_pipe_i8(ConvArgs a, int ntiles) {
+__global__ __launch_bounds__(512, 1) void conv_pipe_i8(ConvArgs a, int ntiles, int pf) {
   __shared__ __attribute__((aligned(16))) unsigned char smem_raw[pipe_smem<BM, false>()];
-  pipe_walk<ABL, BM, true, false>(a, smem_raw, ntiles);
+  pipe_walk<ABL, BM, true, false>(a, smem_raw, ntiles, pf != 0);
 }
 template <int ABL, int BM>
-__global__ __launch_bounds__(512, 1) void conv_pipew_i8(ConvArgs a, int ntiles) {
+__global__ __launch_bounds__(512, 1) void conv_pipew_i8(ConvArgs a, int ntiles, int pf) {
   __shared__ __attribute__((aligned(16))) unsigned char smem_raw[pipe_smem<BM, true>()];
-  pipe_walk<ABL, BM, true, true>(a, smem_raw, ntiles);
+  pipe_walk<ABL, BM, true, true>(a, smem_raw, ntiles, pf != 0);
 }
 
 bool conv_pipe_ok(const ConvArgs& a) {
@@ -872,11 +1003,29 @@ static bool pipe_win_ok(const ConvArgs& a, int bm) {
          a.ih == a.oh && a.iw == a.ow && bm + 2 * a.iw + 2 <= kWinRows;
 }
 
+// Cross-tile prefetch (register-epilogue layers): a workgroup issues its next tile's
+// prologue loads (window + K-blocks 0 .. NSt-2) right after its K-loop, before the
+// epilogue, whose stores then drain under the next tile's first K-blocks instead of in
+// front of them.  Needs nk >= NSt - 1 and byte offsets of the output / residual views
+// below 2^31 - 16 (the epilogue's fixed-count buffer ops).  rtdm_set_tuning("conv_pipe_pf", 0)
+// turns it off (bit-identical either way).
+static int g_pipe_pf = 1;
+void set_pipe_pf(int v) { g_pipe_pf = v ? 1 : 0; }
+static bool pipe_pf_ok(const ConvArgs& a, int abl, int nk) {
+  if (!g_pipe_pf || !(abl & 512) || nk < kPNS - 1 || !a.e.full.ptr || a.e.pool.ptr || a.e.up.ptr || a.e.scale)
+    return false;
+  const int64_t pix = (int64_t)a.n * a.oh * a.ow;
+  const int64_t lim = (1ll << 31) - 16;
+  if ((pix * a.e.full.cs) * 2 >= lim) return false;
+  if (a.e.res.ptr && (pix * a.e.res.cs) * 2 >= lim) return false;
+  return true;
+}
+
 #define RTDM_PIPE_KERNEL(NAME)                                                                  \
   template <int ABL, int BM>                                                                    \
   struct NAME##_k {                                                                             \
-    static void go(dim3 g, hipStream_t s, const ConvArgs& a, int nt) {                          \
-      hipLaunchKernelGGL((NAME<ABL, BM>), g, dim3(512), 0, s, a, nt);                          \
+    static void go(dim3 g, hipStream_t s, const ConvArgs& a, int nt, int pf) {                  \
+      hipLaunchKernelGGL((NAME<ABL, BM>), g, dim3(512), 0, s, a, nt, pf);                      \
     }                                                                                           \
   };
 RTDM_PIPE_KERNEL(conv_pipe_f16)
@@ -886,26 +1035,27 @@ RTDM_PIPE_KERNEL(conv_pipew_i8)
 #undef RTDM_PIPE_KERNEL
 
 template <template <int, int> class K, int BM>
-static void launch_abl(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int nt) {
+static void launch_abl(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int nt, int pf) {
   switch (abl) {
     case 8:
-      if constexpr (BM >= 128) K<8, BM>::go(g, s, a, nt);
+      if constexpr (BM >= 128) K<8, BM>::go(g, s, a, nt, pf);
       break;
-    case 128: K<128, BM>::go(g, s, a, nt); break;
-    case 384: K<384, BM>::go(g, s, a, nt); break;
-    case 640: K<640, BM>::go(g, s, a, nt); break;
-    case 896: K<896, BM>::go(g, s, a, nt); break;
-    case 1024: K<1024, BM>::go(g, s, a, nt); break;
-    default: K<0, BM>::go(g, s, a, nt); break;
+    case 128: K<128, BM>::go(g, s, a, nt, pf); break;
+    case 384: K<384, BM>::go(g, s, a, nt, pf); break;
+    case 640: K<640, BM>::go(g, s, a, nt, pf); break;
+    case 896: K<896, BM>::go(g, s, a, nt, pf); break;
+    case 1024: K<1024, BM>::go(g, s, a, nt, pf); break;
+    default: K<0, BM>::go(g, s, a, nt, pf); break;
   }
 }
 
 template <int BM>
 static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid, bool win) {
+  const int abl = pipe_abl(a), pf = pipe_pf_ok(a, abl, a.kpad / kPBK) ? 1 : 0;
   if constexpr (BM >= 128) {
-    if (win) return launch_abl<conv_pipew_f16_k, BM>(pipe_abl(a), grid, s, a, ntiles);
+    if (win) return launch_abl<conv_pipew_f16_k, BM>(abl, grid, s, a, ntiles, pf);
   }
-  launch_abl<conv_pipe_f16_k, BM>(pipe_abl(a), grid, s, a, ntiles);
+  launch_abl<conv_pipe_f16_k, BM>(abl, grid, s, a, ntiles, pf);
 }
 
 static const char* pipe_name(bool i8, bool win, int abl, int bm) {
@@ -950,16 +1100,16 @@ void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
   const int cap = conv_pipe_mode() == 13 ? ntiles : pipe_cus();
   const dim3 grid((unsigned)(ntiles < cap ? ntiles : cap));
   switch (a.head_w ? 1 : conv_pipe_mode()) {
-    case 2: hipLaunchKernelGGL((conv_pipe_f16<1, 256>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 3: hipLaunchKernelGGL((conv_pipe_f16<2, 256>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 4: hipLaunchKernelGGL((conv_pipe_f16<3, 256>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 5: hipLaunchKernelGGL((conv_pipe_f16<4, 256>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 6: hipLaunchKernelGGL((conv_pipe_f16<16, 256>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 7: hipLaunchKernelGGL((conv_pipe_f16<19, 256>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 8: hipLaunchKernelGGL((conv_pipe_f16<32, 256>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 9: hipLaunchKernelGGL((conv_pipe_f16<48, 256>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 10: hipLaunchKernelGGL((conv_pipe_f16<96, 256>), grid, dim3(512), 0, s, a, ntiles); break;
-    case 11: hipLaunchKernelGGL((conv_pipe_f16<0, 256>), grid, dim3(512), 0, s, a, ntiles); break;
+    case 2: hipLaunchKernelGGL((conv_pipe_f16<1, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 3: hipLaunchKernelGGL((conv_pipe_f16<2, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 4: hipLaunchKernelGGL((conv_pipe_f16<3, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 5: hipLaunchKernelGGL((conv_pipe_f16<4, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 6: hipLaunchKernelGGL((conv_pipe_f16<16, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 7: hipLaunchKernelGGL((conv_pipe_f16<19, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 8: hipLaunchKernelGGL((conv_pipe_f16<32, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 9: hipLaunchKernelGGL((conv_pipe_f16<48, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 10: hipLaunchKernelGGL((conv_pipe_f16<96, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 11: hipLaunchKernelGGL((conv_pipe_f16<0, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
     default: {
       const bool win = pipe_win_ok(a, bm);
       if (bm == 256)
@@ -1003,19 +1153,19 @@ void launch_conv_pipe_i8(const ConvArgs& a_in, hipStream_t s) {
   const int ntiles = (int)nt;
   const dim3 grid((unsigned)(ntiles < pipe_cus() ? ntiles : pipe_cus()));
   const bool win = pipe_win_ok(a, bm);
-  const int abl = pipe_abl(a);
+  const int abl = pipe_abl(a), pf = pipe_pf_ok(a, abl, a.kpad / 128) ? 1 : 0;
   if (bm == 256) {
     if (win)
-      launch_abl<conv_pipew_i8_k, 256>(abl, grid, s, a, ntiles);
+      launch_abl<conv_pipew_i8_k, 256>(abl, grid, s, a, ntiles, pf);
     else
-      launch_abl<conv_pipe_i8_k, 256>(abl, grid, s, a, ntiles);
+      launch_abl<conv_pipe_i8_k, 256>(abl, grid, s, a, ntiles, pf);
   } else if (bm == 128) {
     if (win)
-      launch_abl<conv_pipew_i8_k, 128>(abl, grid, s, a, ntiles);
+      launch_abl<conv_pipew_i8_k, 128>(abl, grid, s, a, ntiles, pf);
     else
-      launch_abl<conv_pipe_i8_k, 128>(abl, grid, s, a, ntiles);
+      launch_abl<conv_pipe_i8_k, 128>(abl, grid, s, a, ntiles, pf);
   } else {
-    launch_abl<conv_pipe_i8_k, 64>(abl, grid, s, a, ntiles);
+    launch_abl<conv_pipe_i8_k, 64>(abl, grid, s, a, ntiles, pf);
   }
   RTDM_HIP(hipGetLastError());
 }

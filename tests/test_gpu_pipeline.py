@@ -279,6 +279,32 @@ def test_window_mode_bit_identical(dev, case):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608:16", "yolov3-aider-416@416:12"])
+@pytest.mark.parametrize("bm", [0, 256, 64])
+def test_cross_tile_prefetch_bit_identical(dev, case, bm):
+    """conv_pipe cross-tile prefetch (rtdm_set_tuning("conv_pipe_pf")): a workgroup issues
+    its next tile's prologue loads before its register epilogue, whose stores / residual
+    loads are fixed-count buffer ops.  Batches large enough that workgroups walk several
+    tiles (the prefetch path runs), with the Darknet-53 fused shortcut add (yolov3): same
+    io bits on and off."""
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    cfg, rest = case.split("@")
+    size, b = (int(v) for v in rest.split(":"))
+    x = torch.from_numpy(synth_frames(b, size, size, seed=31)).to(dev)
+    outs = {}
+    try:
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", bm))
+        for v in (0, 1):
+            L.check(L.lib().rtdm_set_tuning(b"conv_pipe_pf", v))
+            m, _, _, _ = _detector(cfg, size)
+            outs[v] = m(x)[0].cpu()
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_pf", 1))
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416", "yolov3-spp-aider@608"])
 def test_head1x1_bit_identical(dev, case):
     """Stand-alone YOLO head convs on head1x1_f16 (register-resident, no LDS) against
