@@ -76,12 +76,11 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
 
 // Fused-head epilogue for the 4 rows m0..m0+3 of head channel c (YOLOLayer
 // inference branch, models.py:252-258): bias -> activation -> decode -> io.
-__device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v) {
+// bias / anc: the channel's head bias and (w / h channels) anchor, loaded by the caller.
+__device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v, float bias, float anc) {
   const Epilogue& e = a.head_e;
   if (m0 >= a.M) return;
-  const float bias = e.bias[c];
   const int ai = c / e.no, k = c - ai * e.no;
-  const float anc = k == 2 || k == 3 ? e.anchor_vec[2 * ai + (k - 2)] : 0.f;
   int n0, oy0, ox0;
   row_to_pix(a, m0, n0, oy0, ox0);
   const size_t plane = (size_t)a.oh * a.ow;
@@ -297,7 +296,8 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   constexpr bool REG = (ABL & 512) != 0;
   constexpr bool RES_ = (ABL & 256) != 0;
   // cross-tile prefetch (pf, register epilogue only: the LDS ring is free during it)
-  constexpr bool PF = REG;
+  constexpr bool HEAD = (ABL & 8) != 0;
+  constexpr bool PF = REG || HEAD;
   // Epilogue channel constants, loaded at the tile's start so their latency hides under
   // the K-loop.  Register epilogue: the 4 channels (4g..4g+3 of each 16-column block)
   // of this lane's accumulators.  Fused head: the FN columns of this lane's accumulators.
@@ -599,7 +599,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   };
   if (PF && pre) {
     skip_prologue();
-    wait_vmn_lgkm0<WAITN + pipe_epi_ops<RES_, FM, FN>()>();
+    // (fused head: its io stores are per-lane conditional, so younger than K-block NSt-2
+    // only a lower bound of them: none — the wait also covers them)
+    wait_vmn_lgkm0<WAITN + (HEAD ? 0 : pipe_epi_ops<RES_, FM, FN>())>();
   } else if (nk >= NSt - 1) {
     prologue_issue(G0);
     skip_prologue();
@@ -722,6 +724,23 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     //      order as the unfused head conv.
     _Float16* Hs = smem;
     const Epilogue& e = a.e;
+    // head weight fragments and decode constants first: their loads are older than the
+    // next tile's prefetch, and their latency hides under the activated-tile writes
+    const _Float16* hw = (const _Float16*)a.head_w;  // [32][128]
+    h8 hbf[BN / 32][2];
+#pragma unroll
+    for (int ks = 0; ks < BN / 32; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) hbf[ks][t] = *(const h8*)(hw + (16 * t + fr) * BN + 32 * ks + 8 * g);
+    float hbias[2], hanc[2];
+#pragma unroll
+    for (int tq = 0; tq < 2; ++tq) {
+      const int c = 16 * tq + fr;
+      const bool cv = c < a.head_cout;
+      const int ai = c / a.head_e.no, k = c - ai * a.head_e.no;
+      hbias[tq] = cv ? a.head_e.bias[c] : 0.f;
+      hanc[tq] = cv && (k == 2 || k == 3) ? a.head_e.anchor_vec[2 * ai + (k - 2)] : 0.f;
+    }
 #pragma unroll
     for (int tn = 0; tn < FN; ++tn) {
       const int col = wn * (BN / WN) + tn * 16 + fr;
@@ -750,29 +769,34 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     for (int i = 0; i < HT; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) hacc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    const _Float16* hw = (const _Float16*)a.head_w;  // [32][128]
 #pragma unroll
     for (int ks = 0; ks < BN / 32; ++ks) {
-      h8 af[HT], bf[2];
+      h8 af[HT];
 #pragma unroll
       for (int t = 0; t < HT; ++t) {
         const int row = HR * wid + 16 * t + fr;
         af[t] = *(const h8*)(Hs + row * BN + 8 * ((4 * ks + g) ^ (row & 15)));
       }
 #pragma unroll
-      for (int t = 0; t < 2; ++t) bf[t] = *(const h8*)(hw + (16 * t + fr) * BN + 32 * ks + 8 * g);
-#pragma unroll
       for (int tm = 0; tm < HT; ++tm)
 #pragma unroll
         for (int tq = 0; tq < 2; ++tq)
-          hacc[tm][tq] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[tm], bf[tq], hacc[tm][tq], 0, 0, 0);
+          hacc[tm][tq] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[tm], hbf[ks][tq], hacc[tm][tq], 0, 0, 0);
+    }
+    if (pf && next >= 0) {  // the activated tile is consumed: prefetch under the decode / io stores
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      prologue_issue(make_geo(next));
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int tm = 0; tm < HT; ++tm)
 #pragma unroll
       for (int tq = 0; tq < 2; ++tq) {
         const int c = 16 * tq + fr;
-        if (c < a.head_cout) head_epi4(a, m_base + HR * wid + 16 * tm + 4 * g, c, hacc[tm][tq]);
+        if (c < a.head_cout)
+          head_epi4(a, m_base + HR * wid + 16 * tm + 4 * g, c, hacc[tm][tq], hbias[tq], hanc[tq]);
       }
     return;
   }
@@ -1012,8 +1036,9 @@ static bool pipe_win_ok(const ConvArgs& a, int bm) {
 static int g_pipe_pf = 1;
 void set_pipe_pf(int v) { g_pipe_pf = v ? 1 : 0; }
 static bool pipe_pf_ok(const ConvArgs& a, int abl, int nk) {
-  if (!g_pipe_pf || !(abl & 512) || nk < kPNS - 1 || !a.e.full.ptr || a.e.pool.ptr || a.e.up.ptr || a.e.scale)
-    return false;
+  if (!g_pipe_pf || nk < kPNS - 1) return false;
+  if (abl == 8) return true;  // fused head: prefetch after the head GEMM, before the decode
+  if (!(abl & 512) || !a.e.full.ptr || a.e.pool.ptr || a.e.up.ptr || a.e.scale) return false;
   const int64_t pix = (int64_t)a.n * a.oh * a.ow;
   const int64_t lim = (1ll << 31) - 16;
   if ((pix * a.e.full.cs) * 2 >= lim) return false;
