@@ -281,9 +281,10 @@ def main():
     first, b = shard_range(global_batch, world, rank)
     if args.inflight <= 0:
         # measured on MI355X (profiles/r02k_*): b8 1 / 2 / 3 / 4 in flight 18.5k / 21.6k / 24.2k / 21.2k
-        # frames/s; b64 1 / 2 / 3: 37.3k / 41.4k / 40.6k.  GPU_MAX_HW_QUEUES is 4: one hardware
-        # queue per in-flight batch, plus RCCL's
-        args.inflight = 3 if b <= 16 else 2
+        # frames/s; b64 1 / 2 / 3: 37.3k / 41.4k / 40.6k; r02cg (200 steps): b16 2 / 3 / 4 32.7k /
+        # 35.3k / 31.8k, b32 2 / 3 38.9k / 39.3k.  GPU_MAX_HW_QUEUES is 4: one hardware queue per
+        # in-flight batch, plus RCCL's
+        args.inflight = 3 if b <= 32 else 2
     pipes, text, stream, sd = build(args, world, rank)
     pipe, det = pipes[0], pipes[0].detector
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in pipes[1:]]
