@@ -348,8 +348,11 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
     for (int i = tid; i < G::NPIX * padw; i += 256) At[(i / padw) * AS + 3 * CC + i % padw] = (_Float16)0.f;
   }
   const _Float16* __restrict__ in = a.in + a.in_co;
-  // work item j of this block: tile blockIdx.x + (j / nch) * gridDim.x, channel chunk j % nch
-  auto item_tile = [&](int j) { return (int)blockIdx.x + (j / nch) * (int)gridDim.x; };
+  // work item j of this block: tile t0 + (j / nch) * tstep (XCD-contiguous walk: neighbouring
+  // tiles' halos share the XCD's L2), channel chunk j % nch
+  int t0, tend, tstep;
+  xcd_span(blockIdx.x, gridDim.x, ntiles, t0, tend, tstep);
+  auto item_tile = [&](int j) { return t0 + (j / nch) * tstep; };
   auto prefetch = [&](u32x4(&pre)[PV], int j) {
     const int tile = item_tile(j), ch = j % nch;
     const int tx = tile % tiles_x, t1 = tile / tiles_x;
@@ -581,7 +584,7 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
 
   // two register prefetch sets: item j+2's halo is in flight while item j computes
   u32x4 preA[PV], preB[PV];
-  auto valid = [&](int j) { return item_tile(j) < ntiles; };
+  auto valid = [&](int j) { return item_tile(j) < tend; };
   if (valid(0)) prefetch(preA, 0);
   if (valid(1)) prefetch(preB, 1);
   for (int j = 0; valid(j); ++j) {

@@ -150,6 +150,30 @@ __device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
   return (int)((t + (((uint32_t)n - t) >> 1)) >> (f.l - 1));
 }
 
+// XCD-contiguous work order.  The dispatcher deals blockIdx round-robin over the 8 XCDs
+// (XCD = blockIdx % 8); these maps give each XCD one contiguous run of the logical order,
+// so neighbouring tiles / row bands (whose halos overlap) share that XCD's L2 instead of
+// each XCD fetching the shared rows from HBM.
+// One logical block per launched block (a bijection of [0, nb)):
+__device__ __forceinline__ int xcd_block(int bid, int nb) {
+  const int x = bid & 7, q = nb >> 3, r = nb & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+// Persistent blocks over ntiles tiles: block bid walks first, first + step, ... < end.
+// Every XCD that owns tiles has a block when nb >= 8 or ntiles <= nb; otherwise the plain
+// grid-stride order.
+__device__ __forceinline__ void xcd_span(int bid, int nb, int ntiles, int& first, int& end, int& step) {
+  if (nb < 8 && ntiles > nb) {
+    first = bid, end = ntiles, step = nb;
+    return;
+  }
+  const int x = bid & 7, q = ntiles >> 3, r = ntiles & 7;
+  const int lo = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  first = lo + (bid >> 3);
+  end = lo + q + (x < r ? 1 : 0);
+  step = (nb - x + 7) >> 3;
+}
+
 struct ConvArgs {
   const void* in = nullptr;
   int in_cs = 0, in_co = 0, in_kind = IN_NHWC;

@@ -250,8 +250,9 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
   const int s = a.stride, pad = a.pad;
   constexpr int ROWS = stem_rows(POOL);
   const int bpi = (a.oh + ROWS - 1) / ROWS;
-  const int n = blockIdx.x / bpi;
-  const int oy0 = (blockIdx.x - n * bpi) * ROWS;
+  const int bl = xcd_block(blockIdx.x, gridDim.x);  // consecutive bands (shared halo rows) on one XCD
+  const int n = bl / bpi;
+  const int oy0 = (bl - n * bpi) * ROWS;
   const int nrows = (ROWS - 1) * s + 3;
   const int cols = (a.ow - 1) * s - pad + 5;  // LDS column = x + 1, x in [-1, (ow-1)*s - pad + 3]
   const int ls = cols + stem_xcols(POOL, s);   // LDS row stride (overrun columns: never staged)
@@ -1120,9 +1121,10 @@ __global__ __launch_bounds__(256) void conv3_pool_small(ConvArgs a) {
   // LeakyReLU as max(x, slope x) (0 < slope < 1; slope 1 = linear): same values, no branch
   const float slope = e.act == ACT_LEAKY ? e.slope : 1.f;
   int buf = 0;
-  int tile = blockIdx.x;
-  if (tile < ntiles) prefetch(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
+  int tile, tend, tstep;  // XCD-contiguous tile walk (horizontal neighbours share the halo columns)
+  xcd_span(blockIdx.x, gridDim.x, ntiles, tile, tend, tstep);
+  if (tile < tend) prefetch(tile);
+  for (; tile < tend; tile += tstep) {
     _Float16* xb_w = xs + buf * XS;
 #pragma unroll
     for (int k = 0; k < PV; ++k)
@@ -1130,7 +1132,7 @@ __global__ __launch_bounds__(256) void conv3_pool_small(ConvArgs a) {
     __syncthreads();
     const int tx = tile % tiles_x, t1 = tile / tiles_x;
     const int ty = t1 % tiles_y, n = t1 / tiles_y;
-    if (tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);  // in flight during the MFMAs
+    if (tile + tstep < tend) prefetch(tile + tstep);  // in flight during the MFMAs
     const _Float16* xb = xb_w + (wr * WROWS * HW + p) * PS;
     f4 acc[WROWS][WCH];
 #pragma unroll

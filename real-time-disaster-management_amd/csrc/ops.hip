@@ -1071,8 +1071,9 @@ __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __res
   uint32_t* himg = (uint32_t*)(rsx_lds + kRsRing * kRsRowB);  // [band_rows + kRsTaps][256] packed (r,g,b)
   int* kv = (int*)(himg + (band_rows + kRsTaps) * 256);    // [kRsBand][kRsTaps]
   const int bands = (out + kRsBand - 1) / kRsBand;
-  const int b = blockIdx.x / bands;
-  const int yy0 = (blockIdx.x - b * bands) * kRsBand;
+  const int bl = xcd_block(blockIdx.x, gridDim.x);  // consecutive bands (shared tap rows) on one XCD
+  const int b = bl / bands;
+  const int yy0 = (bl - b * bands) * kRsBand;
   const int nyy = out - yy0 < kRsBand ? out - yy0 : kRsBand;
   const int r0 = bv[2 * yy0];
   const int r1 = bv[2 * (yy0 + nyy - 1)] + bv[2 * (yy0 + nyy - 1) + 1];
