@@ -46,9 +46,12 @@ struct PipeCfg {
 // Window mode (3x3 / stride 1 / pad 1, linear row order): per 64-channel block the tile's
 // input rows m_base - W - 1 .. m_base + BM + W (BM + 2W + 2 pixels, at most kWinRows) sit
 // in LDS once; the 9 taps read shifted views of it.  Layout: two window buffers (channel
-// blocks alternate), the 3-stage B ring, a 1 KB zero area (out-of-image taps read it).
+// blocks alternate), the 3-stage B ring, a 2 KB zero area of 16 swizzled rows (an
+// out-of-image tap reads zero row (i & 15), slot g ^ (i & 7) for the window row i it
+// replaces: the same 4-bank group as the real read, so border pixels add no bank conflicts;
+// a single shared zero slot cost 2-way conflicts on every border fragment read).
 constexpr int kWinRows = 440;
-constexpr int kWinSmem = (2 * kWinRows * kPBK + kPNS * kPBN * kPBK + 8 * kPBK) * 2;
+constexpr int kWinSmem = (2 * kWinRows * kPBK + kPNS * kPBN * kPBK + 16 * kPBK) * 2;
 static_assert(kWinSmem <= 163840, "window LDS");
 
 // s_waitcnt vmcnt(N) lgkmcnt(0), any N < 64 (gfx9 encoding: vmcnt bits 3:0 and 15:14)
@@ -354,7 +357,13 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 
   // ---- per-lane staging state.  A op j of wave w fills tile rows 8(NA w + j) + lane/8,
   //      B op j rows 8(NB w + j) + lane/8; LDS slot lane%8 of a row holds k-vector
-  //      slot ^ ((row >> 1) & 7) (the read side applies the same involution).
+  //      slot ^ (row & 7) (the read side applies the same involution).  ds_read_b128 serves
+  //      a wave in 4 lane groups of 16, each mixing 8 lanes of one 16-lane row block (rows
+  //      R..R+15 by fr, one k-slot group g) with 8 of the next (g ^ 1): with slot = g ^ (row & 7)
+  //      the 16 reads hit 16 distinct 4-bank groups (8·(row & 1) + slot) for ANY row offset R,
+  //      so the window mode's tap-shifted rows read conflict-free too (the former
+  //      (row >> 1) & 7 swizzle was conflict-free only for even R: 31 % of the window
+  //      kernel's LDS cycles were bank conflicts, profiles/r02ci_pmc_table.txt).
   //      Per-tile part (PipeGeo): A row offsets / tap masks, the window origin, the weight
   //      panel; built for this tile and, for the cross-tile prefetch, for the next one. ----
   const int slot = lane & 7;
@@ -373,7 +382,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 #pragma unroll
     for (int j = 0; j < (WIN ? 0 : NA); ++j) {
       const int r = 8 * (NA * wid + j) + (lane >> 3);
-      const int kofs = 16 * (slot ^ ((r >> 1) & 7));  // bytes
+      const int kofs = 16 * (slot ^ (r & 7));  // bytes
       const int m = G.m_base + r;
       int n = 0, oy = 0, ox = 0;
       if (m < a.M) row_to_pix(a, m, n, oy, ox);
@@ -390,7 +399,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     }
     if constexpr (WIN) {
       G.wp0 = G.m_base - a.iw - 1 + wrow0;
-      G.wv0 = G.wp0 * a.in_cs * ES + 16 * (slot ^ ((wrow0 >> 1) & 7));  // + 64j rows keeps the swizzle
+      G.wv0 = G.wp0 * a.in_cs * ES + 16 * (slot ^ (wrow0 & 7));  // + 64j rows keeps the swizzle
     } else {
       G.wp0 = G.wv0 = 0;
     }
@@ -401,7 +410,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int r = 8 * (NB * wid + j) + (lane >> 3);
-    voff_b[j] = r * a.kpad * ES + 16 * (slot ^ ((r >> 1) & 7));
+    voff_b[j] = r * a.kpad * ES + 16 * (slot ^ (r & 7));
   }
   const char* in = (const char*)a.in + (size_t)a.in_co * ES;
   const int64_t in_bytes = ((int64_t)a.n * a.ih * a.iw * a.in_cs - a.in_co) * ES;
@@ -486,7 +495,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   };
 
   const int fr = lane & 15, g = lane >> 4;
-  const int rsw = (fr >> 1) & 7;
+  const int rsw = fr & 7;  // fragment rows start at multiples of 16
   const int so0 = 8 * ((0 + g) ^ rsw), so1 = 8 * ((4 + g) ^ rsw);
   const int a_row = (wm * (BM / WM) + fr) * BK, b_row = ((WIN ? 0 : BM) + wn * (BN / WN) + fr) * BK;
 
@@ -513,13 +522,15 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     }
   }
   // byte offsets; the 16-row fragment blocks tm share the swizzle of block 0 (rows + 16 tm)
-  const int zoff = (2 * kWinRows * BK + kPNS * BN * BK + 8 * g) * 2;
+  const int zbase = (2 * kWinRows * BK + kPNS * BN * BK) * 2;
   const int wrd0 = wm * (BM / WM) + fr;
   auto win_addr = [&]() {  // aoff for K-block (rd_o, rd_i), then advance the read cursor
     const int t = __builtin_amdgcn_readfirstlane(rd_i);
     const int kh = (t * 11) >> 5, kw = t - 3 * kh;
     const int i = wrd0 + kh * a.iw + kw;
-    const int off = ((rd_o & 1) * kWinRows + i) * BK * 2 + 16 * (g ^ ((i >> 1) & 7));
+    const int sw = 16 * (g ^ (i & 7));
+    const int off = ((rd_o & 1) * kWinRows + i) * BK * 2 + sw;
+    const int zoff = zbase + (i & 15) * BK * 2 + sw;  // rows i + 16 tm: the same zero row
 #pragma unroll
     for (int tm = 0; tm < FM; ++tm) aoff[tm] = ((amask[tm] >> t) & 1u) ? off + tm * 16 * BK * 2 : zoff;
     if (++rd_i == 9) {
@@ -897,7 +908,7 @@ __device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem
   const int hi = lo + q + (xcd < r ? 1 : 0);
   const int bx = (nb - xcd + 7) >> 3;  // workgroups on this XCD (>= 1: this one)
   if constexpr (WIN) {  // the zero area: written once, outside every epilogue's LDS use
-    if (threadIdx.x < 64) {
+    if (threadIdx.x < 128) {
       u32x4* z = reinterpret_cast<u32x4*>(smem_raw + (2 * kWinRows * kPBK + kPNS * kPBN * kPBK) * 2);
       z[threadIdx.x] = u32x4{0u, 0u, 0u, 0u};
     }

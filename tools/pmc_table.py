@@ -5,7 +5,8 @@ python tools/pmc_table.py TAG [npasses]
 Columns: us = dispatch time; GHz = GRBM_GUI_ACTIVE / 8 XCDs / wall (effective clock);
 mfma% = SQ_VALU_MFMA_BUSY_CYCLES over all SIMD-cycles (GRBM_GUI_ACTIVE x 128);
 wait/inst/act = SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY shares of SQ_WAVE_CYCLES;
-ldsconf = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; l2hit = TCC_HIT / (TCC_HIT + TCC_MISS)."""
+ldsconf = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; lds% = SQ_LDS_IDX_ACTIVE over all CU-cycles
+(GRBM_GUI_ACTIVE x 256 CUs / 8 XCDs: the LDS-array busy share); l2hit = TCC_HIT / (TCC_HIT + TCC_MISS)."""
 import sqlite3
 import sys
 
@@ -35,7 +36,7 @@ def g(m, k, default=0.0):
 
 
 print(f"{'kernel':34s} {'us':>7s} {'GHz':>5s} {'waves':>6s} {'mfma/w':>7s} {'mfma%':>6s} {'wait':>5s} {'inst':>5s} "
-      f"{'act':>5s} {'ldsI/w':>6s} {'ldsconf':>7s} {'vmrd/w':>6s} {'valu/w':>7s} {'l2hit':>6s}")
+      f"{'act':>5s} {'ldsI/w':>6s} {'ldsconf':>7s} {'lds%':>5s} {'vmrd/w':>6s} {'valu/w':>7s} {'l2hit':>6s}")
 for m in merged:
     w = max(1.0, g(m, "SQ_WAVES", 1))
     cyc = max(1.0, g(m, "SQ_WAVE_CYCLES", 1))
@@ -48,4 +49,5 @@ for m in merged:
     print(f"{name:34s} {g(m, 'dur') / 1000:7.1f} {ghz:5.2f} {w:6.0f} {g(m, 'SQ_INSTS_MFMA') / w:7.1f} {mf:6.1f} "
           f"{g(m, 'SQ_WAIT_ANY') / cyc:5.2f} {g(m, 'SQ_WAIT_INST_ANY') / cyc:5.2f} {g(m, 'SQ_ACTIVE_INST_ANY') / cyc:5.2f} "
           f"{g(m, 'SQ_INSTS_LDS') / w:6.1f} {g(m, 'SQ_LDS_BANK_CONFLICT') / max(1.0, g(m, 'SQ_LDS_IDX_ACTIVE', 1)):7.3f} "
+          f"{100 * g(m, 'SQ_LDS_IDX_ACTIVE') / max(1.0, gui * 32):5.1f} "
           f"{g(m, 'SQ_INSTS_VMEM_RD') / w:6.1f} {g(m, 'SQ_INSTS_VALU') / w:7.1f} {hit / max(1.0, hit + miss):6.3f}")
