@@ -46,12 +46,11 @@ struct PipeCfg {
 // Window mode (3x3 / stride 1 / pad 1, linear row order): per 64-channel block the tile's
 // input rows m_base - W - 1 .. m_base + BM + W (BM + 2W + 2 pixels, at most kWinRows) sit
 // in LDS once; the 9 taps read shifted views of it.  Layout: two window buffers (channel
-// blocks alternate), the 3-stage B ring, a 2 KB zero area of 16 swizzled rows (an
-// out-of-image tap reads zero row (i & 15), slot g ^ (i & 7) for the window row i it
-// replaces: the same 4-bank group as the real read, so border pixels add no bank conflicts;
-// a single shared zero slot cost 2-way conflicts on every border fragment read).
+// blocks alternate), the 3-stage B ring, a 1 KB zero area (out-of-image taps read it; a
+// per-row swizzled 2 KB zero area removes the border reads' bank conflicts but its
+// per-K-block address VALU cost more: r02ck).
 constexpr int kWinRows = 440;
-constexpr int kWinSmem = (2 * kWinRows * kPBK + kPNS * kPBN * kPBK + 16 * kPBK) * 2;
+constexpr int kWinSmem = (2 * kWinRows * kPBK + kPNS * kPBN * kPBK + 8 * kPBK) * 2;
 static_assert(kWinSmem <= 163840, "window LDS");
 
 // s_waitcnt vmcnt(N) lgkmcnt(0), any N < 64 (gfx9 encoding: vmcnt bits 3:0 and 15:14)
@@ -522,15 +521,13 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     }
   }
   // byte offsets; the 16-row fragment blocks tm share the swizzle of block 0 (rows + 16 tm)
-  const int zbase = (2 * kWinRows * BK + kPNS * BN * BK) * 2;
+  const int zoff = (2 * kWinRows * BK + kPNS * BN * BK + 8 * g) * 2;
   const int wrd0 = wm * (BM / WM) + fr;
   auto win_addr = [&]() {  // aoff for K-block (rd_o, rd_i), then advance the read cursor
     const int t = __builtin_amdgcn_readfirstlane(rd_i);
     const int kh = (t * 11) >> 5, kw = t - 3 * kh;
     const int i = wrd0 + kh * a.iw + kw;
-    const int sw = 16 * (g ^ (i & 7));
-    const int off = ((rd_o & 1) * kWinRows + i) * BK * 2 + sw;
-    const int zoff = zbase + (i & 15) * BK * 2 + sw;  // rows i + 16 tm: the same zero row
+    const int off = ((rd_o & 1) * kWinRows + i) * BK * 2 + 16 * (g ^ (i & 7));
 #pragma unroll
     for (int tm = 0; tm < FM; ++tm) aoff[tm] = ((amask[tm] >> t) & 1u) ? off + tm * 16 * BK * 2 : zoff;
     if (++rd_i == 9) {
@@ -908,7 +905,7 @@ __device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem
   const int hi = lo + q + (xcd < r ? 1 : 0);
   const int bx = (nb - xcd + 7) >> 3;  // workgroups on this XCD (>= 1: this one)
   if constexpr (WIN) {  // the zero area: written once, outside every epilogue's LDS use
-    if (threadIdx.x < 128) {
+    if (threadIdx.x < 64) {
       u32x4* z = reinterpret_cast<u32x4*>(smem_raw + (2 * kWinRows * kPBK + kPNS * kPBN * kPBK) * 2);
       z[threadIdx.x] = u32x4{0u, 0u, 0u, 0u};
     }
