@@ -127,7 +127,12 @@ const char* rtdm_build_arch(void);
  * afterwards); key "acff_persist": 1 = persistent ACFF kernel for the large
  * classifier maps (default), 0 = 8x8-tile fused ACFF kernel (at launch); key
  * "two_streams": 1 = detector head branches on a side stream (default), 0 = one
- * stream (takes effect for handles created afterwards).                         */
+ * stream (takes effect for handles created afterwards).  conv_pipe variants, all
+ * bit-identical to each other (at launch): "conv_pipe_bm" 0 = tile rows by the
+ * cost model (default) | 256 | 128 | 64; "conv_pipe_win" 1 = window mode for
+ * 3x3/s1 layers (default); "conv_pipe_korder" 1 = channel-block-outer K order
+ * (default; 0 changes the fp32 summation order); "conv_pipe_pf" 1 = cross-tile
+ * prologue prefetch (default).                                                   */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 
 /* ---- classifier ------------------------------------------------------------ */
