@@ -56,27 +56,32 @@ void launch_chan_absmax(View v, int n, int h, int w, int c, unsigned* out, hipSt
   RTDM_HIP(hipGetLastError());
 }
 
-// 8 channels per thread: one 16-byte fp16 load, one 8-byte int8 store.
-__global__ __launch_bounds__(256) void quantize_kernel(const _Float16* __restrict__ p, int cs, int co, int64_t npix,
-                                                       int cin, const float* __restrict__ inv_scale,
+// 8 channels per thread: one 16-byte fp16 load, one 8-byte int8 store.  32-bit indices
+// with a multiply-shift division by the channel-group count (the former 64-bit divide per
+// element cost more than the 3 bytes of memory traffic), the 8 inverse scales as two
+// 16-byte loads.
+__global__ __launch_bounds__(256) void quantize_kernel(const _Float16* __restrict__ p, int cs, int co, int npix,
+                                                       int cin, FastDiv fgroups, const float* __restrict__ inv_scale,
                                                        int8_t* __restrict__ q) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
   const int groups = cin / 8;
-  const int64_t total = npix * groups;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t px = i / groups;
-    const int g = (int)(i - px * groups);
-    const h8 x = *(const h8*)(p + px * cs + co + g * 8);
+  const int total = npix * groups;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int px = fdiv(i, fgroups);
+    const int g = i - px * groups;
+    const h8 x = *(const h8*)(p + (size_t)px * cs + co + g * 8);
+    const f4 s0 = *(const f4*)(inv_scale + g * 8), s1 = *(const f4*)(inv_scale + g * 8 + 4);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      int v = (int)rintf((float)x[j] * inv_scale[g * 8 + j]);
+      int v = (int)rintf((float)x[j] * (j < 4 ? s0[j] : s1[j - 4]));
       v = v < -127 ? -127 : (v > 127 ? 127 : v);
       if (j < 4)
         lo |= ((uint32_t)v & 255u) << (8 * j);
       else
         hi |= ((uint32_t)v & 255u) << (8 * (j - 4));
     }
-    *(uint2*)(q + px * cin + g * 8) = make_uint2(lo, hi);
+    *(uint2*)(q + (size_t)px * cin + g * 8) = make_uint2(lo, hi);
   }
 }
 
@@ -85,9 +90,10 @@ void launch_quantize(View v, int n, int h, int w, int c, const float* inv_scale,
   const int64_t npix = (int64_t)n * h * w;
   const int64_t total = npix * (c / 8);
   if (total <= 0) return;
+  RTDM_REQUIRE(total < (1ll << 31), RTDM_E_CAPACITY, "quantize: too many elements");
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(quantize_kernel, dim3(blocks), dim3(256), 0, s, (const _Float16*)v.ptr, v.cs, v.co, npix, c,
-                     inv_scale, q);
+  hipLaunchKernelGGL(quantize_kernel, dim3(blocks), dim3(256), 0, s, (const _Float16*)v.ptr, v.cs, v.co, (int)npix, c,
+                     make_fastdiv(c / 8), inv_scale, q);
   RTDM_HIP(hipGetLastError());
 }
 
