@@ -262,8 +262,15 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
   // ---- stage the input rows iy0 .. iy0+nrows-1 (fp16, 4 channels / pixel) ----
   if (a.in_kind == IN_FRAME_U8 && (W & 3) == 0 && cols >= W + 1) {
     const int gpr = W >> 2;  // 4-pixel groups per row (12 bytes)
-    for (int r = 0; r < nrows; ++r)
-    for (int g = tid; g < gpr; g += 256) {
+    // (row, group) items flattened over all 256 threads (a per-row loop left 256 - gpr
+    // threads idle every row: 104 of 256 at 608 columns)
+    int r = tid / gpr, g = tid - r * gpr;
+    for (; r < nrows; g += 256) {
+      while (g >= gpr) {
+        g -= gpr;
+        ++r;
+      }
+      if (r >= nrows) break;
       const int y = iy0 + r;
       uint32_t d0 = 0, d1 = 0, d2 = 0;
       if ((unsigned)y < (unsigned)H && !(ABL & 1)) {
