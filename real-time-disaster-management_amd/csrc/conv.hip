@@ -263,29 +263,43 @@ __global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
   if (a.in_kind == IN_FRAME_U8 && (W & 3) == 0 && cols >= W + 1) {
     const int gpr = W >> 2;  // 4-pixel groups per row (12 bytes)
     // (row, group) items flattened over all 256 threads (a per-row loop left 256 - gpr
-    // threads idle every row: 104 of 256 at 608 columns)
+    // threads idle every row: 104 of 256 at 608 columns), four items per thread per pass
+    // with all their loads issued before the first conversion (one load latency per pass,
+    // not per item)
     int r = tid / gpr, g = tid - r * gpr;
-    for (; r < nrows; g += 256) {
-      while (g >= gpr) {
-        g -= gpr;
-        ++r;
-      }
-      if (r >= nrows) break;
-      const int y = iy0 + r;
-      uint32_t d0 = 0, d1 = 0, d2 = 0;
-      if ((unsigned)y < (unsigned)H && !(ABL & 1)) {
-        const uint32_t* src = (const uint32_t*)((const uint8_t*)a.in + ((size_t)(n * H + y) * W + 4 * g) * 3);
-        d0 = src[0];
-        d1 = src[1];
-        d2 = src[2];
-      }
-      const uint32_t b[12] = {d0 & 255u, (d0 >> 8) & 255u, (d0 >> 16) & 255u, d0 >> 24,
-                              d1 & 255u, (d1 >> 8) & 255u, (d1 >> 16) & 255u, d1 >> 24,
-                              d2 & 255u, (d2 >> 8) & 255u, (d2 >> 16) & 255u, d2 >> 24};
-      uint2* dst = stem_lds + r * ls + 4 * g + 1;
+    while (r < nrows) {
+      uint32_t d[4][3];
+      int rk[4], gk[4];
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-        dst[p] = make_uint2(pack_h2((float)b[3 * p], (float)b[3 * p + 1]), pack_h2((float)b[3 * p + 2], 0.f));
+      for (int k = 0; k < 4; ++k) {
+        rk[k] = r;
+        gk[k] = g;
+        d[k][0] = d[k][1] = d[k][2] = 0u;
+        const int y = iy0 + r;
+        if (r < nrows && (unsigned)y < (unsigned)H && !(ABL & 1)) {
+          const uint32_t* src = (const uint32_t*)((const uint8_t*)a.in + ((size_t)(n * H + y) * W + 4 * g) * 3);
+          d[k][0] = src[0];
+          d[k][1] = src[1];
+          d[k][2] = src[2];
+        }
+        g += 256;
+        while (g >= gpr) {
+          g -= gpr;
+          ++r;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (rk[k] >= nrows) break;
+        const uint32_t d0 = d[k][0], d1 = d[k][1], d2 = d[k][2];
+        const uint32_t b[12] = {d0 & 255u, (d0 >> 8) & 255u, (d0 >> 16) & 255u, d0 >> 24,
+                                d1 & 255u, (d1 >> 8) & 255u, (d1 >> 16) & 255u, d1 >> 24,
+                                d2 & 255u, (d2 >> 8) & 255u, (d2 >> 16) & 255u, d2 >> 24};
+        uint2* dst = stem_lds + rk[k] * ls + 4 * gk[k] + 1;
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          dst[p] = make_uint2(pack_h2((float)b[3 * p], (float)b[3 * p + 1]), pack_h2((float)b[3 * p + 2], 0.f));
+      }
     }
     const int npad = cols - W;  // LDS column 0 and columns W+1 .. cols-1 are padding
     for (int idx = tid; idx < nrows * npad; idx += 256) {
