@@ -244,7 +244,7 @@ __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
 // ABL (diagnostic builds only, outputs wrong when non-zero): 1 = no frame loads,
 // 2 = no output stores, 4 = no MFMA.
 template <bool POOL, int NTN, int ABL = 0>
-__global__ __launch_bounds__(256) void conv_stem3(ConvArgs a) {
+__global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LDS bound (<= 31 KB per block at 608); lets the compiler keep the fragment reads in flight
   extern __shared__ __attribute__((aligned(16))) uint2 stem_lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int s = a.stride, pad = a.pad;
@@ -1066,7 +1066,7 @@ __global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
 // pixel stride CIN + 8 halfs (16 consecutive pixels hit distinct banks).
 // --------------------------------------------------------------------------
 template <int CIN, int COUT, int TH, int WROWS, int WCH>
-__global__ __launch_bounds__(256) void conv3_pool_small(ConvArgs a) {
+__global__ __launch_bounds__(256, CIN == 16 ? 3 : 2) void conv3_pool_small(ConvArgs a) {  // CIN 16: 3 blocks per CU (<= 168 registers, no spill; CIN 32 would spill)
   constexpr int TW = 16, HW = TW + 2, PS = CIN + 8;
   constexpr int CG = CIN / 8;                // 8-channel groups per tap
   constexpr int NQ = 9 * CG;                 // 8-channel groups in K
