@@ -1066,7 +1066,7 @@ __global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
 // pixel stride CIN + 8 halfs (16 consecutive pixels hit distinct banks).
 // --------------------------------------------------------------------------
 template <int CIN, int COUT, int TH, int WROWS, int WCH>
-__global__ __launch_bounds__(256, CIN == 16 ? 3 : 2) void conv3_pool_small(ConvArgs a) {  // CIN 16: 3 blocks per CU (<= 168 registers, no spill; CIN 32 would spill)
+__global__ __launch_bounds__(256, CIN == 16 || WCH == 1 ? 3 : 2) void conv3_pool_small(ConvArgs a) {  // 3 blocks per CU (<= 168 registers): CIN 16, and CIN 32 with one 16-channel tile per wave (WCH 1: half the weight registers; with WCH 2 it would spill)
   constexpr int TW = 16, HW = TW + 2, PS = CIN + 8;
   constexpr int CG = CIN / 8;                // 8-channel groups per tap
   constexpr int NQ = 9 * CG;                 // 8-channel groups in K
@@ -1239,9 +1239,9 @@ static void launch_pool_small(const ConvArgs& a, hipStream_t s) {
     const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cu_count());
     hipLaunchKernelGGL((conv3_pool_small<16, 32, 16, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   } else {
-    static const int per_cu = resident_blocks(conv3_pool_small<32, 64, 8, 4, 2>, 256, 0);
+    static const int per_cu = resident_blocks(conv3_pool_small<32, 64, 8, 8, 1>, 256, 0);
     const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cu_count());
-    hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 8, 1>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   }
 }
 
@@ -1354,7 +1354,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     return names[a.quad ? 1 : 0][ntn == 1 ? 0 : ntn == 2 ? 1 : 2];
   }
   if (dtype == RTDM_F16 && pool_small_ok(a))
-    return a.cin == 16 ? "conv3_pool_small<16,32,16,4,2>" : "conv3_pool_small<32,64,8,4,2>";
+    return a.cin == 16 ? "conv3_pool_small<16,32,16,4,2>" : "conv3_pool_small<32,64,8,8,1>";
   if (dtype == RTDM_F16 && direct_ok(a)) {
     const int bn = direct_cfg(a.cout_pad).bn;
     return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
