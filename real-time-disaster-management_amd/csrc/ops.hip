@@ -401,21 +401,22 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ in, 
 }
 
 template <typename T, int VEC>
+// 32-bit item index (total < 2^31, checked at launch) split by multiply-shift divisions:
+// the 64-bit div / mod chain per item cost more than the item's memory traffic.
 __global__ __launch_bounds__(256) void maxpool_vec_kernel(const T* __restrict__ in, int in_cs, int in_co, int n,
                                                           int h, int w, int c, int k, int stride, int pad,
                                                           int zero_rb, T* __restrict__ out, int out_cs, int out_co,
-                                                          int oh, int ow) {
+                                                          int oh, int ow, FastDiv fcg, FastDiv fow, FastDiv foh) {
   typedef T tv __attribute__((ext_vector_type(VEC)));
   const int cg = c / VEC;
-  const int64_t total = (int64_t)n * oh * ow * cg;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int g = (int)(idx % cg);
-    int64_t p = idx / cg;
-    const int ox = (int)(p % ow);
-    p /= ow;
-    const int oy = (int)(p % oh);
-    const int b = (int)(p / oh);
+  const int total = n * oh * ow * cg;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    int p = fdiv(idx, fcg);
+    const int g = idx - p * cg;
+    const int q = fdiv(p, fow);
+    const int ox = p - q * ow;
+    const int b = fdiv(q, foh);
+    const int oy = q - b * oh;
     float m[VEC];
 #pragma unroll
     for (int j = 0; j < VEC; ++j) m[j] = -INFINITY;
@@ -447,14 +448,16 @@ void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, 
   const int64_t total = (int64_t)n * oh * ow * c;
   if (total <= 0) return;
   const int vec = dtype == RTDM_F16 ? 8 : 4;
-  if (c % vec == 0 && ((iv.cs | iv.co | ov.cs | ov.co) % vec) == 0) {
+  if (c % vec == 0 && ((iv.cs | iv.co | ov.cs | ov.co) % vec) == 0 && total / vec < (1ll << 31)) {
     const int gv = grid_for(total / vec, 256);
+    const FastDiv fcg = make_fastdiv(c / vec), fow = make_fastdiv(ow), foh = make_fastdiv(oh);
     if (dtype == RTDM_F16)
       hipLaunchKernelGGL((maxpool_vec_kernel<_Float16, 8>), dim3(gv), dim3(256), 0, s, (const _Float16*)iv.ptr, iv.cs,
-                         iv.co, n, h, w, c, k, stride, pad, zero_rb, (_Float16*)ov.ptr, ov.cs, ov.co, oh, ow);
+                         iv.co, n, h, w, c, k, stride, pad, zero_rb, (_Float16*)ov.ptr, ov.cs, ov.co, oh, ow, fcg, fow,
+                         foh);
     else
       hipLaunchKernelGGL((maxpool_vec_kernel<float, 4>), dim3(gv), dim3(256), 0, s, (const float*)iv.ptr, iv.cs, iv.co,
-                         n, h, w, c, k, stride, pad, zero_rb, (float*)ov.ptr, ov.cs, ov.co, oh, ow);
+                         n, h, w, c, k, stride, pad, zero_rb, (float*)ov.ptr, ov.cs, ov.co, oh, ow, fcg, fow, foh);
     RTDM_HIP(hipGetLastError());
     return;
   }
