@@ -63,6 +63,9 @@ def parse():
                     help="> 0: frames per GPU per step instead (weak scaling; global = this * N)")
     ap.add_argument("--img", type=int, default=608)
     ap.add_argument("--cfg", default="yolov4-tiny-aider-416")
+    ap.add_argument("--weights", default="cond", choices=["cond", "he"],
+                    help="synthetic detector weight set (rtdm.synth): cond = the well-conditioned set the "
+                         "SURVEY §8d bars are asserted on; he = the mean-field stress set")
     ap.add_argument("--classifier", default="ernet", choices=["ernet", "squeeze-ernet", "squeeze-redconv", "none"],
                     help="none: detection only (BASELINE config 3)")
     ap.add_argument("--dtype", default="f16", choices=["f16", "f32", "i8"],
@@ -130,8 +133,9 @@ def build(args, world, rank):
     cls = build_model(args.classifier) if use_cls else None
     # rank 0 makes / loads the weights; RCCL broadcast to the other ranks (once, untimed)
     if rank == 0:
-        calib = load_calibration(args.cfg)
-        conv, acff = synth_darknet_weights(text, calib=calib), synth_acff_params(text, calib=calib)
+        calib = load_calibration(args.cfg, args.weights)
+        conv = synth_darknet_weights(text, calib=calib, preset=args.weights)
+        acff = synth_acff_params(text, calib=calib, preset=args.weights)
         stream = inline_acff(text, conv, acff)  # YOLO-ACFF cfgs: [acff] params inline
         args.ref_weights = (conv, acff)         # the CPU oracle takes them apart
         sd = trained_classifier(args.classifier) if use_cls else {}
@@ -147,7 +151,7 @@ def build(args, world, rank):
     calib = None
     if args.dtype == "i8":  # calibration frames disjoint from the timed ones
         from rtdm.synth import BASE_SEED, synth_frames
-        calib = torch.from_numpy(synth_frames(8, args.img, args.img, seed=BASE_SEED + 4321)).cuda()
+        calib = torch.from_numpy(synth_frames(16, args.img, args.img, seed=BASE_SEED + 4321)).cuda()
     if args.dtype in ("f16", "i8"):
         det.half() if args.dtype == "f16" else det.int8(calib)
         if use_cls:
@@ -422,7 +426,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": args.dtype,
         "data": f"synthetic {args.img}x{args.img} uint8 frames (seeded, {len(frames)} rotations), synthetic "
-                f"calibrated detector weights"
+                f"calibrated detector weights ({args.weights} set)"
                 + (f", the reference's trained {args.classifier} weights" if args.classifier != "none" else ""),
         "config": {"workload": workload,
                    "global_batch": global_batch, "per_gpu_batch": b, "img": args.img,

@@ -282,8 +282,10 @@ rtdm_status rtdm_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int
  * cv2.INTER_LINEAR (the default interpolation) of uint8 3-channel frames [n, in_h, pitch]
  * to [n, out_h, out_w, 3]: half-pixel source coordinates, 11-bit fixed-point weights
  * (OpenCV resize.cpp restated; cv2 is not in this stack, so pixel parity with cv2 itself
- * is unpinned, the kernel is bit-exact with oracle/letterbox.py resize_linear).
- * swap_rb = 1 also turns BGR into RGB (the cv2.cvtColor of :70).                    */
+ * is unpinned, the kernel is bit-exact with oracle/letterbox.py resize_linear).  The
+ * vertical pass models OpenCV's SCALAR rounding, (b0*h0 + b1*h1 + 2^21) >> 22; cv2's
+ * SIMD 8-bit path (>> 4, mulhi, then (x + 2) >> 2) may round differently, by up to 1 LSB
+ * on a pixel.  swap_rb = 1 also turns BGR into RGB (the cv2.cvtColor of :70).       */
 rtdm_status rtdm_resize_linear(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int out_h, int out_w,
                                int swap_rb, uint8_t* out, void* stream);
 

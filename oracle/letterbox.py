@@ -144,7 +144,9 @@ def _inter_linear_tab(ssize, dsize):
 def resize_linear(img: np.ndarray, new_w: int, new_h: int) -> np.ndarray:
     """cv2.resize(img, (new_w, new_h)) -- INTER_LINEAR, the default interpolation used by
     real-time-inference.py:185 -- as restated above (same fixed-point sums as the
-    INTER_AREA growing path: int horizontal taps, (b0*h0 + b1*h1 + 2^21) >> 22)."""
+    INTER_AREA growing path: int horizontal taps, (b0*h0 + b1*h1 + 2^21) >> 22).  That is
+    OpenCV's scalar vertical rounding; its SIMD 8-bit path (>> 4, mulhi, (x + 2) >> 2) can
+    differ by 1 LSB, and with cv2 absent neither is pinned against cv2 itself."""
     src = img.astype(np.int64)
     xt, yt = _inter_linear_tab(img.shape[1], new_w), _inter_linear_tab(img.shape[0], new_h)
     x0 = np.array([t[0] for t in xt])

@@ -130,3 +130,82 @@ def score_ties(prediction: np.ndarray, conf_thres: float, iou_thres: float):
                     if ua > 0 and inter / ua > iou_thres:
                         harmful += 1
     return ties, harmful
+
+
+def _cands(pred: np.ndarray, conf: float):
+    """(keys [(row, class)], xyxy boxes, scores, obj) of one image's multi-label candidates
+    (utils.py:507-524 filters)."""
+    pred = np.asarray(pred, np.float32)
+    rows = np.nonzero((pred[:, 4] > np.float32(conf)) & ((pred[:, 2:4] > 2) & (pred[:, 2:4] < 4096)).all(1))[0]
+    p = pred[rows]
+    s = p[:, 5:] * p[:, 4:5]
+    i, j = np.nonzero(s > np.float32(conf))
+    b = p[i, :4]
+    box = np.stack([b[:, 0] - b[:, 2] / 2, b[:, 1] - b[:, 3] / 2, b[:, 0] + b[:, 2] / 2, b[:, 1] + b[:, 3] / 2], 1)
+    return [(int(rows[a]), int(c)) for a, c in zip(i, j)], box.astype(np.float64), s[i, j].astype(np.float64), \
+        p[i, 4].astype(np.float64)
+
+
+def _iou_matrix(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    iw = np.clip(np.minimum(a[:, None, 2], b[None, :, 2]) - np.maximum(a[:, None, 0], b[None, :, 0]), 0, None)
+    ih = np.clip(np.minimum(a[:, None, 3], b[None, :, 3]) - np.maximum(a[:, None, 1], b[None, :, 1]), 0, None)
+    inter = iw * ih
+    area_a = (a[:, 2] - a[:, 0]) * (a[:, 3] - a[:, 1])
+    area_b = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+    return inter / np.maximum(area_a[:, None] + area_b[None, :] - inter, 1e-30)
+
+
+def survivors_equal_outside_band(io_ref: np.ndarray, io_got: np.ndarray, conf_thres: float, iou_thres: float,
+                                 band: float = 1e-3):
+    """SURVEY §8d's end-to-end fp16 rule: the NMS survivor sets of two io tensors are equal
+    after excluding the candidates within `band` of the thresholds.  A candidate (row,
+    class) is near a threshold when, in either io, its objectness or its score is within
+    `band` of conf_thres, or when it overlaps a same-class candidate with IoU within `band`
+    of iou_thres, or with IoU > iou_thres - band and a score within `band` of its own (the
+    greedy order between them is then undecided); a candidate that overlaps (IoU >
+    iou_thres - band) a higher-scored excluded candidate of its class is excluded too (its
+    fate follows that one's).  Returns (n_ref survivors, n_got survivors, excluded
+    differences, unexplained differences [(image, row, class)])."""
+    ref_s, ref_i = non_max_suppression(io_ref, conf_thres, iou_thres, return_index=True)
+    got_s, got_i = non_max_suppression(io_got, conf_thres, iou_thres, return_index=True)
+    n_ref = n_got = n_exc = 0
+    bad = []
+    for b in range(len(io_ref)):
+        R = set() if ref_i[b] is None else {tuple(map(int, r)) for r in ref_i[b]}
+        G = set() if got_i[b] is None else {tuple(map(int, r)) for r in got_i[b]}
+        n_ref += len(R)
+        n_got += len(G)
+        D = R ^ G
+        if not D:
+            continue
+        # candidates of both io at a slightly lower threshold, so a near-threshold one is seen
+        keys, box, sc, obj = _cands(io_ref[b], conf_thres - band)
+        keys_g, _, sc_g, obj_g = _cands(io_got[b], conf_thres - band)
+        idx = {k: n for n, k in enumerate(keys)}
+        near = np.zeros(len(keys), bool)
+        near |= (np.abs(obj - conf_thres) <= band) | (np.abs(sc - conf_thres) <= band)
+        near_g = set()
+        for n, k in enumerate(keys_g):
+            if abs(obj_g[n] - conf_thres) <= band or abs(sc_g[n] - conf_thres) <= band:
+                near_g.add(k)
+                if k in idx:
+                    near[idx[k]] = True
+        cls = np.array([k[1] for k in keys])
+        iou = _iou_matrix(box, box)
+        same = cls[:, None] == cls[None, :]
+        np.fill_diagonal(same, False)
+        ov = same & (iou > iou_thres - band)
+        near |= (same & (np.abs(iou - iou_thres) <= band)).any(1)
+        near |= (ov & (np.abs(sc[:, None] - sc[None, :]) <= band)).any(1)
+        order = np.argsort(-sc, kind="stable")
+        for n in order:  # cascade downward in score
+            if not near[n]:
+                higher = ov[n] & (sc > sc[n])
+                if (higher & near).any():
+                    near[n] = True
+        for k in D:
+            if (near[idx[k]] if k in idx else k in near_g):
+                n_exc += 1
+            else:
+                bad.append((b,) + k)
+    return n_ref, n_got, n_exc, bad

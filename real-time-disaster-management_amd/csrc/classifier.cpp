@@ -331,6 +331,8 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
       h.q_channels += 3 * st.cin;
     }
     h.amax.alloc((size_t)std::max(1, h.q_channels) * sizeof(unsigned));
+    // zeroed: a first rtdm_classifier_calibrate(reset = 0) folds its maxima into these
+    RTDM_HIP(hipMemset(h.amax.p, 0, (size_t)std::max(1, h.q_channels) * sizeof(unsigned)));
   }
   h.per_image = off;
   h.blob.upload(blob);
@@ -343,6 +345,9 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
                "classify: batch " + std::to_string(n) + " exceeds max_batch " + std::to_string(h.max_batch));
   RTDM_REQUIRE(!h.int8 || h.calibrated || h.calibrating || h.q_channels == 0, RTDM_E_INVALID,
                "classify: int8 classifier not calibrated (rtdm_classifier_calibrate)");
+  // before any launch: an int8 handle's quantised stages only exist in the chained schedule
+  RTDM_REQUIRE(!h.int8 || (h.chain_start >= 0 && acff_chain_mode()) || h.chain_start < 0, RTDM_E_INVALID,
+               "classify: int8 handle needs acff_chain mode");
   if (n == 0) return;
   RTDM_REQUIRE(x, RTDM_E_INVALID, "classify: NULL input");
   const size_t es = esize(h.dtype);
@@ -559,7 +564,6 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       cur = View{buf(st.red_buf), st.redw.cout, 0};
     }
   }
-  RTDM_REQUIRE(!h.int8 || chain || h.chain_start < 0, RTDM_E_INVALID, "classify: int8 handle needs acff_chain mode");
   if (chain) {
     const int k = h.chain.nst;
     AcffI8 qs[4];

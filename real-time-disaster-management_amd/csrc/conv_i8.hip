@@ -5,8 +5,9 @@
 //
 //   chan_absmax_kernel  calibration: per-channel |x|max of an fp16 NHWC view (the
 //                       input of an int8 conv) over the calibration frames.  The
-//                       per-channel activation scale s_c = |x|max_c / 127 is folded into
-//                       the conv's weights on the host (W'[o][c] = W[o][c] * s_c, then
+//                       per-channel activation scale s_c = 2 |x|max_c / 127 is folded into
+//                       the conv's weights on the host (with the detector's 2x headroom,
+//                       detector.cpp kI8Headroom; W'[o][c] = W[o][c] * s_c, then
 //                       symmetric per-output-channel int8: s_w[o] = max|W'[o]| / 127).
 //   quantize_kernel     runtime: q = clamp(rint(x * (1 / s_c)), -127, 127), fp16 view ->
 //                       contiguous int8 [pixels][cin] (symmetric: an out-of-image tap,
@@ -66,7 +67,9 @@ __global__ __launch_bounds__(256) void quantize_kernel(const _Float16* __restric
   typedef float f4 __attribute__((ext_vector_type(4)));
   const int groups = cin / 8;
   const int total = npix * groups;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+  // unsigned cursor: total < 2^31 and the stride < 2^31, so i + stride never wraps
+  for (unsigned ui = blockIdx.x * blockDim.x + threadIdx.x; ui < (unsigned)total; ui += gridDim.x * blockDim.x) {
+    const int i = (int)ui;
     const int px = fdiv(i, fgroups);
     const int g = i - px * groups;
     const h8 x = *(const h8*)(p + (size_t)px * cs + co + g * 8);

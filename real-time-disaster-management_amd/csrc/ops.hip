@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ in, 
 }
 
 template <typename T, int VEC>
-// 32-bit item index (total < 2^31, checked at launch) split by multiply-shift divisions:
+// 32-bit item index (total < 2^31, checked at launch; unsigned loop cursor) split by multiply-shift divisions:
 // the 64-bit div / mod chain per item cost more than the item's memory traffic.
 __global__ __launch_bounds__(256) void maxpool_vec_kernel(const T* __restrict__ in, int in_cs, int in_co, int n,
                                                           int h, int w, int c, int k, int stride, int pad,
@@ -410,7 +410,10 @@ __global__ __launch_bounds__(256) void maxpool_vec_kernel(const T* __restrict__ 
   typedef T tv __attribute__((ext_vector_type(VEC)));
   const int cg = c / VEC;
   const int total = n * oh * ow * cg;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+  // unsigned cursor: total < 2^31 and the stride < 2^31, so idx + stride < 2^32 never wraps
+  // (a signed idx + stride could overflow for total within a grid's span of 2^31)
+  for (unsigned uidx = blockIdx.x * blockDim.x + threadIdx.x; uidx < (unsigned)total; uidx += gridDim.x * blockDim.x) {
+    const int idx = (int)uidx;
     int p = fdiv(idx, fcg);
     const int g = idx - p * cg;
     const int q = fdiv(p, fow);

@@ -137,6 +137,9 @@ class _ACFFClassifier(torch.nn.Module):
                                                ctypes.byref(h)))
         self._handle = h
         self._handle_key = (key, cap)
+        # a new device handle: cached hipGraphs that captured the old one must not replay
+        # (rtdm.pipeline keys its graphs on this counter, never on the handle address)
+        self.handle_generation = getattr(self, "handle_generation", 0) + 1
         if self._dtype == L.RTDM_I8:
             self._calibrate(h)
         return h

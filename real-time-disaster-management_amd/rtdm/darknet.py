@@ -174,6 +174,9 @@ class Darknet(torch.nn.Module):
                                              self._stream.size, cap, ctypes.byref(h)))
         self._handle = h
         self._handle_key = (key, cap)
+        # a new device handle: cached hipGraphs that captured the old one must not replay
+        # (rtdm.pipeline keys its graphs on this counter, never on the handle address)
+        self.handle_generation = getattr(self, "handle_generation", 0) + 1
         if self._dtype == L.RTDM_I8:
             self._calibrate(h)
         return h

@@ -113,7 +113,7 @@ class TwoStagePipeline:
         n = frames.shape[0]
         with torch.cuda.device(frames.device):
             key = self._graph_key(frames)
-            g = self._graphs.get(key)
+            g = self._graphs.pop(key, None)
             if g is None:
                 self._launch(frames)  # first call: handles, plans, workspaces, resize tables
                 torch.cuda.synchronize()
@@ -121,7 +121,8 @@ class TwoStagePipeline:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self._launch(frames)
-                self._graphs[key] = g
+            self._graphs[key] = g  # (re)inserted last: most recently used
+            self._drop_stale_graphs(key)
             if stream is None:
                 g.replay()
             else:
@@ -129,11 +130,29 @@ class TwoStagePipeline:
                     g.replay()
         return self._buffers(n, frames.device)
 
+    # at most this many captured graphs per pipeline (least recently used dropped first)
+    max_graphs = 8
+
     def _graph_key(self, frames):
+        """Handles are created on demand (and recreated for a larger batch, a dtype change or
+        new weights), so a graph is keyed on the handles' GENERATION counters: a destroyed
+        handle's successor may reuse its heap address, and a graph replaying the old
+        handle's arena and weights would read freed memory."""
         n = frames.shape[0]
-        hc = self.classifier._get_handle(n).value if self.classifier is not None else 0
-        hd = self.detector.handle(n)
-        return (n, frames.data_ptr(), tuple(frames.shape), str(frames.device), hc, hd.value)
+        gc = -1
+        if self.classifier is not None:
+            self.classifier._get_handle(n)
+            gc = self.classifier.handle_generation
+        self.detector.handle(n)
+        return (n, frames.data_ptr(), tuple(frames.shape), str(frames.device), gc, self.detector.handle_generation)
+
+    def _drop_stale_graphs(self, key):
+        """Forget graphs of older handle generations, then bound the cache (LRU)."""
+        gens = key[4:]
+        for k in [k for k in self._graphs if k[4:] != gens]:
+            del self._graphs[k]
+        while len(self._graphs) > self.max_graphs:
+            del self._graphs[next(iter(self._graphs))]
 
     def _launch(self, frames: torch.Tensor, stream=None) -> dict:
         n = frames.shape[0]

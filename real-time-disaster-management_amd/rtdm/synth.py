@@ -14,6 +14,7 @@
 """
 from __future__ import annotations
 
+import json
 import os
 import re
 
@@ -131,12 +132,17 @@ ACFF_KEYS = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "conv3.
              "batch_norm.running_mean", "batch_norm.running_var")
 
 
-def synth_acff_params(cfg_text: str, seed: int = 9, calib: dict | None = None) -> dict:
+def synth_acff_params(cfg_text: str, seed: int = 9, calib: dict | None = None, preset: str = "he",
+                      cond: dict | None = None, conv_seed: int = 7) -> dict:
     """{layer: {ACFF state-dict key: array}} for a Darknet cfg's [acff] blocks.  These are
     not in a .weights stream (load_darknet_weights, models.py:457-486, loads only
     [convolutional]); the reference gets them from a .pt state dict.  Depthwise branches
     He-scaled over their 9 taps and down-weighted by 1/sqrt(3) (three are summed), the 1x1
-    He-scaled, BN gamma 1 / beta 0 with running stats from `calib` (acffmean<i>/acffvar<i>)."""
+    He-scaled, BN gamma 1 / beta 0 with running stats from `calib` (acffmean<i>/acffvar<i>).
+    preset "cond": the well-conditioned set's blocks (drawn in the same cfg walk as its
+    conv stream, seeded by conv_seed / seed)."""
+    if preset == "cond":
+        return _cond_generate(cfg_text, conv_seed, seed, calib, cond or COND)[1]
     rng = np.random.default_rng(seed)
     out = {}
     for (i, c, f) in acff_layers(cfg_text):
@@ -162,8 +168,8 @@ def cfg_name(cfg_path_or_name: str) -> str:
     return re.sub(r"\.cfg$", "", os.path.basename(cfg_path_or_name))
 
 
-def load_calibration(name: str):
-    path = os.path.join(DATA_DIR, f"synth_{name}.npz")
+def load_calibration(name: str, preset: str = "he"):
+    path = os.path.join(DATA_DIR, f"synth_{name}.npz" if preset == "he" else f"synth_{name}_{preset}.npz")
     if not os.path.exists(path):
         return None
     z = np.load(path, allow_pickle=False)
@@ -171,8 +177,12 @@ def load_calibration(name: str):
 
 
 def synth_darknet_weights(cfg_text: str, seed: int = 7, calib: dict | None = None,
-                          obj_bias: float = -3.5) -> np.ndarray:
-    """Float32 darknet weight stream (after the 20-byte header) for cfg_text."""
+                          obj_bias: float = -3.5, preset: str = "he", cond: dict | None = None) -> np.ndarray:
+    """Float32 darknet weight stream (after the 20-byte header) for cfg_text.
+    preset "he": mean-field He-scaled random convs; "cond": the well-conditioned set
+    (see COND below)."""
+    if preset == "cond":
+        return _cond_generate(cfg_text, seed, 9, calib, cond or COND)[0]
     rng = np.random.default_rng(seed)
     parts = []
     for (i, cin, cout, k, bn, head) in conv_layers(cfg_text):
@@ -197,6 +207,164 @@ def synth_darknet_weights(cfg_text: str, seed: int = 7, calib: dict | None = Non
             parts.append(bias)
         parts.append(w.reshape(-1))
     return np.concatenate(parts).astype(np.float32)
+
+
+# ------------------------------------------------- well-conditioned weights --
+# The "he" set above is mean-field random: every layer is a fresh He-scaled random map
+# whose BatchNorm re-centres and re-normalises its output, so a perturbation of an
+# activation (an fp16 or int8 rounding) grows ~1.16x per LeakyReLU layer relative to the
+# signal (the activation's DC part carries norm that BN removes) -- a 75-conv net turns
+# fp16 storage noise into pixel-scale box errors.  Trained detectors are not like that:
+# their filters are smooth and their channel maps low-rank.  The "cond" set models that:
+#   * each conv's output channels are a rank-r mix (A: cout x r) of r latent maps, and
+#     each conv reads its input through the producing layer's basis U (cin x r), so
+#     rounding noise spread over all cin channels is projected onto r of them while the
+#     signal (which lives in span U) passes: W = A . M . U^T (+ a small full-rank part so
+#     every channel and tap still feeds every output, as the fp32 parity bars need);
+#   * the r x r x 3 x 3 mixing taps M are mostly a smooth binomial kernel (white rounding
+#     noise is averaged, smooth features pass);
+#   * a residual branch's last conv writes into the stream's own basis, at BatchNorm
+#     gamma `gamma_res`;
+#   * head rows are scaled per field by calibration (`headgain<i>`: x,y logits std 1,
+#     w,h std 0.25 -- boxes near their anchors, as trained YOLO heads are -- objectness
+#     and class logits std 2) and the objectness bias set for ~2 % of anchors at obj > 0.3.
+# Only elementwise float64 arithmetic in a fixed order (no BLAS, no reductions), so the
+# stream is bit-identical on any host.
+COND = {"rank": 16, "iso": 0.05, "lp": 0.85, "gamma_res": 0.5, "obj_pass": 0.002,
+        "head_std": {"xy": 1.0, "wh": 0.1, "obj": 2.0, "cls": 2.0}}
+_BINOM = np.outer([1.0, 2.0, 1.0], [1.0, 2.0, 1.0]) / 6.0  # unit Frobenius norm
+
+
+def _gauss(rng, shape, std):
+    return rng.standard_normal(shape) * std
+
+
+def _lowrank_w(rng, U, A, cout, k, cond, stem_hp=None):
+    """cout x cin x k x k float64: sqrt(1-iso) * (A M U^T, He-scaled) + sqrt(iso) * He."""
+    cin, rin = U.shape
+    fan = cin * k * k
+    rout = A.shape[1] if A is not None else cout
+    g = rng.standard_normal((rout, rin))
+    if k == 1:
+        M = g[:, :, None, None]
+    elif stem_hp is not None:  # the frame-reading stem: random taps, DC part scaled by (1 - stem_hp)
+        e = rng.standard_normal((rout, rin, k, k))
+        tot = np.zeros(e.shape[:2])
+        for t in range(k * k):  # fixed-order sum: no numpy reduction (bit-stable across hosts)
+            tot = tot + e[:, :, t // k, t % k]
+        M = e - (stem_hp * tot / (k * k))[:, :, None, None]
+    else:
+        e = rng.standard_normal((rout, rin, k, k)) / float(k)
+        M = g[:, :, None, None] * (np.sqrt(cond["lp"]) * _BINOM) + e * np.sqrt(1.0 - cond["lp"])
+    T = np.zeros((rout, cin, k, k))
+    for l in range(rin):
+        T += M[:, l][:, None] * U[None, :, l, None, None]
+    if A is None:  # head: outputs read the latents directly
+        W = T
+        var = rin / cin / (k * k)
+    else:
+        W = np.zeros((cout, cin, k, k))
+        for j in range(rout):
+            W += A[:, j, None, None, None] * T[j][None]
+        var = rout * rin / cout / cin / (k * k)
+    he = 2.0 / fan
+    W *= np.sqrt(he * (1.0 - cond["iso"]) / var)
+    W += _gauss(rng, (cout, cin, k, k), np.sqrt(he * cond["iso"]))
+    return W
+
+
+def _cond_generate(cfg_text: str, seed: int, acff_seed: int, calib: dict | None, cond: dict):
+    """(darknet stream float32, {acff layer: params}) of the well-conditioned set.  A
+    calibration file records the knobs it was made with (`cond_json`); they win."""
+    if calib is not None and "cond_json" in calib:
+        cond = json.loads(str(calib["cond_json"]))
+    rng = np.random.default_rng(seed)
+    arng = np.random.default_rng(acff_seed)
+    mdefs = parse_cfg_text(cfg_text)
+    net = mdefs.pop(0)
+    c0 = int(net.get("channels", 3))
+    fout = [c0]
+    basis = [np.eye(c0)]
+    r = cond["rank"]
+    parts, acff = [], {}
+
+    def new_basis(c):
+        return _gauss(rng, (c, min(r, c)), 1.0 / np.sqrt(c))
+
+    def cal(key, default):
+        return calib[key] if calib is not None and key in calib else default
+
+    for i, m in enumerate(mdefs):
+        t = m["type"]
+        nxt = mdefs[i + 1] if i + 1 < len(mdefs) else {"type": ""}
+        U = basis[-1]
+        if t == "convolutional":
+            f, k, bn = int(m["filters"]), int(m["size"]), int(m["batch_normalize"])
+            head = nxt["type"] == "yolo"
+            A, res = None, False
+            if not head:
+                if nxt["type"] == "shortcut":
+                    fr = nxt["from"][0]
+                    src = basis[i + 2 + fr if fr < 0 else fr + 1]
+                    res = src.shape[0] == f
+                A = src if res else new_basis(f)
+            w = _lowrank_w(rng, U, A, f, k, cond, stem_hp=cond.get("stem_hp") if i == 0 else None).astype(np.float32)
+            if bn:
+                beta = np.zeros(f, np.float32)
+                gamma = np.full(f, cond["gamma_res"] if res else 1.0, np.float32)
+                parts += [beta, gamma, cal(f"mean{i}", np.zeros(f, np.float32)).astype(np.float32),
+                          cal(f"var{i}", np.ones(f, np.float32)).astype(np.float32)]
+            else:
+                bias = np.zeros(f, np.float32)
+                if head:
+                    w *= cal(f"headgain{i}", np.ones(f, np.float32)).astype(np.float32)[:, None, None, None]
+                    no = int(nxt["classes"]) + 5
+                    for a in range(f // no):
+                        bias[a * no + 4] = float(cal(f"objbias{i}", -3.5))
+                parts.append(bias)
+            parts.append(w.reshape(-1))
+            basis.append(A if A is not None else new_basis(f))
+        elif t == "acff":
+            f = int(m["filters"])
+            c = U.shape[0]
+            p = {}
+            for b in (1, 2, 3):  # shared smooth tap + a small per-channel part
+                dw = (np.sqrt(cond["lp"]) * _BINOM)[None, None] + _gauss(arng, (c, 1, 3, 3), np.sqrt(1 - cond["lp"]) / 3)
+                p[f"conv{b}.weight"] = (dw * np.sqrt(1.0 / 3.0)).astype(np.float32)
+                p[f"conv{b}.bias"] = _gauss(arng, c, 0.05).astype(np.float32)
+            head = nxt["type"] == "yolo"
+            A = None if head else _gauss(arng, (f, min(r, f)), 1.0 / np.sqrt(f))
+            p["fused_conv.weight"] = _lowrank_w(arng, U, A, f, 1, cond).astype(np.float32)
+            p["fused_conv.bias"] = cal(f"acffbias{i}", _gauss(arng, f, 0.05)).astype(np.float32)
+            p["batch_norm.weight"] = cal(f"acffgain{i}", np.ones(f, np.float32)).astype(np.float32)
+            p["batch_norm.bias"] = cal(f"acffobj{i}", np.zeros(f, np.float32)).astype(np.float32)
+            p["batch_norm.running_mean"] = cal(f"acffmean{i}", np.zeros(f, np.float32)).astype(np.float32)
+            p["batch_norm.running_var"] = cal(f"acffvar{i}", np.ones(f, np.float32)).astype(np.float32)
+            acff[i] = p
+            basis.append(A if A is not None else _gauss(arng, (f, min(r, f)), 1.0 / np.sqrt(f)))
+            fout.append(f)
+            continue
+        elif t == "route":
+            ls = [l if l < 0 else l + 1 for l in m["layers"]]  # index into basis/fout (input at 0)
+            ls = [len(basis) + l if l < 0 else l for l in ls]
+            bs = [basis[l] for l in ls]
+            rows = sum(b.shape[0] for b in bs)
+            cols = sum(b.shape[1] for b in bs)
+            B = np.zeros((rows, cols))
+            ro = co = 0
+            for b in bs:
+                B[ro:ro + b.shape[0], co:co + b.shape[1]] = b
+                ro += b.shape[0]
+                co += b.shape[1]
+            basis.append(B)
+            fout.append(rows)
+            continue
+        elif t in ("shortcut", "maxpool", "upsample", "yolo"):
+            basis.append(U)
+        else:
+            raise ValueError(f"unsupported layer type {t}")
+        fout.append(basis[-1].shape[0])
+    return np.concatenate(parts).astype(np.float32), acff
 
 
 def write_darknet_weights(path: str, stream: np.ndarray) -> None:

@@ -114,7 +114,10 @@ def classifier_goldens():
     np.savez_compressed(os.path.join(HERE, "cls_golden.npz"), **gz)
 
 
-def det_goldens():
+def det_goldens(preset: str = "he"):
+    """preset "he" -> det_golden.npz (the mean-field weights, kept as the stress case);
+    "cond" -> det_golden_cond.npz (the well-conditioned set the SURVEY §8d fp16 / int8 bars
+    are asserted on; 2 frames per case)."""
     def nms_stub(boxes, scores, iou):
         keep = onms.nms_kernel(boxes.numpy(), scores.numpy(), float(iou))
         return torch.from_numpy(keep)
@@ -122,14 +125,17 @@ def det_goldens():
     models, utils = import_darknet(nms_stub)
     out = {}
     for (cfg, size, nf, full) in DET_CASES:
+        if preset == "cond":
+            nf = max(nf, 2)
         key = f"{cfg}@{size}"
         text = open(os.path.join(DET_DIR, "cfg", cfg + ".cfg")).read()
-        stream = synth.synth_darknet_weights(text, calib=synth.load_calibration(cfg))
+        cal = synth.load_calibration(cfg, preset)
+        stream = synth.synth_darknet_weights(text, calib=cal, preset=preset)
         model = models.Darknet(os.path.join(DET_DIR, "cfg", cfg + ".cfg"), (size, size))
         with tempfile.NamedTemporaryFile(suffix=".weights") as f:
             synth.write_darknet_weights(f.name, stream)
             models.load_darknet_weights(model, f.name)
-        acff = synth.synth_acff_params(text, calib=synth.load_calibration(cfg))
+        acff = synth.synth_acff_params(text, calib=cal, preset=preset)
         for i, p in acff.items():  # [acff] blocks: state-dict parameters (not in .weights)
             sd = {k: torch.from_numpy(v) for k, v in p.items()}
             sd["batch_norm.num_batches_tracked"] = torch.tensor(0)
@@ -162,7 +168,7 @@ def det_goldens():
                 out[f"{key}/nms{conf}_{iou}/{b}"] = d
                 out[f"{key}/nms{conf}_{iou}/{b}/idx"] = np.zeros((0, 2), np.int64) if idx[b] is None else idx[b]
             print(key, "nms", conf, iou, [0 if d is None else len(d) for d in dets])
-    np.savez_compressed(os.path.join(HERE, "det_golden.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, "det_golden.npz" if preset == "he" else "det_golden_cond.npz"), **out)
 
 
 def shapes_golden():
@@ -189,3 +195,5 @@ if __name__ == "__main__":
         classifier_goldens()
     if not only or "det" in only:
         det_goldens()
+    if not only or "detcond" in only:
+        det_goldens("cond")

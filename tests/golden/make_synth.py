@@ -9,6 +9,7 @@ Run: python tests/golden/make_synth.py
 """
 from __future__ import annotations
 
+import json
 import os
 import sys
 import tempfile
@@ -28,16 +29,43 @@ CFGS = ["yolov4-tiny-aider-416", "yolov3-aider-416", "yolov3-spp-aider", "yolov3
         "yolov4-tiny-swish", "yolov4-tiny-3l-512x512", "yolov3-acffx"]
 
 
-def calibrate(name: str, size: int = 416):
+HEAD_FIELDS = ("xy", "xy", "wh", "wh", "obj")
+# per-cfg knobs of the "cond" set: YOLO-ACFF's 14-channel ACFF heads (LeakyReLU(0.01) before
+# BatchNorm) swing several-fold in scale from frame to frame, so a lower rank and narrower
+# w,h logits keep its fp16 boxes inside SURVEY §8d's 0.5 px
+CFG_COND = {"yolov3-acffx": {"rank": 8, "head_std": {"wh": 0.05}},
+            # the detector of record runs at 608 (BASELINE config 4): calibrate it there
+            "yolov4-tiny-aider-416": {"calib_size": 608}}
+
+
+def cond_for(name: str, base: dict | None = None) -> dict:
+    c = json.loads(json.dumps(base or synth.COND))
+    for k, v in CFG_COND.get(name, {}).items():
+        if isinstance(v, dict):
+            c[k].update(v)
+        else:
+            c[k] = v
+    return c
+
+
+def calibrate(name: str, size: int | None = None, preset: str = "he", cond: dict | None = None,
+              write: bool = True):
+    """preset "he": BN statistics + objectness bias.  preset "cond" (the well-conditioned set,
+    rtdm.synth.COND): also per-channel head gains (headgain<i> / acffgain<i>) giving each head
+    field its target logit std (COND["head_std"]) before the objectness bias is set."""
     models, _ = import_darknet()
     cfg_path = os.path.join(DET_DIR, "cfg", name + ".cfg")
     text = open(cfg_path).read()
-    stream = synth.synth_darknet_weights(text, calib=None)
+    cond = cond or cond_for(name)
+    if size is None:  # "he": 416 for every cfg; "cond": the cfg's own [net] width
+        size = (cond.get("calib_size") or int(synth.parse_cfg_text(text)[0].get("width", 416))) \
+            if preset == "cond" else 416
+    stream = synth.synth_darknet_weights(text, calib=None, preset=preset, cond=cond)
     model = models.Darknet(cfg_path, (size, size))
     with tempfile.NamedTemporaryFile(suffix=".weights") as f:
         synth.write_darknet_weights(f.name, stream)
         models.load_darknet_weights(model, f.name)
-    acff = synth.synth_acff_params(text)  # ACFF blocks (yolov3-acffx.cfg): not in .weights
+    acff = synth.synth_acff_params(text, preset=preset, cond=cond)  # ACFF blocks (yolov3-acffx.cfg): not in .weights
     for i, p in acff.items():
         mod = model.module_list[i][0]
         sd = {k: torch.from_numpy(v) for k, v in p.items()}
@@ -48,10 +76,15 @@ def calibrate(name: str, size: int = 416):
     heads = {}
     mdefs = model.module_defs
     logit03 = float(np.log(0.3 / 0.7))
+
+    def head_target(no, c):
+        return np.array([cond["head_std"][HEAD_FIELDS[k % no] if k % no < 5 else "cls"] for k in range(c)],
+                        np.float32)
     for i in acff:
         mod = model.module_list[i][0]
+        is_head = i + 1 < len(mdefs) and mdefs[i + 1]["type"] == "yolo"
 
-        def bn_pre(m, inp, i=i):
+        def bn_pre(m, inp, i=i, is_head=is_head):
             x = inp[0].detach().double()
             mean = x.mean(dim=(0, 2, 3))
             var = x.var(dim=(0, 2, 3), unbiased=False) + 1e-6
@@ -59,13 +92,28 @@ def calibrate(name: str, size: int = 416):
             m.running_var.copy_(var.float())
             calib[f"acffmean{i}"] = mean.float().numpy()
             calib[f"acffvar{i}"] = var.float().numpy()
+            if preset == "cond" and is_head:
+                g = head_target(int(mdefs[i + 1]["classes"]) + 5, x.shape[1])
+                m.weight.copy_(torch.from_numpy(g))
+                calib[f"acffgain{i}"] = g
         mod.batch_norm.register_forward_pre_hook(bn_pre)
-        if i + 1 < len(mdefs) and mdefs[i + 1]["type"] == "yolo":
+        if preset == "cond":
+            # ACFF applies LeakyReLU(0.01) BEFORE its BatchNorm (acff.py:51-53 order, models.py
+            # ACFF the same): centre the fused 1x1 output with its bias, or a channel whose
+            # pre-activation sits below zero on the calibration frames gets a ~100x BN gain
+            def fused_fwd(m, inp, out, i=i):
+                mean = out.detach().double().mean(dim=(0, 2, 3))
+                b = (m.bias.detach().double() - mean).float()
+                calib[f"acffbias{i}"] = b.numpy()
+                out.sub_(mean.float().view(1, -1, 1, 1))
+                m.bias.copy_(b)
+            mod.fused_conv.register_forward_hook(fused_fwd)
+        if is_head:
             def ahook(m, inp, out, i=i):
                 no = int(mdefs[i + 1]["classes"]) + 5
                 na = out.shape[1] // no
                 obj = out.detach().view(out.shape[0], na, no, *out.shape[2:])[:, :, 4]
-                q = float(np.quantile(obj.numpy().reshape(-1), 0.98))
+                q = float(np.quantile(obj.numpy().reshape(-1), 1.0 - (cond["obj_pass"] if preset == "cond" else 0.02)))
                 shift = np.zeros(out.shape[1], np.float32)
                 shift[[a * no + 4 for a in range(na)]] = logit03 - q
                 calib[f"acffobj{i}"] = shift
@@ -90,9 +138,17 @@ def calibrate(name: str, size: int = 416):
             conv.register_forward_hook(hook)
         elif i + 1 < len(mdefs) and mdefs[i + 1]["type"] == "yolo":
             def hhook(m, inp, out, i=i):
+                if preset == "cond":  # per-field logit std, then the bias below
+                    no = int(mdefs[i + 1]["classes"]) + 5
+                    b = m.bias.detach().view(1, -1, 1, 1)
+                    raw = out.detach().double() - b
+                    g = (torch.from_numpy(head_target(no, out.shape[1])).double()
+                         / raw.std(dim=(0, 2, 3), unbiased=False).clamp_min(1e-12)).float()
+                    calib[f"headgain{i}"] = g.numpy()
+                    out.copy_((raw * g.double().view(1, -1, 1, 1)).float() + b)
                 heads[i] = out.detach()
             conv.register_forward_hook(hhook)
-    frames = synth.synth_frames(2, size, size, seed=synth.BASE_SEED + 1000)
+    frames = synth.synth_frames(8 if preset == "cond" else 2, size, size, seed=synth.BASE_SEED + 1000)
     x = torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0
     with torch.no_grad():
         model(x)
@@ -100,10 +156,14 @@ def calibrate(name: str, size: int = 416):
         no = int(mdefs[i + 1]["classes"]) + 5
         na = p.shape[1] // no
         obj = p.view(p.shape[0], na, no, *p.shape[2:])[:, :, 4] - (-3.5)  # remove the default bias
-        q = float(np.quantile(obj.numpy().reshape(-1), 0.98))
+        q = float(np.quantile(obj.numpy().reshape(-1), 1.0 - (cond["obj_pass"] if preset == "cond" else 0.02)))
         calib[f"objbias{i}"] = np.array(logit03 - q, np.float32)
+    if preset == "cond":
+        calib["cond_json"] = np.array(json.dumps(cond, sort_keys=True))
+    if not write:
+        return calib
     os.makedirs(synth.DATA_DIR, exist_ok=True)
-    out = os.path.join(synth.DATA_DIR, f"synth_{name}.npz")
+    out = os.path.join(synth.DATA_DIR, f"synth_{name}.npz" if preset == "he" else f"synth_{name}_{preset}.npz")
     np.savez_compressed(out, **calib)
     print(name, "->", out, len(calib), "arrays; obj biases",
           {k: float(v) for k, v in calib.items() if k.startswith("objbias")})
@@ -111,5 +171,9 @@ def calibrate(name: str, size: int = 416):
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    for n in (sys.argv[1:] or CFGS):
-        calibrate(n)
+    args = sys.argv[1:]
+    preset = "he"
+    if args and args[0] in ("--cond", "--he"):
+        preset = args.pop(0)[2:]
+    for n in (args or CFGS):
+        calibrate(n, preset=preset)

@@ -1,21 +1,21 @@
-"""GPU: the int8-quantised detector (RTDM_I8, BASELINE config 5) against the fp32 oracle.
+"""GPU: the int8-quantised detector and classifier (RTDM_I8, BASELINE config 5).
 
-The reference has no numeric int8 oracle (its int8 artefacts are opaque TensorRT
-engines / calibration caches).  The int8 path is checked against a model
-of the same scheme on the oracle (oracle/int8.py: per-channel activation scales folded
-into per-output-channel int8 weights, the same eligible convs, calibrated on the same
-frames): the HIP int8 io may deviate from the fp32 oracle by at most 1.5x that model's
-own deviation (max and 99th percentile of xy px, relative wh and probabilities), and its
-detection match (same class, IoU >= 0.9, SURVEY §8d's criterion) may trail the model's by
-at most 5 points.
+The reference has no numeric int8 path (opaque TensorRT engines and entropy-calibration
+caches), so the int8 paths are judged as §8d says, against the fp32 oracle:
+  detector:   detection match (same class, IoU >= 0.9) of the fp32 survivors at conf 0.3 /
+              IoU 0.4 >= 97 % (survivors whose confidence is within 0.02 of the threshold
+              excluded: int8 moves scores by ~1e-2), on the well-conditioned synthetic
+              weights (rtdm.synth COND),
+              16 evaluation frames, 16 disjoint calibration frames;
+  classifier: top-1 agreement with fp32 >= 99 % on frames whose fp32 top-2 logit gap is not
+              a near-tie.
+The HIP kernels are also held to a model of the same scheme on the oracle (oracle/int8.py:
+per-input-channel activation scales 2 |x|max / 127 folded into per-output-channel int8
+weights; the int8 convs are the Cin % 128 == 0 ones except a conv whose output only a YOLO
+head conv reads): io deviation from fp32 within 1.5x the model's own.
 
-SURVEY §8d's absolute bar (>= 97 % detection match) is out of reach of ANY 8-bit format
-on these synthetic BatchNorm-calibrated weights: the oracle with bf16 conv inputs and
-weights matches 91/105 of its own fp32 survivors, with 0.2 % multiplicative noise per conv
-input 97/105, and a single int8 layer (L8) alone 65/105 (tools/int8_emulate.py; the
-mean-field BN nets at init amplify a perturbation ~1.2x per layer).  The bar is
-therefore the scheme's own error, measured, with the kernel held to it.  Calibration
-frames are disjoint from the evaluation frames.
+The mean-field "he" weights (kept as the fp32 stress case) amplify any perturbation ~1.2x
+per layer; no 8-bit scheme reaches 97 % on them (the scheme model: 33 % at 2x headroom).
 """
 import ctypes
 
@@ -67,34 +67,42 @@ def _stats(io, ref):
             (d[..., 4:].max(), np.percentile(d[..., 4:], 99))]
 
 
-@pytest.mark.parametrize("case,nframes", [("yolov4-tiny-aider-416@608", 4)])
-def test_int8_detector_vs_scheme_model(dev, case, nframes):
-    from oracle import int8 as OQ
-    from oracle.darknet import DarknetRef
-    from rtdm.darknet import Darknet
-    from rtdm.synth import BASE_SEED, load_calibration, synth_darknet_weights, synth_frames
-    cfg, size = case.split("@")
-    size = int(size)
+def _det_cond(cfg):
+    from rtdm.synth import load_calibration, synth_darknet_weights
     text = cfg_text(cfg)
-    stream = synth_darknet_weights(text, calib=load_calibration(cfg))
-    cal_frames = synth_frames(8, size, size, seed=BASE_SEED + 4321)
-    frames = synth_frames(nframes, size, size, seed=BASE_SEED + 700)
-    m = Darknet(text, (size, size))
-    m.load_weight_stream(stream)
-    m.int8(torch.from_numpy(cal_frames).to(dev))
-    io = m(torch.from_numpy(frames).to(dev))[0].cpu().numpy()
-    desc = m.describe()
-    assert " dtype i8 " in desc
+    return text, synth_darknet_weights(text, calib=load_calibration(cfg, "cond"), preset="cond")
+
+
+def _int8_names(m, n):
     from rtdm import _lib as L
-    h = m.handle(nframes)
+    h = m.handle(n)
     names = []
     for i in range(L.lib().rtdm_detector_num_steps(h)):
         nm = ctypes.create_string_buffer(64)
         L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, None, None, None))
         names.append(nm.value.decode())
-    n_i8 = sum(n.startswith(("conv_pipe_i8", "conv_pipew_i8")) for n in names)
-    assert n_i8 >= 8, names  # L8..L28 incl. the fused head conv
+    return names
 
+
+def test_int8_detector_survey_bar(dev):
+    from oracle import int8 as OQ
+    from oracle.darknet import DarknetRef
+    from rtdm.darknet import Darknet
+    from rtdm.synth import BASE_SEED, synth_frames
+    cfg, size, nf = "yolov4-tiny-aider-416", 608, 16
+    text, stream = _det_cond(cfg)
+    cal_frames = synth_frames(16, size, size, seed=BASE_SEED + 4321)
+    frames = synth_frames(nf, size, size, seed=BASE_SEED + 700)
+    m = Darknet(text, (size, size))
+    m.load_weight_stream(stream)
+    m.int8(torch.from_numpy(cal_frames).to(dev))
+    io = m(torch.from_numpy(frames).to(dev))[0].cpu().numpy()
+    assert " dtype i8 " in m.describe()
+    names = _int8_names(m, nf)
+    n_i8 = sum(n.startswith(("conv_pipe_i8", "conv_pipew_i8")) for n in names)
+    assert n_i8 == 7, names  # L8 L10 L12 L13 L18 L21 L25; L14 / L28 feed only a head: fp16
+
+    torch.set_num_threads(16)
     ref = DarknetRef(text, stream)
     xe = torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0
     xc = torch.from_numpy(cal_frames).permute(0, 3, 1, 2).float() / 255.0
@@ -108,21 +116,22 @@ def test_int8_detector_vs_scheme_model(dev, case, nframes):
         assert g[0] <= 1.5 * f[0] + s and g[1] <= 1.5 * f[1] + s, (name, g, f)
     mh, t = _match(io32, io)
     me, _ = _match(io32, emu)
-    print(f"int8 detection match: HIP {mh}/{t}, scheme model {me}/{t}")
-    assert t > 20 and mh / t >= me / t - 0.05, (mh, me, t)
+    print(f"int8 detection match: HIP {mh}/{t} = {mh / t:.4f}, scheme model {me}/{t}")
+    assert t >= 60, t
+    assert mh / t >= 0.97, (mh, t)
 
 
 def test_int8_first_layer_vs_fp16(dev):
     """The first int8 conv (L8 of yolov4-tiny-aider-416@608) against the fp16 run of the same
-    frames: within 4 % mean relative error (measured 2.8 % with the per-channel scheme)."""
+    frames: mean relative error within 6 % (2x headroom doubles the activation step of the
+    former |x|max / 127 scheme, measured 2.8 % there)."""
     from rtdm.darknet import Darknet
-    from rtdm.synth import BASE_SEED, load_calibration, synth_darknet_weights, synth_frames
-    text = cfg_text("yolov4-tiny-aider-416")
-    stream = synth_darknet_weights(text, calib=load_calibration("yolov4-tiny-aider-416"))
+    from rtdm.synth import BASE_SEED, synth_frames
+    text, stream = _det_cond("yolov4-tiny-aider-416")
     x = torch.from_numpy(synth_frames(3, 608, 608, seed=BASE_SEED + 700)).to(dev)
     q = Darknet(text, (608, 608))
     q.load_weight_stream(stream)
-    q.int8(torch.from_numpy(synth_frames(8, 608, 608, seed=BASE_SEED + 4321)).to(dev))
+    q.int8(torch.from_numpy(synth_frames(16, 608, 608, seed=BASE_SEED + 4321)).to(dev))
     q(x)
     f = Darknet(text, (608, 608))
     f.load_weight_stream(stream)
@@ -131,7 +140,7 @@ def test_int8_first_layer_vs_fp16(dev):
     a, b = f.layer_output(8, 3), q.layer_output(8, 3)
     rel = float((a - b).abs().mean() / a.abs().mean())
     print("L8 int8 vs fp16 mean relative error", rel)
-    assert rel <= 0.04
+    assert rel <= 0.06
 
 
 def test_int8_requires_calibration(dev):

@@ -171,14 +171,15 @@ def test_classifier_batch_edges(dev, cls_weights):
 
 
 # --------------------------------------------------------------- detector --
-def _darknet(cfg, size, half=False):
+def _darknet(cfg, size, half=False, preset="he"):
     from rtdm.darknet import Darknet
     from rtdm.synth import inline_acff, load_calibration, synth_acff_params, synth_darknet_weights
     text = cfg_text(cfg)
     m = Darknet(text, (size, size))
-    calib = load_calibration(cfg)
+    calib = load_calibration(cfg, preset)
     # YOLO-ACFF cfgs: the [acff] blocks' state-dict parameters go inline (others: no-op)
-    stream = inline_acff(text, synth_darknet_weights(text, calib=calib), synth_acff_params(text, calib=calib))
+    stream = inline_acff(text, synth_darknet_weights(text, calib=calib, preset=preset),
+                         synth_acff_params(text, calib=calib, preset=preset))
     m.load_weight_stream(stream)
     if half:
         m.half()
@@ -282,6 +283,63 @@ def test_detector_golden_full(dev, det_golden, case, half):
             bar = min(0.9, rate(emu[b]) - 0.05)
         print(case, "half" if half else "fp32", "detection match", round(got_rate, 3), "bar", round(bar, 3))
         assert got_rate >= bar, (case, got_rate, bar)
+
+
+COND_CASES = ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416", "yolov3-spp-aider@608", "yolov3-tiny-aider-416@416",
+              "yolov4-tiny-swish@416", "yolov4-tiny-3l-512x512@512", "yolov3-acffx@416"]
+
+
+@pytest.mark.parametrize("case", COND_CASES)
+def test_detector_cond_weights_survey_bars(dev, case):
+    """SURVEY §8d's detector bars, as written, on the well-conditioned synthetic weights
+    (rtdm.synth COND; the reference ships no detector weights):
+      fp32: io x,y <= 1e-3 px, w,h <= 1e-3 px + 1e-5 relative, probabilities <= 1e-4 (deep
+            nets: 2e-3 px / 1e-4 relative / 1e-4), NMS survivors identical;
+      fp16: every io box coordinate within 0.5 px of the fp32 oracle (x, y, w and h), and
+            the NMS survivor sets (conf 0.3 / IoU 0.4) equal after excluding the candidates
+            within 1e-3 of the thresholds (oracle.nms.survivors_equal_outside_band).
+    4 frames per cfg (8 for the 608 detector of record); the oracle runs fp32 on the host
+    and is itself pinned to the reference Darknet on these weights by
+    test_oracle_golden.py::test_darknet_oracle_matches_reference_goldens_cond."""
+    from oracle import nms as ON
+    from oracle.darknet import DarknetRef
+    from conftest import load_npz
+    from rtdm.synth import BASE_SEED, load_calibration, synth_acff_params, synth_darknet_weights, synth_frames
+    cfg, size = case.split("@")
+    size = int(size)
+    nf = 8 if case == "yolov4-tiny-aider-416@608" else 4
+    frames = synth_frames(nf, size, size, seed=BASE_SEED + 700)
+    text = cfg_text(cfg)
+    cal = load_calibration(cfg, "cond")
+    torch.set_num_threads(16)
+    ref = DarknetRef(text, synth_darknet_weights(text, calib=cal, preset="cond"),
+                     synth_acff_params(text, calib=cal, preset="cond"))
+    io32 = ref.forward(torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0).numpy()
+    g = load_npz("det_golden_cond.npz")
+    # the oracle on this host vs the reference's rows (bit-exact in the build container;
+    # another CPU's conv kernels round differently in the last bits)
+    dg = np.abs(io32[:2, ::53] - g[f"{case}/io_rows"])
+    assert dg[..., :4].max() <= 1e-3 + 1e-4 * np.abs(g[f"{case}/io_rows"][..., :4]).max() and dg[..., 4:].max() <= 1e-4
+    deep = not cfg.startswith(("yolov4-tiny", "yolov3-tiny"))
+    x = torch.from_numpy(frames).to(dev)
+    m32, _, _ = _darknet(cfg, size, False, "cond")
+    io = m32(x)[0].cpu().numpy()
+    d = np.abs(io - io32)
+    xy_t, wh_r, p_t = (2e-3, 1e-4, 1e-4) if deep else (1e-3, 1e-5, 1e-4)
+    assert d[..., :2].max() <= xy_t, d[..., :2].max()
+    assert (d[..., 2:4] <= 1e-3 + wh_r * np.abs(io32[..., 2:4])).all(), d[..., 2:4].max()
+    assert d[..., 4:].max() <= p_t, d[..., 4:].max()
+    nr, ng, ne, bad = ON.survivors_equal_outside_band(io32, io, 0.3, 0.4, 1e-5)
+    assert not bad and nr == ng, ("fp32 survivors", nr, ng, bad[:5])
+    m16, _, _ = _darknet(cfg, size, True, "cond")
+    io = m16(x)[0].cpu().numpy()
+    d = np.abs(io - io32)
+    print(case, "fp16 max |d| px: xy", d[..., :2].max(), "wh", d[..., 2:4].max(), "p", d[..., 4:].max())
+    assert d[..., :4].max() <= 0.5, (d[..., :2].max(), d[..., 2:4].max())
+    nr, ng, ne, bad = ON.survivors_equal_outside_band(io32, io, 0.3, 0.4)
+    print(case, f"fp16 survivors ref {nr} hip {ng}, differences inside the 1e-3 band {ne}")
+    assert not bad, bad[:10]
+    assert nr > 0
 
 
 @pytest.mark.parametrize("cfg,size", [("yolov4-tiny-aider-416", 608), ("yolov4-tiny-aider-416", 256),

@@ -1,27 +1,29 @@
-"""GPU parity of the exact configuration bench.py reports (BASELINE.json config 4 at
-N=1 and, per rank, at N=8) and of the fp16 detectors against an fp16-storage bound.
+"""GPU parity of the exact configurations bench.py reports (BASELINE.json config 4 at N=1
+and, per rank, at N=8; config 5 in int8) and of the fp16 detectors against an fp16-storage
+bound.
 
 Bench configuration: TwoStagePipeline(ErNET with the reference's trained weights, fp16;
-yolov4-tiny-aider-416.cfg at 608x608, fp16; NMS conf 0.3 / IoU 0.4 / max_det 300) on
-synthetic 608x608 frames.  Checked here:
+yolov4-tiny-aider-416.cfg at 608x608, fp16, the well-conditioned synthetic weights
+rtdm.synth COND; NMS conf 0.3 / IoU 0.4 / max_det 300) on synthetic 608x608 frames
+(SURVEY.md §8d).  Checked here:
   * b64 (N=1), b8 (the per-rank shard at N=8) and b1 rows are BIT-IDENTICAL: every kernel
     computes a frame's outputs in the same order whatever the batch, so a frame's
     result does not depend on the rank count or on which frames share its batch;
   * the hipGraph replay bench.py times is bit-identical to the eager launches;
   * against the oracle (aider-predict.py:76 + detect.py:87-91 restated): class id exact
-    where the oracle's top-2 logit gap >= 0.5, logits <= 2e-2 * max|logit|; every io row
-    within the fp16 bars below; NMS survivors and their (anchor, class) indices bit-exact
-    against the oracle NMS run on the device io, for all 64 frames.
+    where the oracle's top-2 logit gap >= 0.5, logits <= 2e-2 * max|logit|; SURVEY §8d's
+    fp16 box bar (every io box coordinate within 0.5 px of fp32) and survivor rule (equal
+    NMS survivor sets outside the 1e-3 threshold band); NMS survivors and their (anchor,
+    class) indices bit-exact against the oracle NMS run on the device io, all 64 frames.
+The int8 twin (config 5): int8 ErNET + int8 detector at b128 and as b16 shards (N=8), graph
+replay and two batches in flight, rows bit-identical; >= 97 % detection match and >= 99 %
+top-1 agreement against fp32.
 
-fp16 bars (SURVEY.md §8d says boxes <= 0.5 px; that is below what fp16 STORAGE alone
-allows once exp() decodes w,h): the oracle's f16_storage mode (every activation and
-weight rounded to fp16, fp32 arithmetic) measures the floor on the same frames, and
-the HIP fp16 io must stay within 2x that floor (+ a small absolute slack) for xy, the
-relative w,h error and the probabilities -- max and 99th percentile.  Measured floors
-(this container, 1-2 frames): v4-tiny@608 xy 0.11 px, wh 1.8 % rel, p 5.3e-3;
-yolov3-aider@416 xy 1.16 px, wh 13.7 %, p 2.9e-2; yolov3-spp@608 xy 1.38 px, wh 17.4 %,
-p 4.3e-2.  The deep nets' looser io bars in test_gpu_parity.py (2 px / 20 % / 5e-2)
-are ~1.5x these floors.
+The mean-field "he" detector weights stay as the fp16 stress case
+(test_fp16_io_within_storage_floor): there the oracle's f16_storage mode (every activation
+and weight rounded to fp16, fp32 arithmetic) measures the floor on the same frames and the
+HIP fp16 io must stay within 2x it (+ a small slack) -- floors v4-tiny@608 xy 0.11 px, wh
+1.8 % rel; yolov3-aider@416 xy 1.16 px, wh 13.7 %; yolov3-spp@608 xy 1.38 px, wh 17.4 %.
 """
 import numpy as np
 import pytest
@@ -40,26 +42,32 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _detector(cfg, size, half=True):
+def _detector(cfg, size, half=True, preset="he"):
     from rtdm.darknet import Darknet
     from rtdm.synth import inline_acff, load_calibration, synth_acff_params, synth_darknet_weights
     text = cfg_text(cfg)
     m = Darknet(text, (size, size))
-    calib = load_calibration(cfg)
-    conv, acff = synth_darknet_weights(text, calib=calib), synth_acff_params(text, calib=calib)
+    calib = load_calibration(cfg, preset)
+    conv = synth_darknet_weights(text, calib=calib, preset=preset)
+    acff = synth_acff_params(text, calib=calib, preset=preset)
     m.load_weight_stream(inline_acff(text, conv, acff))
     if half:
         m.half()
     return m, text, conv, acff
 
 
-def _pipeline(cls_weights, graphs=False, overlap=True):
+def _pipeline(cls_weights, graphs=False, overlap=True, calib=None):
+    """bench.py's pipeline: fp16, or int8 (both stages) calibrated on `calib` frames."""
     from rtdm.classifier import build_model
     from rtdm.pipeline import TwoStagePipeline
     cls = build_model("ernet")
     cls.load_state_dict(cls_weights["ernet"])
-    cls.half()
-    det, text, conv, acff = _detector(CFG, IMG)
+    det, text, conv, acff = _detector(CFG, IMG, half=calib is None, preset="cond")
+    if calib is None:
+        cls.half()
+    else:
+        cls.int8(calib)
+        det.int8(calib)
     return TwoStagePipeline(cls, det, 0.3, 0.4, max_det=300, graphs=graphs, overlap=overlap), text, conv, acff
 
 
@@ -148,14 +156,18 @@ def test_bench_config_batches_graph_and_oracle(dev, cls_weights):
     srt = np.sort(ref_logits, 1)
     sure = srt[:, -1] - srt[:, -2] >= 0.5
     assert np.array_equal(got.argmax(1)[sure], ref_logits.argmax(1)[sure])
-    # oracle: every io row of 4 frames, fp32 and the fp16-storage floor ---------------
+    # oracle: every io row of 8 frames: SURVEY §8d's 0.5 px boxes and survivor rule --------
+    torch.set_num_threads(16)
     ref = DarknetRef(text, conv, acff)
-    sub = [0, 21, 42, 63]
+    sub = [0, 9, 18, 27, 36, 45, 54, 63]
     xin = torch.from_numpy(frames[sub]).permute(0, 3, 1, 2).float() / 255.0
     io32 = ref.forward(xin).numpy()
-    io16 = ref.forward(xin, f16_storage=True).numpy()
-    got_s, floor_s = _io_vs_floor(b64["io"][sub].numpy(), io32, io16, "bench config io")
-    print("bench io max/p99 (xy px, wh rel, p):", got_s, "fp16-storage floor:", floor_s)
+    d = np.abs(b64["io"][sub].numpy() - io32)
+    print("bench config fp16 io max |d|: xy", d[..., :2].max(), "wh", d[..., 2:4].max(), "p", d[..., 4:].max())
+    assert d[..., :4].max() <= 0.5, (d[..., :2].max(), d[..., 2:4].max())
+    nr, ng, ne, bad = ON.survivors_equal_outside_band(io32, b64["io"][sub].numpy(), 0.3, 0.4)
+    print(f"bench config survivors: oracle {nr}, HIP {ng}, differences inside the band {ne}")
+    assert not bad, bad[:10]
     # NMS on the device io: bit-exact survivors + indices for all 64 frames ------------
     io = b64["io"].numpy()
     rows, idx = ON.non_max_suppression(io, 0.3, 0.4, return_index=True)
@@ -166,6 +178,101 @@ def test_bench_config_batches_graph_and_oracle(dev, cls_weights):
         k = min(len(r), 300)
         assert np.array_equal(b64["det"][b, :k].numpy(), r[:k]), b
         assert np.array_equal(b64["idx"][b, :k].numpy(), (np.zeros((0, 2)) if idx[b] is None else idx[b])[:k]), b
+
+
+def test_int8_bench_config_batches_graph_and_oracle(dev, cls_weights):
+    """BASELINE config 5 as bench.py --dtype i8 runs it: int8 ErNET + int8 yolov4-tiny@608
+    (calibrated on 16 disjoint frames) through TwoStagePipeline at b128, as the eight b16
+    shards of N=8, at b1, under graph replay and with two batches in flight: rows
+    bit-identical; against fp32 (the oracle): detection match >= 97 % (same class, IoU >=
+    0.9, fp32 survivors above conf 0.32) on 16 frames, classifier top-1 agreement >= 99 % on
+    the non-tied frames of all 128; NMS survivors bit-exact with the oracle NMS on the
+    device io."""
+    from oracle import classifier as OC
+    from oracle import nms as ON
+    from oracle import preprocess as OP
+    from oracle.darknet import DarknetRef
+    from rtdm.synth import BASE_SEED, synth_frames
+    from test_gpu_int8 import _match
+    frames = synth_frames(128, IMG, IMG, first=0)
+    x = torch.from_numpy(frames).to(dev)
+    calib = torch.from_numpy(synth_frames(16, IMG, IMG, seed=BASE_SEED + 4321)).to(dev)
+    pipe, text, conv, acff = _pipeline(cls_weights, calib=calib)
+    assert " dtype i8 " in pipe.detector.describe()
+    b128 = _host(pipe(x))
+    torch.cuda.synchronize()
+    for r in range(8):  # the per-rank shards of N = 8 (16 frames per GPU)
+        _same(_host(pipe(x[16 * r:16 * r + 16].contiguous())), _host(b128, slice(16 * r, 16 * r + 16)), f"b16 {r}")
+    p1, _, _, _ = _pipeline(cls_weights, calib=calib)
+    for i in (0, 77, 127):
+        _same(_host(p1(x[i:i + 1].contiguous())), _host(b128, slice(i, i + 1)), f"b1 frame {i}")
+    pg, _, _, _ = _pipeline(cls_weights, graphs=True, calib=calib)
+    for _ in range(2):
+        g = _host(pg(x))
+    _same(g, b128, "graph replay b128")
+    _same(_host(pg(x[16:32].contiguous())), _host(b128, slice(16, 32)), "graph replay b16")
+    from rtdm import _lib as L
+    L.check(L.lib().rtdm_set_tuning(b"two_streams", 0))
+    try:
+        ps = [_pipeline(cls_weights, graphs=True, overlap=False, calib=calib)[0] for _ in range(2)]
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"two_streams", 1))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for rep in range(2):
+        outs = []
+        for j in range(2):
+            with torch.cuda.stream(streams[j]):
+                outs.append(ps[j](x[64 * j:64 * j + 64].contiguous()))
+        torch.cuda.synchronize()
+    for j in range(2):
+        _same(_host(outs[j]), _host(b128, slice(64 * j, 64 * j + 64)), f"in-flight batch {j}")
+    # classifier: top-1 agreement with the fp32 oracle ---------------------------------
+    torch.set_num_threads(16)
+    xc = torch.from_numpy(np.stack([OP.cli_transform(f, 240) for f in frames]))
+    ref_logits = OC.forward("ernet", cls_weights["ernet"], xc)[0].numpy()
+    got = b128["logits"].numpy()
+    top2 = np.sort(ref_logits, 1)[:, -2:]
+    sure = (top2[:, 1] - top2[:, 0]) > 0.05 * np.abs(ref_logits).max(1)
+    agree = float((got.argmax(1) == ref_logits.argmax(1))[sure].mean())
+    print(f"int8 ErNET top-1 agreement {agree:.4f} on {int(sure.sum())}/128 non-tied frames")
+    assert agree >= 0.99
+    # detector: detection match against fp32 on 16 frames ------------------------------
+    sub = list(range(0, 128, 8))
+    io32 = DarknetRef(text, conv, acff).forward(
+        torch.from_numpy(frames[sub]).permute(0, 3, 1, 2).float() / 255.0).numpy()
+    m, t = _match(io32, b128["io"][sub].numpy())
+    print(f"int8 pipeline detection match {m}/{t}")
+    assert t >= 40 and m / t >= 0.97, (m, t)
+    # NMS on the device io: bit-exact survivors + indices, all 128 frames ---------------
+    io = b128["io"].numpy()
+    rows, idx = ON.non_max_suppression(io, 0.3, 0.4, return_index=True)
+    cnt = b128["count"].numpy()
+    for b in range(128):
+        r = np.zeros((0, 6), np.float32) if rows[b] is None else rows[b]
+        assert cnt[b] == len(r), (b, cnt[b], len(r))
+        k = min(len(r), 300)
+        assert np.array_equal(b128["det"][b, :k].numpy(), r[:k]), b
+        assert np.array_equal(b128["idx"][b, :k].numpy(), (np.zeros((0, 2)) if idx[b] is None else idx[b])[:k]), b
+
+
+def test_graph_cache_follows_handle_changes(dev, cls_weights):
+    """graphs are keyed on the handles' generation, not their addresses.  b64,
+    then b128 (recreates both handles), then b64 again with graphs on: each result equals
+    the eager pipeline's."""
+    from rtdm.synth import synth_frames
+    x = torch.from_numpy(synth_frames(128, IMG, IMG, first=0)).to(dev)
+    pe, _, _, _ = _pipeline(cls_weights)
+    want64, want128 = _host(pe(x[:64].contiguous())), None
+    want128 = _host(pe(x))
+    pg, _, _, _ = _pipeline(cls_weights, graphs=True)
+    x64 = x[:64].contiguous()
+    for _ in range(2):
+        _same(_host(pg(x64)), want64, "graph b64")
+    gen = pg.detector.handle_generation
+    _same(_host(pg(x)), want128, "graph b128")
+    assert pg.detector.handle_generation > gen
+    _same(_host(pg(x64)), want64, "graph b64 after the handle changed")
+    assert len(pg._graphs) <= pg.max_graphs
 
 
 @pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416", "yolov3-spp-aider@608",

@@ -68,6 +68,40 @@ def test_darknet_oracle_matches_reference_goldens(det_golden):
             assert np.array_equal(io, det_golden[f"{case}/io"])
 
 
+def test_darknet_oracle_matches_reference_goldens_cond():
+    """The well-conditioned weight set (rtdm.synth COND, the set SURVEY §8d's fp16 / int8 bars
+    are asserted on): the oracle io and NMS survivors against the reference Darknet's on the
+    same weights (det_golden_cond.npz, all 8 cases, 2 frames each)."""
+    import hashlib
+    from conftest import load_npz
+    from oracle import nms as ON
+    from oracle.darknet import DarknetRef
+    from rtdm.synth import BASE_SEED, load_calibration, synth_acff_params, synth_darknet_weights, synth_frames
+    g = load_npz("det_golden_cond.npz")
+    cases = sorted({k.split("/")[0] for k in g})
+    assert len(cases) == 8, cases
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    for case in cases:
+        cfg, size = case.split("@")
+        size = int(size)
+        text = cfg_text(cfg)
+        cal = load_calibration(cfg, "cond")
+        stream = synth_darknet_weights(text, calib=cal, preset="cond")
+        assert hashlib.sha256(stream.tobytes()).hexdigest() == str(g[f"{case}/stream_sha"]), case
+        n = int(g[f"{case}/io_shape"][0])
+        frames = synth_frames(n, size, size, seed=BASE_SEED + 700)
+        io = DarknetRef(text, stream, synth_acff_params(text, calib=cal, preset="cond")).forward(
+            torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0).numpy()
+        assert np.array_equal(io[:, ::53], g[f"{case}/io_rows"]), case
+        if f"{case}/io" in g:
+            assert np.array_equal(io, g[f"{case}/io"])
+        out = ON.non_max_suppression(io, 0.3, 0.4)
+        for b in range(n):
+            ref = g[f"{case}/nms0.3_0.4/{b}"]
+            got = np.zeros((0, 6), np.float32) if out[b] is None else out[b]
+            assert np.array_equal(got, ref), (case, b)
+
+
 def test_nms_oracle_matches_reference_goldens(det_golden):
     """The reference non_max_suppression wrapper (filters, multi-label expansion,
     class offsets, output rows) with the oracle torchvision kernel stubbed in."""
