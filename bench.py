@@ -62,7 +62,9 @@ def parse():
     ap.add_argument("--per-gpu-batch", type=int, default=0,
                     help="> 0: frames per GPU per step instead (weak scaling; global = this * N)")
     ap.add_argument("--img", type=int, default=608)
-    ap.add_argument("--cfg", default="yolov4-tiny-aider-416")
+    ap.add_argument("--cfg", default="yolov4-tiny-aider-416",
+                    help="detector cfg; none: classification only (BASELINE config 2: --classifier squeeze-redconv "
+                         "--cfg none --img 224 --batch 32)")
     ap.add_argument("--weights", default="cond", choices=["cond", "he"],
                     help="synthetic detector weight set (rtdm.synth): cond = the well-conditioned set the "
                          "SURVEY §8d bars are asserted on; he = the mean-field stress set")
@@ -126,26 +128,32 @@ def build(args, world, rank):
     for kv in filter(None, os.environ.get("RTDM_TUNE", "").split(",")):  # diagnostics: "key=v,key=v"
         k, v = kv.split("=")
         L.check(L.lib().rtdm_set_tuning(k.encode(), int(v)))
-    cfg_path = os.path.join(ROOT, "real-time-disaster-management_amd", "rtdm", "cfg", args.cfg + ".cfg")
-    text = open(cfg_path).read()
-    det = Darknet(text, (args.img, args.img))
+    use_det = args.cfg != "none"
+    text = open(os.path.join(ROOT, "real-time-disaster-management_amd", "rtdm", "cfg", args.cfg + ".cfg")).read() \
+        if use_det else None
+    det = Darknet(text, (args.img, args.img)) if use_det else None
     use_cls = args.classifier != "none"
+    if not (use_det or use_cls):
+        raise SystemExit("--cfg none needs a classifier")
     cls = build_model(args.classifier) if use_cls else None
     # rank 0 makes / loads the weights; RCCL broadcast to the other ranks (once, untimed)
     if rank == 0:
-        calib = load_calibration(args.cfg, args.weights)
-        conv = synth_darknet_weights(text, calib=calib, preset=args.weights)
-        acff = synth_acff_params(text, calib=calib, preset=args.weights)
-        stream = inline_acff(text, conv, acff)  # YOLO-ACFF cfgs: [acff] params inline
-        args.ref_weights = (conv, acff)         # the CPU oracle takes them apart
+        stream = None
+        if use_det:
+            calib = load_calibration(args.cfg, args.weights)
+            conv = synth_darknet_weights(text, calib=calib, preset=args.weights)
+            acff = synth_acff_params(text, calib=calib, preset=args.weights)
+            stream = inline_acff(text, conv, acff)  # YOLO-ACFF cfgs: [acff] params inline
+            args.ref_weights = (conv, acff)         # the CPU oracle takes them apart
         sd = trained_classifier(args.classifier) if use_cls else {}
     else:
         stream, sd = None, None
     if world > 1:
         from rtdm.distributed import broadcast_array, broadcast_state_dict
-        stream = broadcast_array(stream)
+        stream = broadcast_array(stream) if use_det else None
         sd = broadcast_state_dict(sd, classifier_param_shapes(args.classifier)) if use_cls else {}
-    det.load_weight_stream(stream)
+    if use_det:
+        det.load_weight_stream(stream)
     if use_cls:
         cls.load_state_dict(sd)
     calib = None
@@ -153,18 +161,22 @@ def build(args, world, rank):
         from rtdm.synth import BASE_SEED, synth_frames
         calib = torch.from_numpy(synth_frames(16, args.img, args.img, seed=BASE_SEED + 4321)).cuda()
     if args.dtype in ("f16", "i8"):
-        det.half() if args.dtype == "f16" else det.int8(calib)
+        if use_det:
+            det.half() if args.dtype == "f16" else det.int8(calib)
         if use_cls:
             cls.half() if args.dtype == "f16" else cls.int8(calib)
     pipes = []
     for j in range(args.inflight):
         if j:  # another instance: own device weights, arenas, buffers and streams
-            det, cls = Darknet(text, (args.img, args.img)), (build_model(args.classifier) if use_cls else None)
-            det.load_weight_stream(stream)
+            det = Darknet(text, (args.img, args.img)) if use_det else None
+            cls = build_model(args.classifier) if use_cls else None
+            if use_det:
+                det.load_weight_stream(stream)
             if use_cls:
                 cls.load_state_dict(sd)
             if args.dtype in ("f16", "i8"):
-                det.half() if args.dtype == "f16" else det.int8(calib)
+                if use_det:
+                    det.half() if args.dtype == "f16" else det.int8(calib)
                 if use_cls:
                     cls.half() if args.dtype == "f16" else cls.int8(calib)
         pipes.append(TwoStagePipeline(cls, det, args.conf, args.iou, args.max_det, overlap=bool(args.overlap),
@@ -229,7 +241,7 @@ def cpu_baseline(args, text, stream, sd):
     cores = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
     torch.set_num_threads(cores)
     conv, acff = getattr(args, "ref_weights", (stream, {}))
-    ref = DarknetRef(text, conv, acff)
+    ref = DarknetRef(text, conv, acff) if text is not None else None
     s = 240 if args.classifier == "ernet" else 140
     sdt = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in sd.items()}
 
@@ -238,12 +250,14 @@ def cpu_baseline(args, text, stream, sd):
             if args.classifier != "none":
                 x = torch.from_numpy(np.stack([OP.cli_transform(f, s) for f in frames]))
                 OC.forward(args.classifier, sdt, x)
+            if ref is None:
+                return
             io = ref.forward(torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0)
         ON.non_max_suppression(io.numpy(), args.conf, args.iou)
 
     warm = synth_frames(2, args.img, args.img, seed=1)
     run(warm)
-    chunk, done, dt = 16, 0, 0.0
+    chunk, done, dt = (16 if ref is not None else 64), 0, 0.0
     while dt < args.cpu_seconds and done < 64 * 16:
         frames = synth_frames(chunk, args.img, args.img, first=done)
         t0 = time.perf_counter()
@@ -253,7 +267,46 @@ def cpu_baseline(args, text, stream, sd):
     return {"value": round(done / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
             "cpu_model": cpu_model(),
             "sample": f"first {done} frames of the same synthetic {args.img}x{args.img} workload in chunks of {chunk}, "
-                      f"fp32 torch-CPU oracle ({args.classifier} + {args.cfg} + decode + NMS), {dt:.1f} s"}
+                      f"fp32 torch-CPU oracle ("
+                      + (f"{args.classifier} + {args.cfg} + decode + NMS" if ref is not None else
+                         f"CLI transform + {args.classifier}") + f"), {dt:.1f} s"}
+
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec; 6.29 TB/s measured float4 copy)
+
+
+def classifier_roofline(args, pipe, frames, b, workload):
+    """Classification only (BASELINE config 2): the classifier is HBM- / latency-bound, so the
+    roofline is bytes: per launch of the step (preprocess, stem, ACFF stages, chain + tail)
+    its algorithmic HBM bytes (maps read + written, rtdm_classifier_read_timing) over its
+    average hipEvent time on the launch stream, eager calls after the timed region; the
+    dominant launch (largest summed time) is reported, with the whole step beside it."""
+    from rtdm import _lib as L
+    cls = pipe.classifier
+    h = cls._get_handle(b)
+    L.check(L.lib().rtdm_classifier_enable_timing(h, args.roofline_steps))
+    for k in range(args.roofline_steps):
+        pipe._launch(frames[k % len(frames)])
+    torch.cuda.synchronize()
+    ms = (ctypes.c_double * 24)()
+    byt = (ctypes.c_double * 24)()
+    names = ctypes.create_string_buffer(24 * 32)
+    nl, calls = ctypes.c_int(), ctypes.c_int()
+    L.check(L.lib().rtdm_classifier_read_timing(h, ms, byt, names, 32, ctypes.byref(nl), ctypes.byref(calls)))
+    L.check(L.lib().rtdm_classifier_enable_timing(h, 0))
+    rows = [(names.raw[32 * i:32 * i + 32].split(b"\0")[0].decode(), ms[i] / calls.value, byt[i]) for i in range(nl.value)]
+    dom = max(rows, key=lambda r: r[1])
+    ach = dom[2] / (dom[1] * 1e-3) / 1e9
+    tot_ms, tot_b = sum(r[1] for r in rows), sum(r[2] for r in rows)
+    tr = pmc_traffic(dom[0], {"workload": workload, "dtype": args.dtype, "per_gpu_batch": b})
+    return {"bound": "hbm", "kernel": dom[0], "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": round(tr["bytes_per_launch"]) if tr else None,
+            "avg_launch_ms": round(dom[1], 4), "algorithmic_bytes_per_launch": round(dom[2]),
+            "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tr["source"] if tr else None,
+            "launches": {r[0]: {"ms": round(r[1], 4), "GB/s": round(r[2] / (r[1] * 1e-3) / 1e9, 1)} for r in rows},
+            "step": {"ms": round(tot_ms, 4), "bytes": round(tot_b), "GB/s": round(tot_b / (tot_ms * 1e-3) / 1e9, 1)},
+            "timing": f"hipEvents around each classifier launch on its stream, {calls.value} eager calls after the "
+                      f"timed region"}
 
 
 def make_frames(args, first, count, dev):
@@ -328,18 +381,25 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     step_ms = [s.elapsed_time(e) for s, e in evs]
-    counts = out["count"].cpu()
-    if world > 1 and rank == 0:  # every rank's shard arrived: counts of the whole global batch
+    counts = out["count"].cpu() if det is not None else None
+    if det is not None and world > 1 and rank == 0:  # every rank's shard arrived: the global batch's counts
         from rtdm.pipeline import unpack_record
         counts = torch.cat([unpack_record(gathered[r], pipe, b)["count"].cpu() for r in range(world)])
 
     # ---- roofline: per-launch hipEvents on the detector's launch streams, eager steps ----
-    workload = ((f"two-stage {args.classifier} -> " if args.classifier != "none" else "detection only: ")
-                + f"{args.cfg}@{args.img} + decode + NMS (conf {args.conf}, iou {args.iou})")
+    if det is None:
+        workload = (f"classification only: {args.classifier} on {args.img}x{args.img} uint8 frames "
+                    f"(CLI transform on device)")
+    else:
+        workload = ((f"two-stage {args.classifier} -> " if args.classifier != "none" else "detection only: ")
+                    + f"{args.cfg}@{args.img} + decode + NMS (conf {args.conf}, iou {args.iou})")
     from rtdm import _lib as L
-    h, steps = step_table(det, b)
     rl = None
-    if args.roofline_steps > 0:
+    if det is None and args.roofline_steps > 0:
+        rl = classifier_roofline(args, pipe, frames, b, workload)
+    if det is not None:
+        h, steps = step_table(det, b)
+    if det is not None and args.roofline_steps > 0:
         L.check(L.lib().rtdm_detector_enable_timing(h, args.roofline_steps))
         for k in range(args.roofline_steps):
             pipe._launch(frames[k % len(frames)])
@@ -388,24 +448,26 @@ def main():
             with open(os.path.join(outdir, "bench_steps.json"), "w") as f:
                 json.dump(per_step, f, indent=1)
 
-    # ---- PCIe-inclusive variant: frames uploaded from pinned host memory each step ----
+    # ---- PCIe-inclusive variant: frames uploaded from pinned host memory each step, on a copy
+    #      stream into double-buffered device inputs (rtdm.pipeline.FrameUploader), so batch
+    #      k+1's upload overlaps batch k's compute ----
     h2d = None
     if args.h2d_steps > 0:
+        from rtdm.pipeline import FrameUploader
         host = [f.cpu().pin_memory() for f in frames]
-        dst = torch.empty_like(frames[0])
-        for k in range(2):
-            dst.copy_(host[k % len(host)], non_blocking=True)
-            pipe(dst)
+        up = FrameUploader(pipes, streams, dev)
+        for k in range(2 * len(pipes)):  # each pipeline's two buffers: capture their graphs
+            up.submit(k, host[k % len(host)])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for k in range(args.h2d_steps):
-            dst.copy_(host[k % len(host)], non_blocking=True)
-            o2 = pipe(dst)
+            o2 = up.submit(k, host[k % len(host)])
             if world > 1:
-                gather_records(o2["record"], gathered if rank == 0 else None)
+                with torch.cuda.stream(streams[k % len(pipes)]):
+                    gather_records(o2["record"], gathered if rank == 0 else None)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -416,10 +478,12 @@ def main():
             e2 = float(t.item())
         h2d = {"value": round(global_batch * args.h2d_steps / e2, 2), "unit": "frames/s",
                "bytes_per_frame": args.img * args.img * 3, "steps": args.h2d_steps,
-               "note": "uint8 frames copied host(pinned)->HBM on the step's stream before each step"}
+               "pcie_GBps": round(global_batch * args.h2d_steps * args.img * args.img * 3 / e2 / 1e9, 2),
+               "note": "uint8 frames copied host(pinned)->HBM on a copy stream, double-buffered per in-flight "
+                       "pipeline (rtdm.pipeline.FrameUploader): uploads overlap compute"}
 
     value = global_batch * args.steps / elapsed
-    pipe_flop = det.flop_per_image + CLASSIFIER_FLOP[args.classifier]
+    pipe_flop = (det.flop_per_image if det is not None else 0.0) + CLASSIFIER_FLOP[args.classifier]
     rec = {
         "metric": METRIC,
         "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
@@ -439,7 +503,7 @@ def main():
         "pipeline": {"flop_per_frame": pipe_flop,
                      "pipeline_tflops": round(pipe_flop * value / world / 1e12, 2),
                      "pipeline_frac": round(pipe_flop * value / world / 1e12 / MFMA_F16_DENSE_PEAK_TFLOPS, 4),
-                     "detections_per_frame": round(float(counts.float().mean()), 2)},
+                     "detections_per_frame": round(float(counts.float().mean()), 2) if counts is not None else None},
         "h2d": h2d,
     }
     if rank == 0 and world == 1 and args.cpu_baseline:

@@ -142,6 +142,16 @@ rtdm_status rtdm_classifier_create(int kind, int dtype, const rtdm_param* params
                                    int max_batch, rtdm_classifier* out);
 rtdm_status rtdm_classifier_destroy(rtdm_classifier h);
 /* Input side length the model expects (140 or 240). */
+/* Per-launch timing of rtdm_classify (bench / roofline): hipEvents recorded on the call's
+ * stream around each kernel launch of the next max_calls calls (0 turns it off).  read:
+ * summed ms per launch over the timed calls, the launch's algorithmic HBM bytes (model
+ * input / activation maps read + written, for the batch of the first timed call), its
+ * name (preprocess, stem, acff<k>, acff_chain, tail) at names + i * name_stride, the
+ * launch count and the timed call count.  Arrays hold >= 24 entries.  Replaces the
+ * reference's per-batch wall-clock timing (evaluate-classification-metrics.py:75-79). */
+rtdm_status rtdm_classifier_enable_timing(rtdm_classifier h, int max_calls);
+rtdm_status rtdm_classifier_read_timing(rtdm_classifier h, double* ms_per_launch, double* bytes_per_launch,
+                                        char* names, int name_stride, int* n_launches, int* calls);
 int rtdm_classifier_input_size(rtdm_classifier h);
 /* Human-readable plan: one line per ACFF block (geometry, kernel, pool, reducer,
  * int8); returns bytes needed including the NUL when buf is too small.            */

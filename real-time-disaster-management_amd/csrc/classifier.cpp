@@ -8,6 +8,7 @@
 //   -> tail (1x1 ->5, AvgPool 5, NCHW flatten, Linear, Softmax).
 // RedConv's conv_red1 is folded into the stem (linear o linear); conv_red2
 // absorbs acff2's BN affine.
+#include <cstdio>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -71,6 +72,17 @@ struct rtdm_classifier_s {
   bool int8 = false, calibrated = false, calibrating = false;
   rtdm::DevBuf amax;
   int q_channels = 0;
+  // optional per-launch timing (rtdm_classifier_enable_timing): events[call][2 * seg + {0,1}]
+  // around each launch of rtdm_classify; names / algorithmic HBM bytes of the launches
+  static constexpr int kMaxSeg = 24;
+  bool timing = false;
+  int timing_cap = 0, timing_calls = 0, n_seg = 0, seg_n = 0;
+  std::vector<hipEvent_t> events;
+  std::vector<std::string> seg_name;
+  std::vector<double> seg_bytes;
+  ~rtdm_classifier_s() {
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
+  }
 };
 
 namespace rtdm {
@@ -351,6 +363,32 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
   if (n == 0) return;
   RTDM_REQUIRE(x, RTDM_E_INVALID, "classify: NULL input");
   const size_t es = esize(h.dtype);
+  // per-launch timing: seg(name, bytes) before a launch, seg_end() after it
+  hipEvent_t* ev = nullptr;
+  int si = 0;
+  if (h.timing && !h.calibrating && h.timing_calls < h.timing_cap) {
+    ev = &h.events[(size_t)h.timing_calls * 2 * rtdm_classifier_s::kMaxSeg];
+    if (h.timing_calls == 0) {
+      h.seg_name.clear();
+      h.seg_bytes.clear();
+    }
+    ++h.timing_calls;
+  }
+  auto seg = [&](const std::string& name, double bytes) {
+    if (!ev) return;
+    RTDM_REQUIRE(si < rtdm_classifier_s::kMaxSeg, RTDM_E_INVALID, "classify timing: too many launches");
+    if (h.timing_calls == 1) {
+      h.seg_name.push_back(name);
+      h.seg_bytes.push_back(bytes);
+    }
+    RTDM_HIP(hipEventRecord(ev[2 * si], s));
+  };
+  auto seg_end = [&]() {
+    if (!ev) return;
+    RTDM_HIP(hipEventRecord(ev[2 * si + 1], s));
+    h.n_seg = ++si;
+  };
+  const double nb = (double)n;
   char* base = h.arena.as<char>();
   auto buf = [&](size_t off) { return (void*)(base + off * es * h.max_batch); };
   const int S = h.S;
@@ -371,7 +409,10 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       h.resize_tmp.alloc(need);
       h.resize_tmp_bytes = need;
     }
+    // bytes: the frames in, the S x S x 3 model input out
+    seg("preprocess", nb * ((double)in_h * in_w * 3 + (double)S * S * 3 * es));
     launch_preprocess(rp, (const uint8_t*)x, n, h.resize_tmp.as<uint8_t>(), buf(h.x0_buf), 0, h.dtype, s);
+    seg_end();
     a.in = buf(h.x0_buf);
     a.in_kind = IN_NHWC;
     a.in_cs = 3;
@@ -403,7 +444,10 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
   a.w_stem = h.blob.at<void>(h.stem.stem_off);
   a.e.bias = h.blob.at<float>(h.stem.b_off);
   a.e.full = View{buf(h.stem_buf), h.stem_cout, 0};
+  seg("stem", nb * ((double)S * S * 3 * (x_kind == RTDM_INPUT_NCHW_F32 ? 4 : es) +
+                    (double)h.stem_oh * h.stem_oh * h.stem_cout * es));
   launch_conv(a, h.dtype, s);
+  seg_end();
 
   View cur{buf(h.stem_buf), h.stem_cout, 0};
   const bool chain = h.chain_start >= 0 && acff_chain_mode();
@@ -429,6 +473,9 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       const bool pool_here = st.pool && !st.red_pool;
       void* dst = st.red && st.red_pool ? buf(st.mid_buf) : buf(st.out_buf);
       AcffI8 qa;
+      // bytes: the stage input map in, its (pooled) output out
+      seg("acff" + std::to_string(si + 1),
+          nb * ((double)st.h * st.w * st.cin + (double)(pool_here ? (lim / 2) * (lim / 2) : lim * lim) * st.cout) * es);
       if (st.persist_cc && (acff_persist_mode() || st.q8))
         launch_acff_persist(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_wt),
                             h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pwc_off), st.cout, st.pw.cout_pad,
@@ -438,6 +485,7 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       launch_acff_fused(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_wt),
                         h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pw.w_off), st.pw.kpad, st.cout, st.pw.cout_pad,
                         h.blob.at<float>(st.pw.b_off), sc, sh, 0.01f, dst, st.cout, pool_here ? 1 : 0, s);
+      seg_end();
       if (st.red && st.red_pool) {
         ConvArgs r;
         r.in = buf(st.mid_buf);
@@ -456,7 +504,9 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
         r.w_f32 = st.redw.mfma ? 0 : 1;
         r.e.bias = h.blob.at<float>(st.redw.b_off);
         r.e.pool = View{buf(st.red_buf), st.redw.cout, 0};
+        seg("conv_red", nb * ((double)r.ih * r.iw * r.cin + (double)(r.e.pool.ptr ? (r.oh / 2) * (r.ow / 2) : r.oh * r.ow) * r.cout) * es);
         launch_conv(r, h.dtype, s);
+        seg_end();
         cur = View{buf(st.red_buf), st.redw.cout, 0};
         continue;
       }
@@ -478,7 +528,9 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
         r.w_f32 = st.redw.mfma ? 0 : 1;
         r.e.bias = h.blob.at<float>(st.redw.b_off);
         r.e.full = View{buf(st.red_buf), st.redw.cout, 0};
+        seg("conv_red", nb * ((double)r.ih * r.iw * r.cin + (double)(r.e.pool.ptr ? (r.oh / 2) * (r.ow / 2) : r.oh * r.ow) * r.cout) * es);
         launch_conv(r, h.dtype, s);
+        seg_end();
         cur = View{buf(st.red_buf), st.redw.cout, 0};
       }
       continue;
@@ -531,7 +583,9 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       r.w_f32 = st.redw.mfma ? 0 : 1;
       r.e.bias = h.blob.at<float>(st.redw.b_off);
       r.e.pool = View{buf(st.red_buf), st.redw.cout, 0};
+      seg("conv_red", nb * ((double)r.ih * r.iw * r.cin + (double)(r.e.pool.ptr ? (r.oh / 2) * (r.ow / 2) : r.oh * r.ow) * r.cout) * es);
       launch_conv(r, h.dtype, s);
+      seg_end();
       cur = View{buf(st.red_buf), st.redw.cout, 0};
       continue;
     }
@@ -560,7 +614,9 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       r.w_f32 = st.redw.mfma ? 0 : 1;
       r.e.bias = h.blob.at<float>(st.redw.b_off);
       r.e.full = View{buf(st.red_buf), st.redw.cout, 0};
+      seg("conv_red", nb * ((double)r.ih * r.iw * r.cin + (double)(r.e.pool.ptr ? (r.oh / 2) * (r.ow / 2) : r.oh * r.ow) * r.cout) * es);
       launch_conv(r, h.dtype, s);
+      seg_end();
       cur = View{buf(st.red_buf), st.redw.cout, 0};
     }
   }
@@ -584,13 +640,20 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       sh[i] = h.blob.at<float>(st.pw.t_off);
       any_q = q8(st, qs[i]) != nullptr || any_q;
     }
+    {
+      const AcffStage& st0 = h.stages[h.chain_start];
+      seg("acff_chain", nb * ((double)st0.h * st0.w * st0.cin * es + 2.0 * 5 * 4));
+    }
     launch_acff_chain(h.chain, cur.ptr, cur.cs, cur.co, n, dw_wt, dw_b, pw, bias, sc, sh, 0.01f,
                       h.blob.at<float>(h.tail_w2), h.tail_pool_pad, h.tail_ph, h.tail_pw, h.blob.at<float>(h.tail_fcw),
                       h.blob.at<float>(h.tail_fcb), logits, probs, s, any_q ? qs : nullptr);
+    seg_end();
     return;
   }
+  seg("tail", nb * ((double)h.tail_h * h.tail_h * h.tail_c * es + 2.0 * 5 * 4));
   launch_cls_tail(cur.ptr, n, h.tail_h, h.tail_h, h.tail_c, h.blob.at<float>(h.tail_w2), h.tail_pool_pad, h.tail_ph,
                   h.tail_pw, h.blob.at<float>(h.tail_fcw), h.blob.at<float>(h.tail_fcb), logits, probs, h.dtype, s);
+  seg_end();
 }
 
 }  // namespace rtdm
@@ -624,6 +687,47 @@ rtdm_status rtdm_classifier_create(int kind, int dtype, const rtdm_param* params
 
 rtdm_status rtdm_classifier_destroy(rtdm_classifier h) {
   return guard([&] { delete h; });
+}
+
+rtdm_status rtdm_classifier_enable_timing(rtdm_classifier h, int max_calls) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "classifier_enable_timing: NULL handle");
+    for (hipEvent_t e : h->events) (void)hipEventDestroy(e);
+    h->events.clear();
+    h->timing = max_calls > 0;
+    h->timing_cap = max_calls > 0 ? max_calls : 0;
+    h->timing_calls = 0;
+    h->n_seg = 0;
+    const size_t ne = (size_t)h->timing_cap * 2 * rtdm_classifier_s::kMaxSeg;
+    h->events.resize(ne);
+    for (size_t i = 0; i < ne; ++i) RTDM_HIP(hipEventCreateWithFlags(&h->events[i], hipEventDisableSystemFence));
+  });
+}
+
+rtdm_status rtdm_classifier_read_timing(rtdm_classifier h, double* ms_per_launch, double* bytes_per_launch,
+                                        char* names, int name_stride, int* n_launches, int* calls) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "classifier_read_timing: NULL handle");
+    const int ns = h->timing_calls > 0 ? h->n_seg : 0;
+    for (int i = 0; i < ns; ++i) {
+      double t = 0.0;
+      for (int c = 0; c < h->timing_calls; ++c) {
+        hipEvent_t* ev = &h->events[(size_t)c * 2 * rtdm_classifier_s::kMaxSeg];
+        float ms = 0.f;
+        RTDM_HIP(hipEventSynchronize(ev[2 * i + 1]));
+        RTDM_HIP(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+        t += ms;
+      }
+      if (ms_per_launch) ms_per_launch[i] = t;
+      if (bytes_per_launch) bytes_per_launch[i] = i < (int)h->seg_bytes.size() ? h->seg_bytes[i] : 0.0;
+      if (names && name_stride > 0) {
+        const std::string& nm = i < (int)h->seg_name.size() ? h->seg_name[i] : std::string();
+        std::snprintf(names + (size_t)i * name_stride, name_stride, "%s", nm.c_str());
+      }
+    }
+    if (n_launches) *n_launches = ns;
+    if (calls) *calls = h->timing_calls;
+  });
 }
 
 int rtdm_classifier_input_size(rtdm_classifier h) { return h ? h->S : 0; }

@@ -71,6 +71,9 @@ SIGNATURES = {
     "rtdm_detector_step_info": (c_int, [c_void_p, c_int, c_char_p, c_int, POINTER(c_int), POINTER(c_double),
                                         POINTER(c_double)]),
     "rtdm_detector_enable_timing": (c_int, [c_void_p, c_int]),
+    "rtdm_classifier_enable_timing": (c_int, [c_void_p, c_int]),
+    "rtdm_classifier_read_timing": (c_int, [c_void_p, POINTER(c_double), POINTER(c_double), c_char_p, c_int,
+                                            POINTER(c_int), POINTER(c_int)]),
     "rtdm_detector_read_timing": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int)]),
     "rtdm_detect": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "rtdm_detect_raw": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),

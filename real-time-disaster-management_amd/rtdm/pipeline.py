@@ -78,8 +78,9 @@ class TwoStagePipeline:
         output (logits, probs, det, idx, count) is a contiguous slice of ONE float32 buffer,
         so a rank ships its whole result to rank 0 with a single gather (SURVEY.md §8e);
         idx and count are int32 bit patterns in that buffer."""
-        shapes = (("logits", (n, 5)), ("probs", (n, 5)), ("det", (n, self.max_det, 6)),
-                  ("idx", (n, self.max_det, 2)), ("count", (n,)))
+        shapes = (("logits", (n, 5)), ("probs", (n, 5)))
+        if self.detector is not None:  # None: classification only (BASELINE config 2)
+            shapes += (("det", (n, self.max_det, 6)), ("idx", (n, self.max_det, 2)), ("count", (n,)))
         out, o = {}, 0
         for k, s in shapes:
             out[k] = (o, s)
@@ -94,10 +95,12 @@ class TwoStagePipeline:
         b = self._bufs.get(key)
         if b is None:
             b = unpack_record(torch.empty(self.record_layout(n)[1], device=device, dtype=torch.float32), self, n)
-            b["io"] = torch.empty((n, self.detector.n_anchors, self.detector.no), device=device, dtype=torch.float32)
-            # NMS scratch of this pipeline alone: pipelines may run on several streams at once
-            b["ws"] = torch.empty(workspace_bytes(n, self.detector.n_anchors, self.detector.no - 5), device=device,
-                                  dtype=torch.uint8)
+            if self.detector is not None:
+                b["io"] = torch.empty((n, self.detector.n_anchors, self.detector.no), device=device,
+                                      dtype=torch.float32)
+                # NMS scratch of this pipeline alone: pipelines may run on several streams at once
+                b["ws"] = torch.empty(workspace_bytes(n, self.detector.n_anchors, self.detector.no - 5),
+                                      device=device, dtype=torch.uint8)
             self._bufs[key] = b
         return b
 
@@ -106,7 +109,8 @@ class TwoStagePipeline:
         return self._buffers(n, device)["record"]
 
     def __call__(self, frames: torch.Tensor, stream=None) -> dict:
-        """frames: [B,H,W,3] uint8 CUDA (H,W = detector img_size).  Returns the output views
+        """frames: [B,H,W,3] uint8 CUDA (H,W = detector img_size; any size without a
+        detector).  Returns the output views
         (logits, probs, det, idx, count, io, record), valid once `stream` reaches this point."""
         if not self.graphs:
             return self._launch(frames, stream)
@@ -143,8 +147,11 @@ class TwoStagePipeline:
         if self.classifier is not None:
             self.classifier._get_handle(n)
             gc = self.classifier.handle_generation
-        self.detector.handle(n)
-        return (n, frames.data_ptr(), tuple(frames.shape), str(frames.device), gc, self.detector.handle_generation)
+        gd = -1
+        if self.detector is not None:
+            self.detector.handle(n)
+            gd = self.detector.handle_generation
+        return (n, frames.data_ptr(), tuple(frames.shape), str(frames.device), gc, gd)
 
     def _drop_stale_graphs(self, key):
         """Forget graphs of older handle generations, then bound the cache (LRU)."""
@@ -173,12 +180,59 @@ class TwoStagePipeline:
                                               frames.shape[2], L.ptr(b["logits"]), L.ptr(b["probs"]),
                                               L.stream_ptr(side)))
             joined.record(side)
-            hd = self.detector.handle(n)
-            L.check(L.lib().rtdm_detect(hd, L.ptr(frames), L.RTDM_INPUT_FRAME_U8, n, L.ptr(b["io"]),
-                                        L.stream_ptr(crit)))
-            nms_batched(b["io"], self.conf_thres, self.iou_thres, self.multi_label, None, self.agnostic,
-                        self.max_det, out=(b["det"], b["idx"], b["count"]), stream=crit, workspace=b["ws"])
+            if self.detector is not None:  # None: classification only (BASELINE config 2)
+                hd = self.detector.handle(n)
+                L.check(L.lib().rtdm_detect(hd, L.ptr(frames), L.RTDM_INPUT_FRAME_U8, n, L.ptr(b["io"]),
+                                            L.stream_ptr(crit)))
+                nms_batched(b["io"], self.conf_thres, self.iou_thres, self.multi_label, None, self.agnostic,
+                            self.max_det, out=(b["det"], b["idx"], b["count"]), stream=crit, workspace=b["ws"])
             crit_done.record(crit)
             main.wait_event(joined)
             main.wait_event(crit_done)
         return b
+
+
+class FrameUploader:
+    """Host -> HBM frame upload overlapped with compute (the reference's per-image
+    `torch.from_numpy(img).to(device)`, detect.py:79-83, made asynchronous): pinned host
+    batches are copied on a dedicated copy stream into one of two device buffers per
+    pipeline while the pipeline's stream still computes on the other; the pipeline's stream
+    waits only for its own buffer's copy, and a buffer is not overwritten before the
+    pipeline call that read it has finished (events, no host synchronisation).
+
+        up = FrameUploader([pipe0, pipe1], streams)
+        out = up.submit(k, host_frames)   # batch k runs on pipes[k % P] / streams[k % P]
+    """
+
+    def __init__(self, pipes, streams, device=None):
+        self.pipes = list(pipes)
+        self.streams = list(streams)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.copy = torch.cuda.Stream(device=self.device)
+        self._bufs = {}  # (pipe j, slot, shape) -> device tensor
+        self._free = {}  # (pipe j, slot) -> event recorded after the call that read it
+        self._count = [0] * len(self.pipes)
+
+    def submit(self, k: int, host: torch.Tensor) -> dict:
+        j = k % len(self.pipes)
+        slot = self._count[j] % 2
+        self._count[j] += 1
+        key = (j, slot, tuple(host.shape))
+        dst = self._bufs.get(key)
+        if dst is None:
+            dst = self._bufs[key] = torch.empty(host.shape, dtype=host.dtype, device=self.device)
+        ev_free = self._free.get((j, slot))
+        with torch.cuda.stream(self.copy):
+            if ev_free is not None:
+                self.copy.wait_event(ev_free)
+            dst.copy_(host, non_blocking=True)
+            copied = torch.cuda.Event()
+            copied.record(self.copy)
+        s = self.streams[j]
+        with torch.cuda.stream(s):  # the call's first (eager) run and its graph replays: on s
+            s.wait_event(copied)
+            out = self.pipes[j](dst)
+            done = torch.cuda.Event()
+            done.record(s)
+        self._free[(j, slot)] = done
+        return out
