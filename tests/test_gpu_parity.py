@@ -156,6 +156,39 @@ def test_classifier_acff_chain_matches_per_stage(dev, name, cls_weights):
     assert torch.allclose(out[0][1], out[1][1], atol=1e-4)
 
 
+def test_redconv_config2_b32(dev, cls_weights):
+    """BASELINE config 2 as bench.py --cfg none runs it: Squeeze-ErNET-RedConv fp16 on a
+    batch of 32 224x224 uint8 sources through the device CLI transform (159 resize, 140
+    crop, aider.py:412-431).  Against the oracle (transform + model): logits <= 2e-2 *
+    max|logit|, class id exact where the top-2 gap >= 0.5; b1 rows bit-identical to the
+    b32 rows (batch-invariant kernels); the classification-only pipeline under graph replay
+    bit-identical to eager."""
+    from oracle import classifier as OC
+    from oracle import preprocess as P
+    from rtdm.pipeline import TwoStagePipeline
+    from rtdm.synth import BASE_SEED, synth_frames
+    frames = synth_frames(32, 224, 224, seed=BASE_SEED + 224)
+    x = torch.from_numpy(frames).to(dev)
+    m = _model("squeeze-redconv", cls_weights["squeeze-redconv"], half=True)
+    m.classify_frames(x)
+    got = m.logits.cpu().numpy()
+    ref = OC.forward("squeeze-redconv", cls_weights["squeeze-redconv"],
+                     torch.from_numpy(np.stack([P.cli_transform(f, 140) for f in frames])))[0].numpy()
+    assert np.all(np.abs(got - ref) <= 2e-2 * np.abs(ref).max(1, keepdims=True)), np.abs(got - ref).max()
+    srt = np.sort(ref, 1)
+    sure = srt[:, -1] - srt[:, -2] >= 0.5
+    assert sure.sum() >= 8 and np.array_equal(got.argmax(1)[sure], ref.argmax(1)[sure])
+    for i in (0, 13, 31):
+        m.classify_frames(x[i:i + 1].contiguous())
+        assert torch.equal(m.logits.cpu()[0], torch.from_numpy(got[i])), i
+    pe = TwoStagePipeline(m, None)
+    pg = TwoStagePipeline(m, None, graphs=True)
+    e = pe(x)["logits"].cpu().clone()
+    for _ in range(2):
+        g = pg(x)["logits"].cpu().clone()
+    assert torch.equal(e, g) and torch.equal(e, torch.from_numpy(got))
+
+
 def test_classifier_batch_edges(dev, cls_weights):
     """n = 0, 1 and a batch larger than the first handle capacity."""
     m = _model("squeeze-ernet", cls_weights["squeeze-ernet"])

@@ -1,6 +1,18 @@
+# GPU session (round 3): selected tests (TESTS / KEXPR), then bench lines (BENCHES: ";"-separated arg sets)
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest $R/tests/test_gpu_parity.py $R/tests/test_gpu_int8.py $R/tests/test_gpu_pipeline.py -m gpu -v -s --timeout 300 --timeout-method thread -k "cond or int8 or bench_config or graph_cache" > $OUT/r03a_tests.log 2>&1
-echo "tests rc $?"; tail -15 $OUT/r03a_tests.log
-[ "${BENCH:-1}" = 1 ] && cd $R && timeout -k 10 600 python bench.py --steps 30 --warmup 5 --cpu-baseline 0 > $OUT/r03a_bench.log 2>&1; echo "bench rc $?"; tail -c 1500 $OUT/r03a_bench.log
+TAG=${TAG:-r03}
+if [ -n "${TESTS:-}" ]; then
+  timeout -k 10 ${TTIME:-900} python -u -m pytest $TESTS -m gpu -v -s --timeout 300 --timeout-method thread ${KEXPR:+-k "$KEXPR"} > $OUT/${TAG}_tests.log 2>&1
+  rc=$?; echo "tests rc $rc"; tail -4 $OUT/${TAG}_tests.log
+  [ $rc -eq 0 ] || [ "${CONT:-0}" = 1 ] || exit $rc
+fi
+i=0
+IFS=';' read -ra BL <<< "${BENCHES:-}"
+for b in "${BL[@]}"; do
+  i=$((i+1))
+  (cd $R && timeout -k 10 600 python bench.py $b) > $OUT/${TAG}_bench$i.log 2>&1
+  rc=$?; echo "bench $i ($b) rc $rc"; tail -c 600 $OUT/${TAG}_bench$i.log; echo
+  [ $rc -eq 0 ] || exit $rc
+done
