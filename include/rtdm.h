@@ -132,7 +132,9 @@ const char* rtdm_build_arch(void);
  * cost model (default) | 256 | 128 | 64; "conv_pipe_win" 1 = window mode for
  * 3x3/s1 layers (default); "conv_pipe_korder" 1 = channel-block-outer K order
  * (default; 0 changes the fp32 summation order); "conv_pipe_pf" 1 = cross-tile
- * prologue prefetch (default).                                                   */
+ * prologue prefetch (default; not with ping-pong); "conv_pipe_pp" 1 = ping-pong
+ * K-loop (two wave groups alternating MFMA and memory phases; default 0: measured
+ * 4-18 % slower per layer).                                       */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 
 /* ---- classifier ------------------------------------------------------------ */

@@ -225,6 +225,7 @@ int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 
 void set_pipe_bm(int v);                  // 0 = cost model, else forced
 void set_pipe_korder(int v);              // conv_pipe K order: 0 tap outer, 1 channel-block outer
 void set_pipe_win(int v);                 // conv_pipe window mode (3x3 s1 inputs staged once per channel block)
+void set_pipe_pp(int v);                  // conv_pipe ping-pong K-loop schedule (f16)
 void set_pipe_pf(int v);                  // conv_pipe cross-tile prologue prefetch (register-epilogue layers)
 const char* conv_pipe_name(const ConvArgs& a);  // kernel symbol of that launch
 // int8 twin (RTDM_I8): a.in = quantised contiguous int8 copy of the input, a.w8 int8

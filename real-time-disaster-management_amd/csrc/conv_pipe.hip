@@ -26,6 +26,8 @@
 // with the fused epilogues of conv_epi.h).
 #include "conv_epi.h"
 
+#include <set>
+#include <string>
 #include <type_traits>
 
 namespace rtdm {
@@ -296,6 +298,8 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // per 16x16 block, with the 2x2 pool as two DPP max steps over quad-order rows: no
   // fp32 C tile through LDS and no barrier between the K-loop and the stores.
   constexpr bool REG = (ABL & 512) != 0;
+  // ABL bit 2048: ping-pong schedule (see the PP loop below)
+  constexpr bool PP = (ABL & 2048) != 0;
   constexpr bool RES_ = (ABL & 256) != 0;
   // cross-tile prefetch (pf, register epilogue only: the LDS ring is free during it)
   constexpr bool HEAD = (ABL & 8) != 0;
@@ -593,7 +597,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // wait for 0
   // (cross-tile prefetch: the previous tile of this workgroup issued them before its
   // epilogue, whose exactly EPI vector-memory ops are younger than K-block NSt-2)
-  if constexpr (WIN) win_addr();
+  if constexpr (WIN && !PP) win_addr();
   // the tile cursor past the prologue's NSt-1 K-blocks (issued here or by the previous tile)
   auto skip_prologue = [&]() {
 #pragma unroll
@@ -605,7 +609,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       st_buf = st_buf == NSt - 1 ? 0 : st_buf + 1;
     }
   };
-  if (PF && pre) {
+  if (PP) {
+    // (the ping-pong loop below issues its own prologue)
+  } else if (PF && pre) {
     skip_prologue();
     // (fused head: its io stores are per-lane conditional, so younger than K-block NSt-2
     // only a lower bound of them: none — the wait also covers them)
@@ -621,9 +627,11 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     for (int i = 0; i < nk; ++i) stage();
     wait_vm_lgkm0<0>();
   }
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  read0(0);
+  if constexpr (!PP) {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    read0(0);
+  }
 
   // Cluster A (half 0 of kb): MFMAs on fa0/fb0, interleaved with the reads of half 1
   // (fa1/fb1) and the buffer->LDS loads of kb+NSt-1.  Cluster B (half 1): MFMAs on
@@ -689,11 +697,91 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  if constexpr (!(ABL & 32)) {
+  if constexpr (!(ABL & 32) && !PP) {
     int kb = 0;
     for (; kb + NSt - 1 < nk; ++kb) body(T_{}, T_{});  // stages kb + NSt - 1
     for (; kb + 1 < nk; ++kb) body(F_{}, T_{});        // tail: nothing left to stage (waits vmcnt(0))
     body(F_{}, F_{});
+  }
+  // ---- ping-pong schedule (PP): the 8 waves are two groups of 4 -- group 0 = waves 0-3
+  //      (output rows 0 .. BM/2-1), group 1 = waves 4-7 (rows BM/2 ..), one wave of each
+  //      on every SIMD.  Every wave runs the same sequence -- a memory phase (its share of a
+  //      ring stage's LDS-DMA loads, the next K-block's fragment reads and addresses), then
+  //      an MFMA phase (all 32 MFMAs of that K-block, operands already in registers),
+  //      phases separated by workgroup barriers -- but group 1 runs one phase behind group
+  //      0, so in every phase each SIMD's matrix pipe has one wave issuing MFMAs back to
+  //      back while its partner feeds the next K-block (instead of both waves of a SIMD
+  //      meeting the same barrier, DMA wait and read latency together).  The memory phase
+  //      after K-block k's MFMAs issues stage k+3 (into k's ring slot: both groups have
+  //      read k by then) and reads K-block k+1; before each barrier a wave retires its ops
+  //      of the stage the next phase may read (the one after that stays in flight).
+  //      The loop body has no group-dependent branch, so the accumulators stay in one
+  //      register set.  Per accumulator the MFMA order is unchanged (K-blocks in order,
+  //      half 0 then half 1): bit-identical to the other schedule.
+  if constexpr (PP && !(ABL & 32)) {
+    const bool grp1 = wid >= WAVES / 2;
+    auto mfma_all = [&]() {
+#pragma unroll
+      for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < FN; ++tn) acc[tm][tn] = mfma(fa0[tm], fb0[tn], acc[tm][tn]);
+#pragma unroll
+      for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < FN; ++tn) acc[tm][tn] = mfma(fa1[tm], fb1[tn], acc[tm][tn]);
+    };
+    auto read_kb = [&](int buf) {  // both halves of one K-block's fragments
+      if constexpr (WIN) win_addr();
+      if constexpr (!(ABL & 2)) {
+        read0(buf);
+        read1(buf);
+      }
+    };
+    int ns = 0;  // ring stages issued by this wave
+    auto issue = [&]() {
+      if constexpr (!(ABL & 1)) stage();
+      ++ns;
+    };
+    // retire this wave's ops of stage `need` (and older); a younger issued stage stays in flight
+    auto wait_need = [&](int need) {
+      need = need < nk - 1 ? need : nk - 1;
+      if (ns - 1 > need)
+        wait_vmn_lgkm0<VM>();
+      else
+        wait_vmn_lgkm0<0>();
+    };
+    auto phase_end = [&]() {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // prologue: (window mode: channel block 0's window,) stages 0 and 1
+    if constexpr (WIN) {
+      for (int j = 0; 64 * j < wr; ++j) win_op(G0, j, 0, true);
+    }
+    if (nk > 0) issue();
+    if (nk > 1) issue();
+    wait_need(0);
+    phase_end();
+    if (grp1) phase_end();  // group 1: one phase behind
+    // memory phase before K-block 0: stage 2, K-block 0's fragments
+    if (ns < nk) issue();
+    read_kb(0);
+    wait_need(1);
+    phase_end();
+    int cur = 0;
+    for (int m = 0; m < nk; ++m) {
+      const int nxt = cur == NSt - 1 ? 0 : cur + 1;
+      mfma_all();
+      wait_need(m + 1);
+      phase_end();
+      if (ns < nk) issue();  // stage m + 3
+      if (m + 1 < nk) read_kb(nxt);
+      wait_need(m + 2);
+      phase_end();
+      cur = nxt;
+    }
+    if (!grp1) phase_end();  // the barrier count of group 1
   }
   if constexpr (REG) {
     if (pf) {
@@ -914,7 +1002,7 @@ __device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem
   bool pre = false;
   for (int t = lo + l; t < hi; t += bx) {
     const int nx = pf && t + bx < hi ? t + bx : -1;
-    pipe_tile<ABL, BM, I8, WIN>(a, smem_raw, t, pf, nx, pre);
+    pipe_tile<ABL, BM, I8, WIN>(a, smem_raw, t, pf && !(ABL & 2048), nx, pre);
     pre = nx >= 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1043,8 +1131,13 @@ static bool pipe_win_ok(const ConvArgs& a, int bm) {
 // turns it off (bit-identical either way).
 static int g_pipe_pf = 1;
 void set_pipe_pf(int v) { g_pipe_pf = v ? 1 : 0; }
+// Ping-pong schedule (ABL bit 2048, f16 only): rtdm_set_tuning("conv_pipe_pp", 1) turns it
+// on (bit-identical either way; measured slower, so off by default).
+static int g_pipe_pp = 0;
+void set_pipe_pp(int v) { g_pipe_pp = v ? 1 : 0; }
+
 static bool pipe_pf_ok(const ConvArgs& a, int abl, int nk) {
-  if (!g_pipe_pf || nk < kPNS - 1) return false;
+  if (!g_pipe_pf || nk < kPNS - 1 || (abl & 2048)) return false;
   if (abl == 8) return true;  // fused head: prefetch after the head GEMM, before the decode
   if (!(abl & 512) || !a.e.full.ptr || a.e.pool.ptr || a.e.up.ptr || a.e.scale) return false;
   const int64_t pix = (int64_t)a.n * a.oh * a.ow;
@@ -1067,9 +1160,23 @@ RTDM_PIPE_KERNEL(conv_pipe_i8)
 RTDM_PIPE_KERNEL(conv_pipew_i8)
 #undef RTDM_PIPE_KERNEL
 
-template <template <int, int> class K, int BM>
+template <template <int, int> class K, int BM, bool WITH_PP = false>
 static void launch_abl(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int nt, int pf) {
-  switch (abl) {
+  if constexpr (WITH_PP) {
+    switch (abl) {
+      case 8 | 2048:
+        if constexpr (BM >= 128) K<8 | 2048, BM>::go(g, s, a, nt, pf);
+        return;
+      case 128 | 2048: K<128 | 2048, BM>::go(g, s, a, nt, pf); return;
+      case 384 | 2048: K<384 | 2048, BM>::go(g, s, a, nt, pf); return;
+      case 640 | 2048: K<640 | 2048, BM>::go(g, s, a, nt, pf); return;
+      case 896 | 2048: K<896 | 2048, BM>::go(g, s, a, nt, pf); return;
+      case 1024 | 2048: K<1024 | 2048, BM>::go(g, s, a, nt, pf); return;
+      case 2048: K<2048, BM>::go(g, s, a, nt, pf); return;
+      default: break;
+    }
+  }
+  switch (abl & ~2048) {
     case 8:
       if constexpr (BM >= 128) K<8, BM>::go(g, s, a, nt, pf);
       break;
@@ -1084,36 +1191,29 @@ static void launch_abl(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int nt
 
 template <int BM>
 static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid, bool win) {
-  const int abl = pipe_abl(a), pf = pipe_pf_ok(a, abl, a.kpad / kPBK) ? 1 : 0;
+  const int abl = pipe_abl(a) | (g_pipe_pp ? 2048 : 0), pf = pipe_pf_ok(a, abl, a.kpad / kPBK) ? 1 : 0;
   if constexpr (BM >= 128) {
-    if (win) return launch_abl<conv_pipew_f16_k, BM>(abl, grid, s, a, ntiles, pf);
+    if (win) return launch_abl<conv_pipew_f16_k, BM, true>(abl, grid, s, a, ntiles, pf);
   }
-  launch_abl<conv_pipe_f16_k, BM>(abl, grid, s, a, ntiles, pf);
+  launch_abl<conv_pipe_f16_k, BM, true>(abl, grid, s, a, ntiles, pf);
 }
 
+// kernel symbol of a launch, e.g. conv_pipew_f16<640,256> (the ping-pong schedule, ABL bit
+// 2048, as conv_pipewpp_f16<640,256>); the strings live in a set (stable pointers)
 static const char* pipe_name(bool i8, bool win, int abl, int bm) {
-  static char buf[4][2][7][3][32];
-  static bool init = false;
-  static const int abls[7] = {8, 128, 384, 640, 896, 1024, 0};
-  static const int bms[3] = {256, 128, 64};
-  if (!init) {
-    for (int q = 0; q < 4; ++q)
-      for (int k = 0; k < 7; ++k)
-        for (int b = 0; b < 3; ++b)
-          snprintf(buf[q][0][k][b], 32, "conv_pipe%s_%s<%d,%d>", (q & 1) ? "w" : "", (q & 2) ? "i8" : "f16", abls[k], bms[b]);
-    init = true;
-  }
-  int k = 0, b = 0;
-  while (k < 6 && abls[k] != abl) ++k;
-  while (b < 2 && bms[b] != bm) ++b;
-  return buf[(i8 ? 2 : 0) | (win ? 1 : 0)][0][k][b];
+  static std::set<std::string> names;
+  char b[48];
+  snprintf(b, sizeof b, "conv_pipe%s%s_%s<%d,%d>", win ? "w" : "", (abl & 2048) ? "pp" : "", i8 ? "i8" : "f16",
+           abl & ~2048, bm);
+  return names.insert(b).first->c_str();
 }
 
 const char* conv_pipe_name(const ConvArgs& a_in) {
   ConvArgs a = a_in;
   a.pipe_corder = g_pipe_korder_get() && a.ks == 3 ? 1 : 0;
-  const int bm = pipe_bm(a);
-  return pipe_name(false, pipe_win_ok(a, bm), pipe_abl(a), bm);
+  const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
+  const bool abl_mode = a.head_w || conv_pipe_mode() <= 1 || conv_pipe_mode() == 13;
+  return pipe_name(false, abl_mode && pipe_win_ok(a, bm), pipe_abl(a) | (abl_mode && g_pipe_pp ? 2048 : 0), bm);
 }
 
 // K order of the implicit GEMM: 0 = tap outer (each tap's whole channel run), 1 = 64-channel
@@ -1143,6 +1243,13 @@ void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
     case 9: hipLaunchKernelGGL((conv_pipe_f16<48, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
     case 10: hipLaunchKernelGGL((conv_pipe_f16<96, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
     case 11: hipLaunchKernelGGL((conv_pipe_f16<0, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    // ping-pong ablations (diagnostics): 20 the PP kernel, generic epilogue; 21 no loads;
+    // 22 no fragment reads; 23 neither; 24 no epilogue
+    case 20: hipLaunchKernelGGL((conv_pipe_f16<2048, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 21: hipLaunchKernelGGL((conv_pipe_f16<2049, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 22: hipLaunchKernelGGL((conv_pipe_f16<2050, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 23: hipLaunchKernelGGL((conv_pipe_f16<2051, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    case 24: hipLaunchKernelGGL((conv_pipe_f16<2064, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
     default: {
       const bool win = pipe_win_ok(a, bm);
       if (bm == 256)

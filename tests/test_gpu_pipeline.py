@@ -346,14 +346,55 @@ def test_lean_window_epilogues_bit_identical(dev, case):
                     nm = ctypes.create_string_buffer(64)
                     L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, None, None, None))
                     names.add(nm.value.decode())
-                want = ("<896,",) if cfg.startswith("yolov3") else ("<640,", "conv_pipe_f16<128,")
+                want = ("<896,",) if cfg.startswith("yolov3") else ("<640,", "_f16<128,")
                 for w in want:
                     assert any(w in n for n in names), (w, names)
-                assert any(n.startswith("conv_pipew_f16<") for n in names), names
+                assert any(n.startswith(("conv_pipew_f16<", "conv_pipewpp_f16<")) for n in names), names
     finally:
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe", 1))
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
     assert torch.equal(outs[11], outs[1])
+
+
+@pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608:3", "yolov3-aider-416@416:3", "yolov4-tiny-aider-416@608:9"])
+@pytest.mark.parametrize("pp", [0, 1])
+def test_pingpong_bit_identical(dev, case, pp):
+    """conv_pipe's ping-pong K-loop (rtdm_set_tuning("conv_pipe_pp"): two wave groups
+    alternating MFMA and memory phases) against the per-K-block-barrier schedule, window
+    mode off (pp=0 row) and on: same io bits; 256-row tiles and the cost model's tiles."""
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    cfg, rest = case.split("@")
+    size, b = (int(v) for v in rest.split(":"))
+    x = torch.from_numpy(synth_frames(b, size, size, seed=37)).to(dev)
+    outs = {}
+    try:
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_win", pp))
+        for bm in (256, 0):
+            L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", bm))
+            for v in (0, 1):
+                L.check(L.lib().rtdm_set_tuning(b"conv_pipe_pp", v))
+                m, _, _, _ = _detector(cfg, size)
+                outs[(bm, v)] = m(x)[0].cpu()
+                assert any("pp_f16<" in n for n in _names(m, b)) == bool(v)
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_pp", 0))
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_win", 1))
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
+    for bm in (256, 0):
+        assert torch.equal(outs[(bm, 0)], outs[(bm, 1)]), bm
+
+
+def _names(m, n):
+    import ctypes
+    from rtdm import _lib as L
+    h = m.handle(n)
+    out = set()
+    for i in range(L.lib().rtdm_detector_num_steps(h)):
+        nm = ctypes.create_string_buffer(64)
+        L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, None, None, None))
+        out.add(nm.value.decode())
+    return out
 
 
 @pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416"])
@@ -379,7 +420,7 @@ def test_window_mode_bit_identical(dev, case):
                 nm = ctypes.create_string_buffer(64)
                 L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, None, None, None))
                 names.add(nm.value.decode())
-            assert any(n.startswith("conv_pipew_") for n in names) == bool(v), names
+            assert any(n.startswith(("conv_pipew_", "conv_pipewpp_")) for n in names) == bool(v), names
     finally:
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe_win", 1))
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
