@@ -201,7 +201,11 @@ rtdm_status rtdm_detector_step_info(rtdm_detector h, int step, char* name, int n
  * read_timing synchronises those events and returns the summed ms per step.    */
 rtdm_status rtdm_detector_enable_timing(rtdm_detector h, int max_calls);
 rtdm_status rtdm_detector_read_timing(rtdm_detector h, double* ms_per_step, int* calls);
-/* io: [n, n_anchors_total, no] fp32, exactly the reference's torch.cat(io, 1). */
+/* io: [n, n_anchors_total, no] fp32, exactly the reference's torch.cat(io, 1).
+ * Inputs must be finite: the conv kernels are built with -fno-honor-nans (their max-pool
+ * and LeakyReLU epilogues skip NaN canonicalisation), so a NaN / Inf in an NCHW float
+ * input yields unspecified io rows where the reference would carry NaN to its NMS finite
+ * filter (utils.py:535-536).  uint8 frames (RTDM_INPUT_FRAME_U8) are always finite.   */
 rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float* io, void* stream);
 /* int8 calibration (RTDM_I8 handles): runs the network in fp16 on x (n images, kinds
  * as rtdm_detect) recording every int8 conv's per-input-channel |x|max (max over all

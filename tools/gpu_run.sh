@@ -1,4 +1,4 @@
-# GPU session (round 3): selected tests (TESTS / KEXPR), then bench lines (BENCHES: ";"-separated arg sets)
+# GPU session: selected tests (TESTS / KEXPR), then bench lines (BENCHES: ";"-separated arg sets)
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
