@@ -4,7 +4,7 @@
 #   stages: any of "tests smoke bench prof pmc" (default: all)
 set -u
 TAG=${1:-r01}
-STAGES=${2:-"tests smoke bench prof pmc"}
+STAGES=${2:-"tests smoke bench prof proflaunch pmc"}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
@@ -27,6 +27,13 @@ if has prof; then
   echo "== rocprofv3 kernel stats"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run -- python3 $R/bench.py --steps 10 --warmup 3 --cpu-baseline 0 ${BENCH_ARGS:-} > $OUT/prof_$TAG.log 2>&1
   rc=$?; tail -1 $OUT/prof_$TAG.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has proflaunch; then
+  # the bench's roofline figure is measured on isolated eager launches (per-launch hipEvents
+  # after the timed region); this profile times the same kind of launches alone
+  echo "== rocprofv3 kernel stats, isolated launches"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_${TAG}_rl -o run -- python3 $R/bench.py --steps 1 --warmup 0 --h2d-steps 0 --cpu-baseline 0 --inflight 1 ${BENCH_ARGS:-} > $OUT/prof_${TAG}_rl.log 2>&1
+  rc=$?; tail -1 $OUT/prof_${TAG}_rl.log; [ $rc -eq 0 ] || exit $rc
 fi
 if has pmc; then
   for C in FETCH_SIZE WRITE_SIZE; do
