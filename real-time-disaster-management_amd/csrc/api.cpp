@@ -43,6 +43,10 @@ rtdm_status rtdm_set_tuning(const char* key, int value) {
       set_pipe_pf(value);
     else if (!strcmp(key, "conv_pipe_pp"))
       set_pipe_pp(value);
+    else if (!strcmp(key, "conv_pipe_walk"))
+      set_pipe_walk(value);
+    else if (!strcmp(key, "conv_pipe_c32"))
+      set_pipe_c32(value);
     else if (!strcmp(key, "head1x1"))
       set_head1x1(value);
     else if (!strcmp(key, "dw3_tile"))

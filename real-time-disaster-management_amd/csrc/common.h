@@ -192,6 +192,7 @@ struct ConvArgs {
   FastDiv fd_cin;                // set by conv_set_rows
   int glds_uni = 0;              // conv_glds_f16: uniform-tap staging (set by launch_conv)
   int pipe_corder = 0;           // conv_pipe_f16: channel-block-outer K order (set by launch_conv_pipe)
+  int pipe_g = 0;                // conv_pipe: N-panels per tile-walk group (0: M-major walk; set at launch)
   Epilogue e;
   // Fused YOLO head (conv_pipe_f16 only): a 1x1 conv over this conv's activated
   // output (cout <= 128 = one N tile), head_w fp16 [head_cout_pad][cout_pad] (k = c),
@@ -225,6 +226,9 @@ int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 
 void set_pipe_bm(int v);                  // 0 = cost model, else forced
 void set_pipe_korder(int v);              // conv_pipe K order: 0 tap outer, 1 channel-block outer
 void set_pipe_win(int v);                 // conv_pipe window mode (3x3 s1 inputs staged once per channel block)
+void set_pipe_c32(int v);                 // conv_pipe for Cin = 32 3x3 convs (two taps per K-block)
+int pipe_c32_enabled();                   // (planner: pad their 64 outputs to one 128-channel tile)
+void set_pipe_walk(int v);                // conv_pipe tile walk: N-panels per group (0 = M-major)
 void set_pipe_pp(int v);                  // conv_pipe ping-pong K-loop schedule (f16)
 void set_pipe_pf(int v);                  // conv_pipe cross-tile prologue prefetch (register-epilogue layers)
 const char* conv_pipe_name(const ConvArgs& a);  // kernel symbol of that launch

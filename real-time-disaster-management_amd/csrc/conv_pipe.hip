@@ -370,6 +370,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   //      Per-tile part (PipeGeo): A row offsets / tap masks, the window origin, the weight
   //      panel; built for this tile and, for the cross-tile prefetch, for the next one. ----
   const int slot = lane & 7;
+  // Cin = 32 (c32): a 64-deep K-block spans two taps (k = tap * 32 + c, tap-major as the
+  // weights are packed): k-vector v of a row is tap 2 kb + (v >> 2), channels 8 (v & 3)..
+  const bool c32 = !WIN && a.cin == 32;
   struct Geo {
     int m_base, koff_n;                // koff_n: byte offset of the tile's weight panel
     int voff_a[WIN ? 1 : NA];
@@ -385,7 +388,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 #pragma unroll
     for (int j = 0; j < (WIN ? 0 : NA); ++j) {
       const int r = 8 * (NA * wid + j) + (lane >> 3);
-      const int kofs = 16 * (slot ^ (r & 7));  // bytes
+      const int kofs = 16 * ((slot ^ (r & 7)) & (c32 ? 3 : 7));  // bytes
       const int m = G.m_base + r;
       int n = 0, oy = 0, ox = 0;
       if (m < a.M) row_to_pix(a, m, n, oy, ox);
@@ -428,7 +431,16 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // selected by value (a by-reference select of the counter to bump sends the cursor to
   // scratch, and its loads' vmcnt(0) then drains the LDS-DMA pipeline every K-block).
   const bool corder = a.pipe_corder != 0;
-  const int ni = corder ? ntap : cpt;
+  const int ni = c32 ? nk : corder ? ntap : cpt;
+  // c32: per A op, whether this lane's k-vector is the K-block's second tap
+  uint32_t c32_hi = 0;
+  if (c32) {
+#pragma unroll
+    for (int j = 0; j < (WIN ? 0 : NA); ++j) {
+      const int r = 8 * (NA * wid + j) + (lane >> 3);
+      c32_hi |= (uint32_t)(((slot ^ (r & 7)) >> 2) & 1) << j;
+    }
+  }
   int st_i = 0, st_o = 0, st_buf = 0;
 
   // window mode: buffers, window geometry (rows of the channel block's window: pixels
@@ -465,6 +477,16 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       // j = st_tap - 2 (taps 2..8 -> slices 0..6) of channel block st_c + 1's window
       const int j = st_tap - 2, cw = st_c + 1;
       win_op(G, j < 0 ? 0 : j, cw, j >= 0 && cw < ncb && 64 * j < wr);
+    } else if (c32) {  // taps 2 kb, 2 kb + 1 (kb = st_c); tap 9 is padding (mask bit 0)
+      const int t0 = 2 * st_c, t1 = t0 + 1;
+      const int kh0 = (t0 * 11) >> 5, kw0 = t0 - 3 * kh0, kh1 = (t1 * 11) >> 5, kw1 = t1 - 3 * kh1;
+      const int off0 = (kh0 * a.iw + kw0) * a.in_cs * ES, off1 = (kh1 * a.iw + kw1) * a.in_cs * ES;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const bool hi = (c32_hi >> j) & 1u;
+        const int vo = ((G.vmask[j] >> (hi ? t1 : t0)) & 1u) ? G.voff_a[j] + (hi ? off1 : off0) : (int)0x80000000;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(As + 8 * (NA * wid + j) * BK), 16, vo, 0, 0, 0);
+      }
     } else {
       const int tapoff = ((kh * a.iw + kw) * a.in_cs + st_c * BKE) * ES;
 #pragma unroll
@@ -474,7 +496,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       }
     }
     // weight column of this K-block (tap-major packing) in the tile's panel
-    const int koff = G.koff_n + (st_tap * a.cin + st_c * BKE) * ES;
+    const int koff = G.koff_n + (c32 ? st_c * 64 : st_tap * a.cin + st_c * BKE) * ES;
 #pragma unroll
     for (int j = 0; j < NB; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j], koff,
@@ -985,6 +1007,19 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 // XCD (A panels shared in that XCD's L2), so a tile's epilogue stores drain while the
 // next tile's first K-blocks load, instead of every CU storing, then loading, in
 // lockstep rounds.  Between tiles only LDS is fenced (lgkmcnt): the stores stay in flight.
+// Tile walk order.  Linear walk index t -> logical tile (M-major: mt * ntn + nt).  With
+// a.pipe_g = g (a divisor of ntn, 0 < g < ntn) the walk is N-group major: the g N-panels of
+// one group, M-tile by M-tile, then the next group.  An XCD's 32 CUs then hold 32/g M-tiles
+// x g weight panels at a time instead of 32/ntn x ntn: fewer weight panels live per L2.
+__device__ __forceinline__ int pipe_tile_map(const ConvArgs& a, int t, int ntiles) {
+  const int ntn = a.cout_pad / kPBN, g = a.pipe_g;
+  if (g <= 0 || g >= ntn) return t;
+  const int ntm = ntiles / ntn, per_grp = ntm * g;
+  const int grp = t / per_grp, r = t - grp * per_grp;
+  const int mt = r / g, j = r - mt * g;
+  return mt * ntn + grp * g + j;
+}
+
 template <int ABL, int BM, bool I8, bool WIN>
 __device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem_raw, int ntiles, bool pf) {
   const int nb = gridDim.x, xcd = blockIdx.x & 7, l = blockIdx.x >> 3;
@@ -1001,8 +1036,8 @@ __device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem
   }
   bool pre = false;
   for (int t = lo + l; t < hi; t += bx) {
-    const int nx = pf && t + bx < hi ? t + bx : -1;
-    pipe_tile<ABL, BM, I8, WIN>(a, smem_raw, t, pf && !(ABL & 2048), nx, pre);
+    const int nx = pf && t + bx < hi ? pipe_tile_map(a, t + bx, ntiles) : -1;
+    pipe_tile<ABL, BM, I8, WIN>(a, smem_raw, pipe_tile_map(a, t, ntiles), pf && !(ABL & 2048), nx, pre);
     pre = nx >= 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1036,10 +1071,18 @@ __global__ __launch_bounds__(512, 1) void conv_pipew_i8(ConvArgs a, int ntiles, 
   pipe_walk<ABL, BM, true, true>(a, smem_raw, ntiles, pf != 0);
 }
 
+// Cin = 32 3x3 convs (c32 staging, two taps per K-block; Darknet-53's L1 / L3) when
+// rtdm_set_tuning("conv_pipe_c32", 1) (default)
+static int g_pipe_c32 = 1;
+void set_pipe_c32(int v) { g_pipe_c32 = v ? 1 : 0; }
+int pipe_c32_enabled() { return g_pipe_c32; }
+static bool pipe_c32(const ConvArgs& a) { return a.cin == 32 && a.ks == 3 && a.kpad == 320; }
+
 bool conv_pipe_ok(const ConvArgs& a) {
   if (!a.zero || a.in_kind != IN_NHWC || a.w_f32 || (a.in_cs | a.in_co) % 8 != 0) return false;
-  if (a.cin % 64 != 0 || a.cout_pad % kPBN != 0 || (a.ks != 1 && a.ks != 3)) return false;
-  if (a.kpad != a.ks * a.ks * a.cin) return false;
+  const bool c32 = g_pipe_c32 && pipe_c32(a) && !a.head_w;
+  if ((a.cin % 64 != 0 && !c32) || a.cout_pad % kPBN != 0 || (a.ks != 1 && a.ks != 3)) return false;
+  if (a.kpad != a.ks * a.ks * a.cin && !c32) return false;
   const int64_t elems = (int64_t)a.n * a.ih * a.iw * a.in_cs;
   if (elems >= (1ll << 30) || (int64_t)a.cout_pad * a.kpad * 2 >= (1ll << 31)) return false;
   if (a.head_w) {  // fused head: one N tile, head K = 128, output only through the head
@@ -1119,7 +1162,7 @@ static int pipe_abl(const ConvArgs& a) {
 static int g_pipe_win = 1;
 void set_pipe_win(int v) { g_pipe_win = v ? 1 : 0; }
 static bool pipe_win_ok(const ConvArgs& a, int bm) {
-  return g_pipe_win && bm == 256 && a.ks == 3 && a.stride == 1 && a.pad == 1 && !a.quad && a.pipe_corder &&
+  return g_pipe_win && bm == 256 && a.cin % 64 == 0 && a.ks == 3 && a.stride == 1 && a.pad == 1 && !a.quad && a.pipe_corder &&
          a.ih == a.oh && a.iw == a.ow && bm + 2 * a.iw + 2 <= kWinRows;
 }
 
@@ -1135,6 +1178,15 @@ void set_pipe_pf(int v) { g_pipe_pf = v ? 1 : 0; }
 // on (bit-identical either way; measured slower, so off by default).
 static int g_pipe_pp = 0;
 void set_pipe_pp(int v) { g_pipe_pp = v ? 1 : 0; }
+
+// Tile walk (pipe_tile_map): N-panels per group; 0 = the M-major walk.  rtdm_set_tuning(
+// "conv_pipe_walk", g).  Bit-identical for every g (only the order tiles run in changes).
+static int g_pipe_walk = 0;
+void set_pipe_walk(int v) { g_pipe_walk = v > 0 ? v : 0; }
+static int pipe_walk_g(const ConvArgs& a) {
+  const int ntn = a.cout_pad / kPBN;
+  return g_pipe_walk > 0 && g_pipe_walk < ntn && ntn % g_pipe_walk == 0 ? g_pipe_walk : 0;
+}
 
 static bool pipe_pf_ok(const ConvArgs& a, int abl, int nk) {
   if (!g_pipe_pf || nk < kPNS - 1 || (abl & 2048)) return false;
@@ -1210,7 +1262,7 @@ static const char* pipe_name(bool i8, bool win, int abl, int bm) {
 
 const char* conv_pipe_name(const ConvArgs& a_in) {
   ConvArgs a = a_in;
-  a.pipe_corder = g_pipe_korder_get() && a.ks == 3 ? 1 : 0;
+  a.pipe_corder = g_pipe_korder_get() && a.ks == 3 && a.cin % 64 == 0 ? 1 : 0;
   const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
   const bool abl_mode = a.head_w || conv_pipe_mode() <= 1 || conv_pipe_mode() == 13;
   return pipe_name(false, abl_mode && pipe_win_ok(a, bm), pipe_abl(a) | (abl_mode && g_pipe_pp ? 2048 : 0), bm);
@@ -1224,7 +1276,8 @@ const char* conv_pipe_name(const ConvArgs& a_in) {
 
 void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
   ConvArgs a = a_in;
-  a.pipe_corder = g_pipe_korder && a.ks == 3 ? 1 : 0;
+  a.pipe_corder = g_pipe_korder && a.ks == 3 && a.cin % 64 == 0 ? 1 : 0;
+  a.pipe_g = pipe_walk_g(a);
   const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
   const int64_t nt = (int64_t)((a.M + bm - 1) / bm) * (a.cout_pad / kPBN);
   RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
@@ -1287,6 +1340,7 @@ void launch_conv_pipe_i8(const ConvArgs& a_in, hipStream_t s) {
   ConvArgs a = a_in;
   RTDM_REQUIRE(conv_pipe_i8_ok(a), RTDM_E_INVALID, "conv_pipe_i8: unsupported layer");
   a.pipe_corder = g_pipe_korder && a.ks == 3 ? 1 : 0;
+  a.pipe_g = pipe_walk_g(a);
   const int bm = pipe_bm_nk(a, a.kpad / 128);
   const int64_t nt = (int64_t)((a.M + bm - 1) / bm) * (a.cout_pad / kPBN);
   RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");

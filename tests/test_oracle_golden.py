@@ -203,3 +203,35 @@ def test_trt_postprocess_product_matches_oracle():
             assert np.array_equal(g, e)
     empty = postprocess_yolo([np.zeros((5, 7), np.float32)], 416, 416, 0.3, 0.5, (416, 416))
     assert empty[0].shape == (0, 4)
+
+
+def test_survivor_band_rule():
+    """oracle.nms.survivors_equal_outside_band (SURVEY §8d's end-to-end fp16 rule): equal io
+    -> no difference; a candidate moved across the conf threshold by < the band is excused,
+    by more is not; a swap of two overlapping candidates' scores by < the band is excused
+    (and what it suppresses follows), a swap by more is not."""
+    from oracle import nms as ON
+    io = np.zeros((1, 6, 7), np.float32)
+    # two overlapping boxes (IoU 0.81), one far box, one box near conf 0.3, two others off
+    io[0, :, 0:4] = [[100, 100, 40, 40], [102, 102, 40, 40], [300, 300, 30, 30], [200, 50, 20, 20],
+                     [50, 300, 20, 20], [400, 400, 20, 20]]
+    io[0, :, 4] = [0.9, 0.85, 0.8, 0.3004, 0.1, 0.1]
+    io[0, :, 5] = [1.0, 1.0, 1.0, 1.0, 1.0, 1.0]
+    io[0, :, 6] = 0.0
+    n_ref, n_got, n_exc, bad = ON.survivors_equal_outside_band(io, io.copy(), 0.3, 0.4)
+    assert (n_ref, n_got, n_exc, bad) == (3, 3, 0, [])
+    near = io.copy()
+    near[0, 3, 4] = 0.2996  # crosses 0.3 by 4e-4 (inside 1e-3): excused
+    n_ref, n_got, n_exc, bad = ON.survivors_equal_outside_band(io, near, 0.3, 0.4)
+    assert n_ref == 3 and n_got == 2 and n_exc == 1 and bad == []
+    far = io.copy()
+    far[0, 2, 4] = 0.29  # a clear survivor dropped: not excused
+    assert ON.survivors_equal_outside_band(io, far, 0.3, 0.4)[3] == [(0, 2, 0)]
+    tie = io.copy()
+    tie[0, 0, 4], tie[0, 1, 4] = 0.8500, 0.8504  # overlapping pair, scores within 1e-3 in ref
+    swapped = tie.copy()
+    swapped[0, 0, 4], swapped[0, 1, 4] = 0.8504, 0.8500
+    assert ON.survivors_equal_outside_band(tie, swapped, 0.3, 0.4)[3] == []
+    wide = io.copy()
+    wide[0, 0, 4], wide[0, 1, 4] = 0.85, 0.9  # the same swap by 5e-2: not excused
+    assert len(ON.survivors_equal_outside_band(io, wide, 0.3, 0.4)[3]) == 2
