@@ -1072,8 +1072,10 @@ __global__ __launch_bounds__(512, 1) void conv_pipew_i8(ConvArgs a, int ntiles, 
 }
 
 // Cin = 32 3x3 convs (c32 staging, two taps per K-block; Darknet-53's L1 / L3) when
-// rtdm_set_tuning("conv_pipe_c32", 1) (default)
-static int g_pipe_c32 = 1;
+// rtdm_set_tuning("conv_pipe_c32", 1).  Off by default: their 64 outputs fill half of the
+// 128-channel N tile and K is only 5 K-blocks -- yolov3@416 b16 L1 0.118 -> 0.156 ms,
+// L3 0.141 -> 0.193 ms against conv_mfma_f16 (r03m)
+static int g_pipe_c32 = 0;
 void set_pipe_c32(int v) { g_pipe_c32 = v ? 1 : 0; }
 int pipe_c32_enabled() { return g_pipe_c32; }
 static bool pipe_c32(const ConvArgs& a) { return a.cin == 32 && a.ks == 3 && a.kpad == 320; }
@@ -1181,7 +1183,9 @@ void set_pipe_pp(int v) { g_pipe_pp = v ? 1 : 0; }
 
 // Tile walk (pipe_tile_map): N-panels per group; 0 = the M-major walk.  rtdm_set_tuning(
 // "conv_pipe_walk", g).  Bit-identical for every g (only the order tiles run in changes).
-static int g_pipe_walk = 0;
+// Default 2: yolov4-tiny@608 b64 L12 (8 N-panels) fetches 39 % fewer bytes past L2 (PMC
+// FETCH_SIZE, r03l) at the same time (0.2007 vs 0.2009 ms).
+static int g_pipe_walk = 2;
 void set_pipe_walk(int v) { g_pipe_walk = v > 0 ? v : 0; }
 static int pipe_walk_g(const ConvArgs& a) {
   const int ntn = a.cout_pad / kPBN;
