@@ -80,7 +80,9 @@ def parse():
     ap.add_argument("--priority", type=int, default=0,
                     help="1: detector + NMS on a high-priority stream, classifier on a low-priority one")
     ap.add_argument("--det-streams", type=int, default=1, help="detector head branches on a side stream (2) or not (1)")
-    ap.add_argument("--graphs", type=int, default=1, help="1: replay each step as a hipGraph; 0: eager launches")
+    ap.add_argument("--graphs", type=int, default=-1,
+                    help="1: replay each step as a hipGraph; 0: eager launches; -1: by per-GPU batch (graphs from 64 "
+                         "frames up, eager below)")
     ap.add_argument("--rotate", type=int, default=4, help="distinct frame batches the steps cycle over")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight per GPU (0: 3 for <= 16 frames per GPU, else 2): step k runs on "
@@ -336,12 +338,17 @@ def main():
     if global_batch % world:
         raise SystemExit(f"global batch {global_batch} does not shard evenly over {world} ranks")
     first, b = shard_range(global_batch, world, rank)
-    if args.inflight <= 0:
-        # measured on MI355X (profiles/r02k_*): b8 1 / 2 / 3 / 4 in flight 18.5k / 21.6k / 24.2k / 21.2k
-        # frames/s; b64 1 / 2 / 3: 37.3k / 41.4k / 40.6k; r02cg (200 steps): b16 2 / 3 / 4 32.7k /
-        # 35.3k / 31.8k, b32 2 / 3 38.9k / 39.3k.  GPU_MAX_HW_QUEUES is 4: one hardware queue per
-        # in-flight batch, plus RCCL's
-        args.inflight = 3 if b <= 32 else 2
+    if args.graphs < 0 or args.inflight <= 0:
+        # measured on MI355X (profiles/r03_operating_points.md): below 64 frames per GPU, eager
+        # launches with 4 batches in flight beat graph replay with 3 (b8 33.5k vs 30.4k frames/s,
+        # b16 39.1k vs 36.7k, b32 41.8k vs 39.4k, int8 b16 43.7k vs 40.5k); replayed graphs on a 4th
+        # in-flight stream serialise (b8 graphs 4 in flight: 21-25k).  At b64 graphs with 2 in flight
+        # stay best (45.3k; eager 2 / 3 / 4: 43.8k / 44.4k / 44.8k).
+        small = b < 64
+        if args.graphs < 0:
+            args.graphs = 0 if small else 1
+        if args.inflight <= 0:
+            args.inflight = (4 if not args.graphs else 3) if small else 2
     pipes, text, stream, sd = build(args, world, rank)
     pipe, det = pipes[0], pipes[0].detector
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in pipes[1:]]
