@@ -29,6 +29,7 @@
 #include <set>
 #include <string>
 #include <type_traits>
+#include <utility>
 
 namespace rtdm {
 
@@ -52,7 +53,8 @@ struct PipeCfg {
 // per-row swizzled 2 KB zero area removes the border reads' bank conflicts but its
 // per-K-block address VALU cost more: r02ck).
 constexpr int kWinRows = 440;
-constexpr int kWinSmem = (2 * kWinRows * kPBK + kPNS * kPBN * kPBK + 8 * kPBK) * 2;
+// + a 1 KB junk area: the tap-unrolled loop's window slice 6 rows past kWinRows land there
+constexpr int kWinSmem = (2 * kWinRows * kPBK + kPNS * kPBN * kPBK + 16 * kPBK) * 2;
 static_assert(kWinSmem <= 163840, "window LDS");
 
 // s_waitcnt vmcnt(N) lgkmcnt(0), any N < 64 (gfx9 encoding: vmcnt bits 3:0 and 15:14)
@@ -73,8 +75,15 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
     asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
   else if constexpr (N == 8)
     asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 2)
+    asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
   else
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+// f(integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time
+template <class F, int... I>
+__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
 }
 }  // namespace
 
@@ -300,6 +309,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   constexpr bool REG = (ABL & 512) != 0;
   // ABL bit 2048: ping-pong schedule (see the PP loop below)
   constexpr bool PP = (ABL & 2048) != 0;
+  // window mode with the taps unrolled (see the WLOOP loop below); ABL bit 4096 selects the
+  // generic cursor loop instead (A/B diagnostics)
+  constexpr bool WLOOP = WIN && !PP && !(ABL & 4096);
   constexpr bool RES_ = (ABL & 256) != 0;
   // cross-tile prefetch (pf, register epilogue only: the LDS ring is free during it)
   constexpr bool HEAD = (ABL & 8) != 0;
@@ -309,8 +321,10 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // of this lane's accumulators.  Fused head: the FN columns of this lane's accumulators.
   constexpr int CG = BN / 8;
   float lb[8], ls[8], lh[8], la[8];
+  // (register epilogue: its bias is loaded after the K-loop, load_rb, so that its 4 FN
+  // registers are not live across the loop)
   f4 rb[REG ? FN : 1];
-  if constexpr (REG) {
+  auto load_rb = [&]() {
     const __amdgpu_buffer_rsrc_t rs_bias = __builtin_amdgcn_make_buffer_rsrc((void*)a.e.bias, 0, a.cout * 4, 0x00020000);
 #pragma unroll
     for (int tn = 0; tn < FN; ++tn) {
@@ -318,6 +332,11 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       // buffer load: out-of-range channels (c0 >= cout) load zeros
       rb[tn] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs_bias, c0 * 4, 0, 0));
     }
+  };
+  // WLOOP: the register epilogue's bias / the fused head's constants are loaded in the last
+  // K-block body (their registers are not live across the loop); elsewhere at the tile start
+  if constexpr (REG) {
+    if constexpr (!WLOOP) load_rb();
   } else if constexpr ((ABL & 128) != 0) {
     const int c0 = n_base + (tid % CG) * 8;
     const bool cv = c0 < a.cout;
@@ -346,8 +365,8 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       dq[tn] = col < a.cout ? a.deq[col] : 0.f;
     }
   }
-  float hb[FN], hs[FN], hh[FN];
-  if constexpr ((ABL & 8) != 0) {
+  float hb[FN], hs[FN], hh[FN];  // fused head: loaded after the K-loop (load_hconst)
+  auto load_hconst = [&]() {
 #pragma unroll
     for (int tn = 0; tn < FN; ++tn) {
       const int col = wn * (BN / WN) + tn * 16 + (lane & 15);
@@ -356,7 +375,8 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       hs[tn] = (cv && a.e.scale) ? a.e.scale[col] : 1.f;
       hh[tn] = (cv && a.e.scale) ? a.e.shift[col] : 0.f;
     }
-  }
+  };
+  if constexpr (HEAD && !WLOOP) load_hconst();
 
   // ---- per-lane staging state.  A op j of wave w fills tile rows 8(NA w + j) + lane/8,
   //      B op j rows 8(NB w + j) + lane/8; LDS slot lane%8 of a row holds k-vector
@@ -447,6 +467,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // m_base - W - 1 + row of the flattened batch, zero outside it)
   _Float16* const Bring = WIN ? smem + 2 * kWinRows * BK : smem;
   _Float16* const zarea = smem + 2 * kWinRows * BK + kPNS * BN * BK;
+  _Float16* const jarea = zarea + 8 * BK;
+  typedef __attribute__((address_space(3))) char lds_char;
+  lds_char* const lds0 = (lds_char*)(lds_ptr_t)smem_raw;
   const int wr = BM + 2 * a.iw + 2;              // window rows used
   const int npix = a.n * a.ih * a.iw;
   const int ncb = a.cin / BKE;
@@ -604,6 +627,53 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 #pragma unroll
     for (int t = 0; t < FN; ++t) fb1[t] = *(const h8*)(S + b_row + t * 16 * BK + so1);
   };
+  // WLOOP read side.  The tap TT of a K-block is a compile-time constant: its row shift
+  // sh = kh * W + kw is one scalar, the 16-byte slot g ^ ((row + sh) & 7) comes from a
+  // per-lane table of the 8 residues (3 bits each), and the fragment blocks tm = 1..3 are
+  // ds_read immediate offsets (tm * 2048).  An out-of-image tap reads the zero area: its
+  // address is zb - tm * 2048, so address + immediate = zb (half 1: zb ^ 64, both inside
+  // the 1 KB zero area; 2048 tm and the window parity offset are multiples of 128, so the
+  // half-1 XOR commutes with them).
+  const int zb = (2 * kWinRows * BK + kPNS * BN * BK) * 2;
+  uint32_t wtab = 0;
+  if constexpr (WLOOP) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) wtab |= (uint32_t)((g ^ ((wm * (BM / WM) + fr + r) & 7)) & 7) << (3 * r);
+  }
+  const int lrow = (wm * (BM / WM) + fr) * BK * 2;
+  // The per-tap values derive from a loop-carried zero (zo *= a.pipe_z, which the host keeps
+  // 0; the compiler cannot know it), advanced in every body: otherwise the compiler hoists
+  // the 9 taps' shifts, weight-column offsets and tap-validity masks out of the channel-block
+  // loop, and the SGPRs / VGPRs they need spill (VGPR-lane reloads in the loop, scratch
+  // reloads whose vmcnt(0) drain the LDS-DMA pipeline).
+  int zo = a.pipe_z;
+  auto waddr = [&](auto tt_, int par) {
+    constexpr int TT = decltype(tt_)::value, KH = TT / 3, KW = TT % 3;
+    zo *= a.pipe_z;  // (a product, not a sum: an affine zo would be strength-reduced into
+                     // one induction register per derived value)
+    const int iw_o = a.iw + zo;
+    const int sh = KH * iw_o + KW;
+    const int off = lrow + ((par * kWinRows + sh) << 7) + (int)(((wtab >> (3 * (sh & 7))) & 7u) << 4);
+#pragma unroll
+    for (int tm = 0; tm < FM; ++tm) {
+      const int keep = (int)(amask[tm] << (31 - TT + zo)) >> 31;  // 0 / -1: tap TT valid for this row
+      aoff[tm] = (off & keep) | ((zb - tm * 2048) & ~keep);
+    }
+  };
+  auto wread0 = [&](auto buf_) {
+    const _Float16* S = Bring + decltype(buf_)::value * kPStage;
+#pragma unroll
+    for (int t = 0; t < FM; ++t) fa0[t] = *(const h8*)(smem_raw + aoff[t] + t * 2048);
+#pragma unroll
+    for (int t = 0; t < FN; ++t) fb0[t] = *(const h8*)(S + b_row + t * 16 * BK + so0);
+  };
+  auto wread1 = [&](auto buf_) {
+    const _Float16* S = Bring + decltype(buf_)::value * kPStage;
+#pragma unroll
+    for (int t = 0; t < FM; ++t) fa1[t] = *(const h8*)(smem_raw + (aoff[t] ^ 64) + t * 2048);
+#pragma unroll
+    for (int t = 0; t < FN; ++t) fb1[t] = *(const h8*)(S + b_row + t * 16 * BK + so1);
+  };
   constexpr int NMF = FM * FN, NRD = FM + FN;
   // MFMA / DS-read interleave of one cluster: NRD reads spread over the NMF MFMAs
   auto interleave_reads = [&]() {
@@ -619,7 +689,10 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // wait for 0
   // (cross-tile prefetch: the previous tile of this workgroup issued them before its
   // epilogue, whose exactly EPI vector-memory ops are younger than K-block NSt-2)
-  if constexpr (WIN && !PP) win_addr();
+  if constexpr (WLOOP)
+    waddr(std::integral_constant<int, 0>{}, 0);
+  else if constexpr (WIN && !PP)
+    win_addr();
   // the tile cursor past the prologue's NSt-1 K-blocks (issued here or by the previous tile)
   auto skip_prologue = [&]() {
 #pragma unroll
@@ -652,7 +725,10 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   if constexpr (!PP) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    read0(0);
+    if constexpr (WLOOP)
+      wread0(std::integral_constant<int, 0>{});
+    else
+      read0(0);
   }
 
   // Cluster A (half 0 of kb): MFMAs on fa0/fb0, interleaved with the reads of half 1
@@ -719,7 +795,108 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  if constexpr (!(ABL & 32) && !PP) {
+  // ---- WLOOP: window mode with the 9 taps of a channel block unrolled.  K-block s = 9 cb + t
+  //      with t a compile-time constant in each body, so everything the generic loop derives
+  //      from its cursor per K-block is fixed: the tap's row shift (waddr), the ring stage
+  //      (s % 3 = t % 3: 9 K-blocks per channel block), the K-block staged with it (s + 2:
+  //      tap (t + 2) % 9) and its window slice (slice t of channel block cb + 1's window for
+  //      t <= 6, none for t = 7, 8: no dummy loads), and so the counted vmcnt.  The last
+  //      channel block (no next window; nothing to stage after tap 6) is its own unrolled
+  //      copy.  Per wave and K-block the generic loop spent ~40 SALU + ~25 VALU on cursor,
+  //      window-op and address arithmetic, serially between two MFMAs; here one VALU per
+  //      window op and the fragment address selects remain.  Every accumulator sees the
+  //      same MFMA sequence: bit-identical to the generic loop.
+  if constexpr (WLOOP && !(ABL & 32)) {
+    auto wbody = [&](auto t_, auto stg_, auto wop_, auto nxt_, int cb) {
+      constexpr int T = decltype(t_)::value;
+      constexpr bool STG = decltype(stg_)::value, WOP = decltype(wop_)::value, NXT = decltype(nxt_)::value;
+      constexpr int VMS = STG ? NB + (WOP ? 1 : 0) : 0;  // ops of K-block s + 2 issued here
+      if constexpr (!(ABL & 2)) wread1(std::integral_constant<int, T % 3>{});
+      if constexpr (!NXT) {  // the tile's last K-block: the epilogue constants
+        if constexpr (REG) load_rb();
+        if constexpr (HEAD) load_hconst();
+      }
+      if constexpr (STG && !(ABL & 1)) {
+        if constexpr (WOP) {
+          // slice T of channel block cb + 1's window: one VALU add.  Rows before / past the
+          // batch are out of the buffer's range (zeros); rows past the window (>= wr) load
+          // data no tap reads, except a slice wholly past it, which is pushed out of range by
+          // the scalar 2^31 (pipe_win_ok: input < 2^30 bytes, so even the first tile's
+          // negative offsets stay out of range); rows past kWinRows go to the junk area.
+          const int cw = cb + 1;
+          const int r0 = 64 * T + 8 * wid;
+          // (the destination as an LDS byte offset: a select of two generic LDS pointers
+          // makes the compiler emit an illegal null check of the shared aperture)
+          const int dofs = r0 < kWinRows ? ((cw & 1) * kWinRows + r0) * BK * 2 : (int)((jarea - smem) * 2);
+          const int so = (64 * T * (a.in_cs + zo) + cw * BKE) * ES + (64 * T < wr ? 0 : (int)0x80000000);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(lds0 + dofs), 16, G0.wv0 + so, 0, 0, 0);
+        }
+        constexpr int T2 = (T + 2) % 9;
+        const int koff = G0.koff_n + (T2 * (a.cin + zo) + (cb + (T >= 7 ? 1 : 0)) * BKE) * ES;
+        _Float16* Bs = Bring + ((T + 2) % 3) * kPStage;
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j],
+                                                   koff, 0, 0);
+      }
+#pragma unroll
+      for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < FN; ++tn) acc[tm][tn] = mfma(fa0[tm], fb0[tn], acc[tm][tn]);
+      if constexpr (STG && !(ABL & 1)) {
+        constexpr int half = NMF / 2;
+        constexpr int per_r = half / NRD > 0 ? half / NRD : 1;
+        constexpr int per_v = (NMF - half) / VMS > 0 ? (NMF - half) / VMS : 1;
+#pragma unroll
+        for (int i = 0; i < NRD; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, per_r, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < VMS; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, per_v, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
+      } else {
+        interleave_reads();
+        __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NXT) {
+        waddr(std::integral_constant<int, (T + 1) % 9>{}, (cb + (T == 8 ? 1 : 0)) & 1);
+        // retire K-block s + 1 (s + 2 stays in flight); lgkmcnt(0): this stage's reads are
+        // done in every wave before any wave restages it
+        if constexpr (!(ABL & 4)) {
+          wait_vm_lgkm0<VMS>();
+          __builtin_amdgcn_s_barrier();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(ABL & 2)) wread0(std::integral_constant<int, (T + 1) % 3>{});
+      }
+#pragma unroll
+      for (int tm = 0; tm < FM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < FN; ++tn) acc[tm][tn] = mfma(fa1[tm], fb1[tn], acc[tm][tn]);
+      if constexpr (NXT) interleave_reads();
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    int cb = 0;
+    for (; cb < ncb - 1; ++cb)
+      unroll_seq(
+          [&](auto t_) {
+            constexpr int T = decltype(t_)::value;
+            wbody(t_, T_{}, std::bool_constant<(T <= 6)>{}, T_{}, cb);
+          },
+          std::make_integer_sequence<int, 9>{});
+    unroll_seq(
+        [&](auto t_) {
+          constexpr int T = decltype(t_)::value;
+          wbody(t_, std::bool_constant<(T <= 6)>{}, F_{}, std::bool_constant<(T <= 7)>{}, cb);
+        },
+        std::make_integer_sequence<int, 9>{});
+  } else if constexpr (!(ABL & 32) && !PP) {
     int kb = 0;
     for (; kb + NSt - 1 < nk; ++kb) body(T_{}, T_{});  // stages kb + NSt - 1
     for (; kb + 1 < nk; ++kb) body(F_{}, T_{});        // tail: nothing left to stage (waits vmcnt(0))
@@ -808,7 +985,12 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   if constexpr (REG) {
     if (pf) {
       if (next >= 0) {  // prefetch the next tile's prologue under this tile's epilogue
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // (WLOOP: the bias loads of the last K-block body are the only older vector-memory
+        // ops; retired here, so the epilogue's use of them never waits on the prefetch)
+        if constexpr (WLOOP)
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave is past its last fragment read
         __builtin_amdgcn_sched_barrier(0);
         prologue_issue(make_geo(next));
@@ -1165,7 +1347,8 @@ static int g_pipe_win = 1;
 void set_pipe_win(int v) { g_pipe_win = v ? 1 : 0; }
 static bool pipe_win_ok(const ConvArgs& a, int bm) {
   return g_pipe_win && bm == 256 && a.cin % 64 == 0 && a.ks == 3 && a.stride == 1 && a.pad == 1 && !a.quad && a.pipe_corder &&
-         a.ih == a.oh && a.iw == a.ow && bm + 2 * a.iw + 2 <= kWinRows;
+         a.ih == a.oh && a.iw == a.ow && bm + 2 * a.iw + 2 <= kWinRows &&
+         (int64_t)a.n * a.ih * a.iw * a.in_cs * 2 < (1ll << 30);  // (the window op's 2^31 skip)
 }
 
 // Cross-tile prefetch (register-epilogue layers): a workgroup issues its next tile's
@@ -1186,6 +1369,10 @@ void set_pipe_pp(int v) { g_pipe_pp = v ? 1 : 0; }
 // Default 2: yolov4-tiny@608 b64 L12 (8 N-panels) fetches 39 % fewer bytes past L2 (PMC
 // FETCH_SIZE, r03l) at the same time (0.2007 vs 0.2009 ms).
 static int g_pipe_walk = 2;
+// Window-mode K-loop: 1 = taps unrolled (WLOOP, default), 0 = the generic cursor loop (ABL bit
+// 4096, A/B diagnostics).  rtdm_set_tuning("conv_pipe_wloop", v); bit-identical either way.
+static int g_pipe_wloop = 1;
+void set_pipe_wloop(int v) { g_pipe_wloop = v ? 1 : 0; }
 void set_pipe_walk(int v) { g_pipe_walk = v > 0 ? v : 0; }
 static int pipe_walk_g(const ConvArgs& a) {
   const int ntn = a.cout_pad / kPBN;
@@ -1245,10 +1432,28 @@ static void launch_abl(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int nt
   }
 }
 
+// the generic-cursor window loop (ABL bit 4096), 256-row tiles only
+template <template <int, int> class K, int BM>
+static void launch_abl_w0(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int nt, int pf) {
+  if constexpr (BM == 256) {
+    switch (abl) {
+      case 8: K<8 | 4096, BM>::go(g, s, a, nt, pf); break;
+      case 128: K<128 | 4096, BM>::go(g, s, a, nt, pf); break;
+      case 384: K<384 | 4096, BM>::go(g, s, a, nt, pf); break;
+      case 640: K<640 | 4096, BM>::go(g, s, a, nt, pf); break;
+      case 896: K<896 | 4096, BM>::go(g, s, a, nt, pf); break;
+      case 1024: K<1024 | 4096, BM>::go(g, s, a, nt, pf); break;
+      default: K<4096, BM>::go(g, s, a, nt, pf); break;
+    }
+  }
+}
+
 template <int BM>
 static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid, bool win) {
   const int abl = pipe_abl(a) | (g_pipe_pp ? 2048 : 0), pf = pipe_pf_ok(a, abl, a.kpad / kPBK) ? 1 : 0;
   if constexpr (BM >= 128) {
+    if (win && BM == 256 && !g_pipe_wloop && !(abl & 2048))
+      return launch_abl_w0<conv_pipew_f16_k, BM>(abl, grid, s, a, ntiles, pf);
     if (win) return launch_abl<conv_pipew_f16_k, BM, true>(abl, grid, s, a, ntiles, pf);
   }
   launch_abl<conv_pipe_f16_k, BM, true>(abl, grid, s, a, ntiles, pf);
@@ -1259,8 +1464,8 @@ static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 gr
 static const char* pipe_name(bool i8, bool win, int abl, int bm) {
   static std::set<std::string> names;
   char b[48];
-  snprintf(b, sizeof b, "conv_pipe%s%s_%s<%d,%d>", win ? "w" : "", (abl & 2048) ? "pp" : "", i8 ? "i8" : "f16",
-           abl & ~2048, bm);
+  snprintf(b, sizeof b, "conv_pipe%s%s_%s<%d,%d>", win ? ((abl & 4096) ? "w0" : "w") : "", (abl & 2048) ? "pp" : "",
+           i8 ? "i8" : "f16", abl & ~(2048 | 4096), bm);
   return names.insert(b).first->c_str();
 }
 
@@ -1269,7 +1474,9 @@ const char* conv_pipe_name(const ConvArgs& a_in) {
   a.pipe_corder = g_pipe_korder_get() && a.ks == 3 && a.cin % 64 == 0 ? 1 : 0;
   const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
   const bool abl_mode = a.head_w || conv_pipe_mode() <= 1 || conv_pipe_mode() == 13;
-  return pipe_name(false, abl_mode && pipe_win_ok(a, bm), pipe_abl(a) | (abl_mode && g_pipe_pp ? 2048 : 0), bm);
+  const bool win = abl_mode && pipe_win_ok(a, bm);
+  return pipe_name(false, win, pipe_abl(a) | (abl_mode && g_pipe_pp ? 2048 : 0) | (win && !g_pipe_wloop && !g_pipe_pp ? 4096 : 0),
+                   bm);
 }
 
 // K order of the implicit GEMM: 0 = tap outer (each tap's whole channel run), 1 = 64-channel

@@ -427,6 +427,33 @@ def test_window_mode_bit_identical(dev, case):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608:3", "yolov3-aider-416@416:3",
+                                  "yolov4-tiny-aider-416@608:16", "yolov4-tiny-3l-512x512@512:5"])
+def test_window_loop_unrolled_bit_identical(dev, case):
+    """conv_pipew's tap-unrolled K-loop (compile-time tap per K-block; default) against the
+    generic cursor loop (rtdm_set_tuning("conv_pipe_wloop", 0)): same io bits.  Batches
+    with tiles spanning image boundaries, the last partial tile, several tiles per
+    workgroup (cross-tile prefetch), single- and multi-channel-block windows."""
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    cfg, rest = case.split("@")
+    size, b = (int(v) for v in rest.split(":"))
+    x = torch.from_numpy(synth_frames(b, size, size, seed=41)).to(dev)
+    outs = {}
+    try:
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 256))  # window mode runs on 256-row tiles
+        for v in (0, 1):
+            L.check(L.lib().rtdm_set_tuning(b"conv_pipe_wloop", v))
+            m, _, _, _ = _detector(cfg, size)
+            outs[v] = m(x)[0].cpu()
+            names = _names(m, b)
+            assert any(n.startswith("conv_pipew0_" if v == 0 else "conv_pipew_") for n in names), names
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_wloop", 1))
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608:16", "yolov3-aider-416@416:12"])
 @pytest.mark.parametrize("bm", [0, 256, 64])
 def test_cross_tile_prefetch_bit_identical(dev, case, bm):

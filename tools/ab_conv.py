@@ -30,9 +30,13 @@ ap.add_argument("--key", default="conv_pipe")
 ap.add_argument("--values", default="0,1")
 ap.add_argument("--rounds", type=int, default=6)
 ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--set", default="", help="fixed tunings applied first: key=v,key=v")
 args = ap.parse_args()
 vals = [int(v) for v in args.values.split(",")]
 lib = L.lib()
+for kv in filter(None, args.set.split(",")):
+    k, v = kv.split("=")
+    L.check(lib.rtdm_set_tuning(k.encode(), int(v)))
 
 text = open(os.path.join(ROOT, "real-time-disaster-management_amd", "rtdm", "cfg", args.cfg + ".cfg")).read()
 stream = synth_darknet_weights(text, calib=load_calibration(args.cfg))
