@@ -47,8 +47,6 @@ rtdm_status rtdm_set_tuning(const char* key, int value) {
       set_pipe_walk(value);
     else if (!strcmp(key, "conv_pipe_wloop"))
       set_pipe_wloop(value);
-    else if (!strcmp(key, "conv_pipe_c32"))
-      set_pipe_c32(value);
     else if (!strcmp(key, "head1x1"))
       set_head1x1(value);
     else if (!strcmp(key, "dw3_tile"))

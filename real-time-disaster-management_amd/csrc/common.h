@@ -193,6 +193,7 @@ struct ConvArgs {
   int glds_uni = 0;              // conv_glds_f16: uniform-tap staging (set by launch_conv)
   int pipe_corder = 0;           // conv_pipe_f16: channel-block-outer K order (set by launch_conv_pipe)
   int pipe_g = 0;                // conv_pipe: N-panels per tile-walk group (0: M-major walk; set at launch)
+  int pipe_u = 1;                // conv_pipe: tap-unrolled loop for the per-tap-load 3x3 layers (set at launch)
   int pipe_z = 0;                // always 0: conv_pipew's loop-carried opaque zero (keeps per-tap values in the loop)
   Epilogue e;
   // Fused YOLO head (conv_pipe_f16 only): a 1x1 conv over this conv's activated
@@ -227,8 +228,6 @@ int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 
 void set_pipe_bm(int v);                  // 0 = cost model, else forced
 void set_pipe_korder(int v);              // conv_pipe K order: 0 tap outer, 1 channel-block outer
 void set_pipe_win(int v);                 // conv_pipe window mode (3x3 s1 inputs staged once per channel block)
-void set_pipe_c32(int v);                 // conv_pipe for Cin = 32 3x3 convs (two taps per K-block)
-int pipe_c32_enabled();                   // (planner: pad their 64 outputs to one 128-channel tile)
 void set_pipe_wloop(int v);               // conv_pipe window mode: 1 = taps unrolled (default), 0 = cursor loop
 void set_pipe_walk(int v);                // conv_pipe tile walk: N-panels per group (0 = M-major)
 void set_pipe_pp(int v);                  // conv_pipe ping-pong K-loop schedule (f16)

@@ -312,6 +312,10 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // window mode with the taps unrolled (see the WLOOP loop below); ABL bit 4096 selects the
   // generic cursor loop instead (A/B diagnostics)
   constexpr bool WLOOP = WIN && !PP && !(ABL & 4096);
+  // the same tap-unrolled loop for the per-tap-load (non-window) 3x3 layers (channel-block-outer
+  // K order), chosen at run time; 1x1 layers keep the generic cursor loop
+  constexpr bool ULOOP = !PP && !(ABL & 4096) && !(ABL & 32);
+  const bool uloop = ULOOP && (WIN || (a.ks == 3 && a.pipe_corder != 0 && a.pipe_u != 0));
   constexpr bool RES_ = (ABL & 256) != 0;
   // cross-tile prefetch (pf, register epilogue only: the LDS ring is free during it)
   constexpr bool HEAD = (ABL & 8) != 0;
@@ -336,7 +340,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // WLOOP: the register epilogue's bias / the fused head's constants are loaded in the last
   // K-block body (their registers are not live across the loop); elsewhere at the tile start
   if constexpr (REG) {
-    if constexpr (!WLOOP) load_rb();
+    if (!uloop) load_rb();
   } else if constexpr ((ABL & 128) != 0) {
     const int c0 = n_base + (tid % CG) * 8;
     const bool cv = c0 < a.cout;
@@ -376,7 +380,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       hh[tn] = (cv && a.e.scale) ? a.e.shift[col] : 0.f;
     }
   };
-  if constexpr (HEAD && !WLOOP) load_hconst();
+  if (HEAD && !uloop) load_hconst();
 
   // ---- per-lane staging state.  A op j of wave w fills tile rows 8(NA w + j) + lane/8,
   //      B op j rows 8(NB w + j) + lane/8; LDS slot lane%8 of a row holds k-vector
@@ -390,9 +394,6 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   //      Per-tile part (PipeGeo): A row offsets / tap masks, the window origin, the weight
   //      panel; built for this tile and, for the cross-tile prefetch, for the next one. ----
   const int slot = lane & 7;
-  // Cin = 32 (c32): a 64-deep K-block spans two taps (k = tap * 32 + c, tap-major as the
-  // weights are packed): k-vector v of a row is tap 2 kb + (v >> 2), channels 8 (v & 3)..
-  const bool c32 = !WIN && a.cin == 32;
   struct Geo {
     int m_base, koff_n;                // koff_n: byte offset of the tile's weight panel
     int voff_a[WIN ? 1 : NA];
@@ -408,7 +409,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
 #pragma unroll
     for (int j = 0; j < (WIN ? 0 : NA); ++j) {
       const int r = 8 * (NA * wid + j) + (lane >> 3);
-      const int kofs = 16 * ((slot ^ (r & 7)) & (c32 ? 3 : 7));  // bytes
+      const int kofs = 16 * (slot ^ (r & 7));  // bytes
       const int m = G.m_base + r;
       int n = 0, oy = 0, ox = 0;
       if (m < a.M) row_to_pix(a, m, n, oy, ox);
@@ -451,16 +452,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // selected by value (a by-reference select of the counter to bump sends the cursor to
   // scratch, and its loads' vmcnt(0) then drains the LDS-DMA pipeline every K-block).
   const bool corder = a.pipe_corder != 0;
-  const int ni = c32 ? nk : corder ? ntap : cpt;
-  // c32: per A op, whether this lane's k-vector is the K-block's second tap
-  uint32_t c32_hi = 0;
-  if (c32) {
-#pragma unroll
-    for (int j = 0; j < (WIN ? 0 : NA); ++j) {
-      const int r = 8 * (NA * wid + j) + (lane >> 3);
-      c32_hi |= (uint32_t)(((slot ^ (r & 7)) >> 2) & 1) << j;
-    }
-  }
+  const int ni = corder ? ntap : cpt;
   int st_i = 0, st_o = 0, st_buf = 0;
 
   // window mode: buffers, window geometry (rows of the channel block's window: pixels
@@ -500,16 +492,6 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       // j = st_tap - 2 (taps 2..8 -> slices 0..6) of channel block st_c + 1's window
       const int j = st_tap - 2, cw = st_c + 1;
       win_op(G, j < 0 ? 0 : j, cw, j >= 0 && cw < ncb && 64 * j < wr);
-    } else if (c32) {  // taps 2 kb, 2 kb + 1 (kb = st_c); tap 9 is padding (mask bit 0)
-      const int t0 = 2 * st_c, t1 = t0 + 1;
-      const int kh0 = (t0 * 11) >> 5, kw0 = t0 - 3 * kh0, kh1 = (t1 * 11) >> 5, kw1 = t1 - 3 * kh1;
-      const int off0 = (kh0 * a.iw + kw0) * a.in_cs * ES, off1 = (kh1 * a.iw + kw1) * a.in_cs * ES;
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        const bool hi = (c32_hi >> j) & 1u;
-        const int vo = ((G.vmask[j] >> (hi ? t1 : t0)) & 1u) ? G.voff_a[j] + (hi ? off1 : off0) : (int)0x80000000;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(As + 8 * (NA * wid + j) * BK), 16, vo, 0, 0, 0);
-      }
     } else {
       const int tapoff = ((kh * a.iw + kw) * a.in_cs + st_c * BKE) * ES;
 #pragma unroll
@@ -519,7 +501,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       }
     }
     // weight column of this K-block (tap-major packing) in the tile's panel
-    const int koff = G.koff_n + (c32 ? st_c * 64 : st_tap * a.cin + st_c * BKE) * ES;
+    const int koff = G.koff_n + (st_tap * a.cin + st_c * BKE) * ES;
 #pragma unroll
     for (int j = 0; j < NB; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j], koff,
@@ -649,8 +631,6 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   int zo = a.pipe_z;
   auto waddr = [&](auto tt_, int par) {
     constexpr int TT = decltype(tt_)::value, KH = TT / 3, KW = TT % 3;
-    zo *= a.pipe_z;  // (a product, not a sum: an affine zo would be strength-reduced into
-                     // one induction register per derived value)
     const int iw_o = a.iw + zo;
     const int sh = KH * iw_o + KW;
     const int off = lrow + ((par * kWinRows + sh) << 7) + (int)(((wtab >> (3 * (sh & 7))) & 7u) << 4);
@@ -806,18 +786,40 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   //      window-op and address arithmetic, serially between two MFMAs; here one VALU per
   //      window op and the fragment address selects remain.  Every accumulator sees the
   //      same MFMA sequence: bit-identical to the generic loop.
-  if constexpr (WLOOP && !(ABL & 32)) {
+  //      Non-window 3x3 layers (uloop, !WIN): the same unrolled loop with the per-tap A loads
+  //      of conv_pipe (tap offset one scalar, validity bit test per A op) and the A fragments
+  //      at fixed LDS offsets of the compile-time ring stage.
+  if (uloop) {
+    static_assert(ULOOP == false || NSt == 3, "ring stage s % 3 = tap % 3 (9 taps per channel block)");
     auto wbody = [&](auto t_, auto stg_, auto wop_, auto nxt_, int cb) {
       constexpr int T = decltype(t_)::value;
       constexpr bool STG = decltype(stg_)::value, WOP = decltype(wop_)::value, NXT = decltype(nxt_)::value;
-      constexpr int VMS = STG ? NB + (WOP ? 1 : 0) : 0;  // ops of K-block s + 2 issued here
-      if constexpr (!(ABL & 2)) wread1(std::integral_constant<int, T % 3>{});
+      constexpr int VMS = STG ? NB + (WIN ? (WOP ? 1 : 0) : NA) : 0;  // ops of K-block s + 2 issued here
+      zo *= a.pipe_z;  // (a product, not a sum: an affine zo would be strength-reduced into
+                       // one induction register per derived value)
+      if constexpr (!(ABL & 2)) {
+        if constexpr (WIN)
+          wread1(std::integral_constant<int, T % 3>{});
+        else
+          read1(T % 3);
+      }
       if constexpr (!NXT) {  // the tile's last K-block: the epilogue constants
         if constexpr (REG) load_rb();
         if constexpr (HEAD) load_hconst();
       }
+      if constexpr (STG && !(ABL & 1) && !WIN) {
+        // A: tap (T + 2) % 9 of channel block cb + (T >= 7); out-of-image taps load zeros
+        constexpr int T2 = (T + 2) % 9, KH2 = T2 / 3, KW2 = T2 % 3;
+        const int tapoff = ((KH2 * (a.iw + zo) + KW2) * (a.in_cs + zo) + (cb + (T >= 7 ? 1 : 0)) * BKE) * ES;
+        _Float16* As = smem + ((T + 2) % 3) * kPStage;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+          const int vo = ((G0.vmask[j] >> (T2 + zo)) & 1u) ? G0.voff_a[j] + tapoff : (int)0x80000000;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(As + 8 * (NA * wid + j) * BK), 16, vo, 0, 0, 0);
+        }
+      }
       if constexpr (STG && !(ABL & 1)) {
-        if constexpr (WOP) {
+        if constexpr (WIN && WOP) {
           // slice T of channel block cb + 1's window: one VALU add.  Rows before / past the
           // batch are out of the buffer's range (zeros); rows past the window (>= wr) load
           // data no tap reads, except a slice wholly past it, which is pushed out of range by
@@ -833,7 +835,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
         }
         constexpr int T2 = (T + 2) % 9;
         const int koff = G0.koff_n + (T2 * (a.cin + zo) + (cb + (T >= 7 ? 1 : 0)) * BKE) * ES;
-        _Float16* Bs = Bring + ((T + 2) % 3) * kPStage;
+        _Float16* Bs = WIN ? Bring + ((T + 2) % 3) * kPStage : smem + ((T + 2) % 3) * kPStage + BM * BK;
 #pragma unroll
         for (int j = 0; j < NB; ++j)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j],
@@ -864,7 +866,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (NXT) {
-        waddr(std::integral_constant<int, (T + 1) % 9>{}, (cb + (T == 8 ? 1 : 0)) & 1);
+        if constexpr (WIN) waddr(std::integral_constant<int, (T + 1) % 9>{}, (cb + (T == 8 ? 1 : 0)) & 1);
         // retire K-block s + 1 (s + 2 stays in flight); lgkmcnt(0): this stage's reads are
         // done in every wave before any wave restages it
         if constexpr (!(ABL & 4)) {
@@ -872,7 +874,12 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
           __builtin_amdgcn_s_barrier();
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!(ABL & 2)) wread0(std::integral_constant<int, (T + 1) % 3>{});
+        if constexpr (!(ABL & 2)) {
+          if constexpr (WIN)
+            wread0(std::integral_constant<int, (T + 1) % 3>{});
+          else
+            read0((T + 1) % 3);
+        }
       }
 #pragma unroll
       for (int tm = 0; tm < FM; ++tm)
@@ -896,7 +903,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
           wbody(t_, std::bool_constant<(T <= 6)>{}, F_{}, std::bool_constant<(T <= 7)>{}, cb);
         },
         std::make_integer_sequence<int, 9>{});
-  } else if constexpr (!(ABL & 32) && !PP) {
+  } else if constexpr (!(ABL & 32) && !PP && !WLOOP) {
     int kb = 0;
     for (; kb + NSt - 1 < nk; ++kb) body(T_{}, T_{});  // stages kb + NSt - 1
     for (; kb + 1 < nk; ++kb) body(F_{}, T_{});        // tail: nothing left to stage (waits vmcnt(0))
@@ -987,7 +994,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       if (next >= 0) {  // prefetch the next tile's prologue under this tile's epilogue
         // (WLOOP: the bias loads of the last K-block body are the only older vector-memory
         // ops; retired here, so the epilogue's use of them never waits on the prefetch)
-        if constexpr (WLOOP)
+        if (uloop)
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         else
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1253,20 +1260,10 @@ __global__ __launch_bounds__(512, 1) void conv_pipew_i8(ConvArgs a, int ntiles, 
   pipe_walk<ABL, BM, true, true>(a, smem_raw, ntiles, pf != 0);
 }
 
-// Cin = 32 3x3 convs (c32 staging, two taps per K-block; Darknet-53's L1 / L3) when
-// rtdm_set_tuning("conv_pipe_c32", 1).  Off by default: their 64 outputs fill half of the
-// 128-channel N tile and K is only 5 K-blocks -- yolov3@416 b16 L1 0.118 -> 0.156 ms,
-// L3 0.141 -> 0.193 ms against conv_mfma_f16 (r03m)
-static int g_pipe_c32 = 0;
-void set_pipe_c32(int v) { g_pipe_c32 = v ? 1 : 0; }
-int pipe_c32_enabled() { return g_pipe_c32; }
-static bool pipe_c32(const ConvArgs& a) { return a.cin == 32 && a.ks == 3 && a.kpad == 320; }
-
 bool conv_pipe_ok(const ConvArgs& a) {
   if (!a.zero || a.in_kind != IN_NHWC || a.w_f32 || (a.in_cs | a.in_co) % 8 != 0) return false;
-  const bool c32 = g_pipe_c32 && pipe_c32(a) && !a.head_w;
-  if ((a.cin % 64 != 0 && !c32) || a.cout_pad % kPBN != 0 || (a.ks != 1 && a.ks != 3)) return false;
-  if (a.kpad != a.ks * a.ks * a.cin && !c32) return false;
+  if (a.cin % 64 != 0 || a.cout_pad % kPBN != 0 || (a.ks != 1 && a.ks != 3)) return false;
+  if (a.kpad != a.ks * a.ks * a.cin) return false;
   const int64_t elems = (int64_t)a.n * a.ih * a.iw * a.in_cs;
   if (elems >= (1ll << 30) || (int64_t)a.cout_pad * a.kpad * 2 >= (1ll << 31)) return false;
   if (a.head_w) {  // fused head: one N tile, head K = 128, output only through the head
@@ -1369,10 +1366,17 @@ void set_pipe_pp(int v) { g_pipe_pp = v ? 1 : 0; }
 // Default 2: yolov4-tiny@608 b64 L12 (8 N-panels) fetches 39 % fewer bytes past L2 (PMC
 // FETCH_SIZE, r03l) at the same time (0.2007 vs 0.2009 ms).
 static int g_pipe_walk = 2;
-// Window-mode K-loop: 1 = taps unrolled (WLOOP, default), 0 = the generic cursor loop (ABL bit
-// 4096, A/B diagnostics).  rtdm_set_tuning("conv_pipe_wloop", v); bit-identical either way.
+// 3x3 K-loops: 1 = taps unrolled (default: WLOOP for window mode, the run-time uloop path for
+// the per-tap-load layers), 0 = the generic cursor loop (window mode: ABL bit 4096; A/B
+// diagnostics).  rtdm_set_tuning("conv_pipe_wloop", v); bit-identical either way.
+// Per epilogue (pipe_unroll): the unrolled loop for the register-epilogue layers only.  The
+// LDS C-tile epilogues (pooled / upsampled outputs, ABL 128 / 384) and the fused head (ABL 8)
+// measured 2-3 % slower with it at b64 (r03aa: L6 0.1047 -> 0.1081 ms, L28 0.2592 -> 0.2662):
+// their kernels hold more registers across the loop and the unrolled loop's spill reloads
+// land in the tile prologue.
 static int g_pipe_wloop = 1;
 void set_pipe_wloop(int v) { g_pipe_wloop = v ? 1 : 0; }
+static bool pipe_unroll(int abl) { return g_pipe_wloop && (abl & 512) != 0; }
 void set_pipe_walk(int v) { g_pipe_walk = v > 0 ? v : 0; }
 static int pipe_walk_g(const ConvArgs& a) {
   const int ntn = a.cout_pad / kPBN;
@@ -1452,7 +1456,7 @@ template <int BM>
 static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid, bool win) {
   const int abl = pipe_abl(a) | (g_pipe_pp ? 2048 : 0), pf = pipe_pf_ok(a, abl, a.kpad / kPBK) ? 1 : 0;
   if constexpr (BM >= 128) {
-    if (win && BM == 256 && !g_pipe_wloop && !(abl & 2048))
+    if (win && BM == 256 && !pipe_unroll(abl) && !(abl & 2048))
       return launch_abl_w0<conv_pipew_f16_k, BM>(abl, grid, s, a, ntiles, pf);
     if (win) return launch_abl<conv_pipew_f16_k, BM, true>(abl, grid, s, a, ntiles, pf);
   }
@@ -1475,7 +1479,8 @@ const char* conv_pipe_name(const ConvArgs& a_in) {
   const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
   const bool abl_mode = a.head_w || conv_pipe_mode() <= 1 || conv_pipe_mode() == 13;
   const bool win = abl_mode && pipe_win_ok(a, bm);
-  return pipe_name(false, win, pipe_abl(a) | (abl_mode && g_pipe_pp ? 2048 : 0) | (win && !g_pipe_wloop && !g_pipe_pp ? 4096 : 0),
+  return pipe_name(false, win,
+                   pipe_abl(a) | (abl_mode && g_pipe_pp ? 2048 : 0) | (win && !pipe_unroll(pipe_abl(a)) && !g_pipe_pp ? 4096 : 0),
                    bm);
 }
 
@@ -1489,6 +1494,7 @@ void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
   ConvArgs a = a_in;
   a.pipe_corder = g_pipe_korder && a.ks == 3 && a.cin % 64 == 0 ? 1 : 0;
   a.pipe_g = pipe_walk_g(a);
+  a.pipe_u = pipe_unroll(pipe_abl(a)) ? 1 : 0;
   const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
   const int64_t nt = (int64_t)((a.M + bm - 1) / bm) * (a.cout_pad / kPBN);
   RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
@@ -1514,6 +1520,23 @@ void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
     case 22: hipLaunchKernelGGL((conv_pipe_f16<2050, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
     case 23: hipLaunchKernelGGL((conv_pipe_f16<2051, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
     case 24: hipLaunchKernelGGL((conv_pipe_f16<2064, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+    // tap-unrolled window loop ablations (diagnostics; window-mode register-epilogue layers
+    // only, every other layer runs its normal kernel): 31 no LDS-DMA loads, 32 no fragment
+    // reads, 33 neither, 34 no wait + barrier
+    case 31:
+    case 32:
+    case 33:
+    case 34:
+      if (pipe_win_ok(a, 256) && pipe_abl(a) == 640) {
+        switch (conv_pipe_mode()) {
+          case 31: hipLaunchKernelGGL((conv_pipew_f16<641, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+          case 32: hipLaunchKernelGGL((conv_pipew_f16<642, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+          case 33: hipLaunchKernelGGL((conv_pipew_f16<643, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+          default: hipLaunchKernelGGL((conv_pipew_f16<644, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+        }
+        break;
+      }
+      [[fallthrough]];
     default: {
       const bool win = pipe_win_ok(a, bm);
       if (bm == 256)
@@ -1552,6 +1575,7 @@ void launch_conv_pipe_i8(const ConvArgs& a_in, hipStream_t s) {
   RTDM_REQUIRE(conv_pipe_i8_ok(a), RTDM_E_INVALID, "conv_pipe_i8: unsupported layer");
   a.pipe_corder = g_pipe_korder && a.ks == 3 ? 1 : 0;
   a.pipe_g = pipe_walk_g(a);
+  a.pipe_u = pipe_unroll(pipe_abl(a)) ? 1 : 0;
   const int bm = pipe_bm_nk(a, a.kpad / 128);
   const int64_t nt = (int64_t)((a.M + bm - 1) / bm) * (a.cout_pad / kPBN);
   RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");

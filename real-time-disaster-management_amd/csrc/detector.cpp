@@ -742,11 +742,6 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     const int pad_to = use_mfma && st.yolo >= 0 && !st.head && !st.acff && filters <= 128 && st.cin % 64 == 0 &&
                                (size == 1 || size == 3)
                            ? 128
-                       // Cin = 32 3x3 convs to 64 channels (Darknet-53 L1 / L3): one padded
-                       // 128-channel N tile so conv_pipe's two-taps-per-K-block staging takes them
-                       : use_mfma && pipe_c32_enabled() && st.cin == 32 && size == 3 && filters == 64 && !st.acff &&
-                               st.yolo < 0
-                           ? 128
                            : 0;
     if (weights) {
       std::vector<double> sc(filters, 1.0);

@@ -428,26 +428,31 @@ def test_window_mode_bit_identical(dev, case):
 
 
 @pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608:3", "yolov3-aider-416@416:3",
-                                  "yolov4-tiny-aider-416@608:16", "yolov4-tiny-3l-512x512@512:5"])
+                                  "yolov4-tiny-aider-416@608:16", "yolov4-tiny-3l-512x512@512:5",
+                                  "yolov4-tiny-aider-416@608:8:0", "yolov3-aider-416@416:4:0"])
 def test_window_loop_unrolled_bit_identical(dev, case):
-    """conv_pipew's tap-unrolled K-loop (compile-time tap per K-block; default) against the
-    generic cursor loop (rtdm_set_tuning("conv_pipe_wloop", 0)): same io bits.  Batches
-    with tiles spanning image boundaries, the last partial tile, several tiles per
-    workgroup (cross-tile prefetch), single- and multi-channel-block windows."""
+    """The tap-unrolled 3x3 K-loops (compile-time tap per K-block; default) against the
+    generic cursor loop (rtdm_set_tuning("conv_pipe_wloop", 0)): same io bits, for the
+    window kernels (conv_pipew) and the per-tap-load kernels (conv_pipe, 256 / 128 / 64-row
+    tiles: the ":0" cases use the cost model's tiles).  Batches with tiles spanning image
+    boundaries, the last partial tile, several tiles per workgroup (cross-tile prefetch),
+    single- and multi-channel-block windows."""
     from rtdm import _lib as L
     from rtdm.synth import synth_frames
     cfg, rest = case.split("@")
-    size, b = (int(v) for v in rest.split(":"))
+    size, b, *bm = (int(v) for v in rest.split(":"))
+    bm = bm[0] if bm else 256  # window mode runs on 256-row tiles
     x = torch.from_numpy(synth_frames(b, size, size, seed=41)).to(dev)
     outs = {}
     try:
-        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 256))  # window mode runs on 256-row tiles
+        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", bm))
         for v in (0, 1):
             L.check(L.lib().rtdm_set_tuning(b"conv_pipe_wloop", v))
             m, _, _, _ = _detector(cfg, size)
             outs[v] = m(x)[0].cpu()
             names = _names(m, b)
-            assert any(n.startswith("conv_pipew0_" if v == 0 else "conv_pipew_") for n in names), names
+            if bm == 256:
+                assert any(n.startswith("conv_pipew0_" if v == 0 else "conv_pipew_") for n in names), names
     finally:
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe_wloop", 1))
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))

@@ -104,7 +104,9 @@ def _dist_worker(rank, world, port, q):
         # patterns), unpacked on rank 0
         from rtdm.distributed import gather_records
         from rtdm.pipeline import TwoStagePipeline, unpack_record
-        pipe = TwoStagePipeline(None, None, max_det=7)
+        # (a detector placeholder: the layout has det / idx / count fields only with one;
+        # record_layout reads nothing else from it)
+        pipe = TwoStagePipeline(None, object(), max_det=7)
         lay, total_len = pipe.record_layout(c)
         mine = unpack_record(torch.zeros(total_len), pipe, c)
         mine["logits"][:] = torch.arange(c * 5, dtype=torch.float32).view(c, 5) + 100 * rank
