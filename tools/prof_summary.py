@@ -52,6 +52,8 @@ def main():
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     db = os.path.join(a.gpurun, f"prof_{a.tag}", "run_results.db")
+    if not os.path.exists(db):  # PMC passes only: their own kernel trace gives the launch times
+        db = os.path.join(a.gpurun, f"pmc_FETCH_SIZE_{a.tag}", "run_results.db")
     rows = kernel_rows(db)
     agg = {}
     for name, dur in rows:
