@@ -77,6 +77,8 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
     asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
   else if constexpr (N == 2)
     asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 1)
+    asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
   else
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
@@ -794,7 +796,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     auto wbody = [&](auto t_, auto stg_, auto wop_, auto nxt_, int cb) {
       constexpr int T = decltype(t_)::value;
       constexpr bool STG = decltype(stg_)::value, WOP = decltype(wop_)::value, NXT = decltype(nxt_)::value;
-      constexpr int VMS = STG ? NB + (WIN ? (WOP ? 1 : 0) : NA) : 0;  // ops of K-block s + 2 issued here
+      // ops of K-block s + 2 issued here (ABL bits 8192 / 16384: diagnostics without the window
+      // slices / without the B loads)
+      constexpr int VMS = STG ? ((ABL & 16384) ? 0 : NB) + (WIN ? (WOP && !(ABL & 8192) ? 1 : 0) : NA) : 0;
       zo *= a.pipe_z;  // (a product, not a sum: an affine zo would be strength-reduced into
                        // one induction register per derived value)
       if constexpr (!(ABL & 2)) {
@@ -819,7 +823,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
         }
       }
       if constexpr (STG && !(ABL & 1)) {
-        if constexpr (WIN && WOP) {
+        if constexpr (WIN && WOP && !(ABL & 8192)) {
           // slice T of channel block cb + 1's window: one VALU add.  Rows before / past the
           // batch are out of the buffer's range (zeros); rows past the window (>= wr) load
           // data no tap reads, except a slice wholly past it, which is pushed out of range by
@@ -837,7 +841,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
         const int koff = G0.koff_n + (T2 * (a.cin + zo) + (cb + (T >= 7 ? 1 : 0)) * BKE) * ES;
         _Float16* Bs = WIN ? Bring + ((T + 2) % 3) * kPStage : smem + ((T + 2) % 3) * kPStage + BM * BK;
 #pragma unroll
-        for (int j = 0; j < NB; ++j)
+        for (int j = 0; j < ((ABL & 16384) ? 0 : NB); ++j)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_ptr_t)(Bs + 8 * (NB * wid + j) * BK), 16, voff_b[j],
                                                    koff, 0, 0);
       }
@@ -848,7 +852,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       if constexpr (STG && !(ABL & 1)) {
         constexpr int half = NMF / 2;
         constexpr int per_r = half / NRD > 0 ? half / NRD : 1;
-        constexpr int per_v = (NMF - half) / VMS > 0 ? (NMF - half) / VMS : 1;
+        constexpr int per_v = VMS > 0 && (NMF - half) / VMS > 0 ? (NMF - half) / VMS : 1;
 #pragma unroll
         for (int i = 0; i < NRD; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, per_r, 0);
@@ -1522,16 +1526,21 @@ void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
     case 24: hipLaunchKernelGGL((conv_pipe_f16<2064, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
     // tap-unrolled window loop ablations (diagnostics; window-mode register-epilogue layers
     // only, every other layer runs its normal kernel): 31 no LDS-DMA loads, 32 no fragment
-    // reads, 33 neither, 34 no wait + barrier
+    // reads, 33 neither, 34 no wait + barrier, 35 no window-slice loads (B loads kept), 36 no B
+    // loads (window slices kept)
     case 31:
     case 32:
     case 33:
     case 34:
+    case 35:
+    case 36:
       if (pipe_win_ok(a, 256) && pipe_abl(a) == 640) {
         switch (conv_pipe_mode()) {
           case 31: hipLaunchKernelGGL((conv_pipew_f16<641, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
           case 32: hipLaunchKernelGGL((conv_pipew_f16<642, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
           case 33: hipLaunchKernelGGL((conv_pipew_f16<643, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+          case 35: hipLaunchKernelGGL((conv_pipew_f16<640 | 8192, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
+          case 36: hipLaunchKernelGGL((conv_pipew_f16<640 | 16384, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
           default: hipLaunchKernelGGL((conv_pipew_f16<644, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
         }
         break;
