@@ -134,7 +134,9 @@ const char* rtdm_build_arch(void);
  * (default; 0 changes the fp32 summation order); "conv_pipe_pf" 1 = cross-tile
  * prologue prefetch (default; not with ping-pong); "conv_pipe_pp" 1 = ping-pong
  * K-loop (two wave groups alternating MFMA and memory phases; default 0: measured
- * 4-18 % slower per layer).                                       */
+ * 4-18 % slower per layer); "conv_pipe_wloop" 1 = tap-unrolled
+ * 3x3 K-loop for the register-epilogue layers (default), 0 = the cursor loop;
+ * "conv_pipe_walk" g = tile walk in N-groups of g panels (default 2, 0 = M-major). */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 
 /* ---- classifier ------------------------------------------------------------ */
