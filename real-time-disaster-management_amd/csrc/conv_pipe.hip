@@ -834,8 +834,10 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
           // (the destination as an LDS byte offset: a select of two generic LDS pointers
           // makes the compiler emit an illegal null check of the shared aperture)
           const int dofs = r0 < kWinRows ? ((cw & 1) * kWinRows + r0) * BK * 2 : (int)((jarea - smem) * 2);
-          const int so = (64 * T * (a.in_cs + zo) + cw * BKE) * ES + (64 * T < wr ? 0 : (int)0x80000000);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(lds0 + dofs), 16, G0.wv0 + so, 0, 0, 0);
+          // (offsets in unsigned arithmetic: with the 2^31 skip the sum wraps by design)
+          const uint32_t so = (uint32_t)((64 * T * (a.in_cs + zo) + cw * BKE) * ES) + (64 * T < wr ? 0u : 0x80000000u);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (lds_ptr_t)(lds0 + dofs), 16, (int)((uint32_t)G0.wv0 + so), 0, 0,
+                                                   0);
         }
         constexpr int T2 = (T + 2) % 9;
         const int koff = G0.koff_n + (T2 * (a.cin + zo) + (cb + (T >= 7 ? 1 : 0)) * BKE) * ES;
