@@ -1303,12 +1303,16 @@ static int g_pipe_bm = 0;
 void set_pipe_bm(int v) { g_pipe_bm = (v == 256 || v == 128 || v == 64) ? v : 0; }
 static int pipe_bm_nk(const ConvArgs& a, int nk);
 int pipe_bm(const ConvArgs& a) { return pipe_bm_nk(a, a.kpad / kPBK); }
+static bool pipe_win_ok(const ConvArgs& a, int bm);
 static int pipe_bm_nk(const ConvArgs& a, int nk) {
   const bool head = a.head_w != nullptr;
   if (g_pipe_bm && !(head && g_pipe_bm == 64)) return g_pipe_bm;
   const int ntn = a.cout_pad / kPBN, cus = pipe_cus();
   static const int bms[3] = {256, 128, 64};
-  static const double eff[3] = {1.0, 0.85, 0.65};
+  // 256-row tiles of window-mode layers run the tap-unrolled window loop: ~1.2x the K-loop
+  // rate of the per-tap-load 256-row tiles (b64 L10 / L14 on 256-row window tiles 0.0614 /
+  // 0.0682 ms against 0.0664 / 0.0710 on the 128-row tiles this model picked without it, r03ak)
+  const double eff[3] = {!head && pipe_win_ok(a, 256) ? 1.2 : 1.0, 0.85, 0.65};
   const double ovh = 3.0 + (head ? 4.0 : 0.0);
   int best = 256;
   double best_t = 1e300;
