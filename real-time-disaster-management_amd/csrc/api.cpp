@@ -45,6 +45,8 @@ rtdm_status rtdm_set_tuning(const char* key, int value) {
       set_pipe_pp(value);
     else if (!strcmp(key, "conv_pipe_walk"))
       set_pipe_walk(value);
+    else if (!strcmp(key, "conv_pipe_cost"))
+      set_pipe_cost(value);
     else if (!strcmp(key, "conv_pipe_wloop"))
       set_pipe_wloop(value);
     else if (!strcmp(key, "head1x1"))

@@ -228,6 +228,7 @@ int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 
 void set_pipe_bm(int v);                  // 0 = cost model, else forced
 void set_pipe_korder(int v);              // conv_pipe K order: 0 tap outer, 1 channel-block outer
 void set_pipe_win(int v);                 // conv_pipe window mode (3x3 s1 inputs staged once per channel block)
+void set_pipe_cost(int v);                // conv_pipe tile-rows objective: 0 latency (rounds), 1 throughput (CU-time)
 void set_pipe_wloop(int v);               // conv_pipe window mode: 1 = taps unrolled (default), 0 = cursor loop
 void set_pipe_walk(int v);                // conv_pipe tile walk: N-panels per group (0 = M-major)
 void set_pipe_pp(int v);                  // conv_pipe ping-pong K-loop schedule (f16)

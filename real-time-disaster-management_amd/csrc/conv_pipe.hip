@@ -1303,6 +1303,13 @@ static int g_pipe_bm = 0;
 void set_pipe_bm(int v) { g_pipe_bm = (v == 256 || v == 128 || v == 64) ? v : 0; }
 static int pipe_bm_nk(const ConvArgs& a, int nk);
 int pipe_bm(const ConvArgs& a) { return pipe_bm_nk(a, a.kpad / kPBK); }
+// Objective of the tile-rows model: 0 = latency (rounds of tiles over the CUs: a launch that
+// has the GPU to itself), 1 = throughput (CU-time: tiles x per-tile time, for several batches
+// in flight whose launches fill each other's idle CUs).  rtdm_set_tuning("conv_pipe_cost", v);
+// bench.py sets 1 with more than one batch in flight.  Throughput favours 256-row tiles:
+// b8 31.8k -> 33.0k, b16 36.9k -> 39.3k frames/s with 4 in flight (r03an, forced 256 rows).
+static int g_pipe_cost = 0;
+void set_pipe_cost(int v) { g_pipe_cost = v ? 1 : 0; }
 static bool pipe_win_ok(const ConvArgs& a, int bm);
 static int pipe_bm_nk(const ConvArgs& a, int nk) {
   const bool head = a.head_w != nullptr;
@@ -1318,7 +1325,7 @@ static int pipe_bm_nk(const ConvArgs& a, int nk) {
   double best_t = 1e300;
   for (int i = 0; i < (head ? 2 : 3); ++i) {
     const int64_t tiles = (int64_t)((a.M + bms[i] - 1) / bms[i]) * ntn;
-    const double rounds = (double)((tiles + cus - 1) / cus);
+    const double rounds = g_pipe_cost ? (double)tiles : (double)((tiles + cus - 1) / cus);
     const double t = rounds * (bms[i] / 256.0 * nk / eff[i] + ovh * bms[i] / 256.0 + 1.0);
     if (t < best_t * 0.97) {
       best_t = t;
