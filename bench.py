@@ -362,7 +362,10 @@ def main():
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in pipes[1:]]
     frames = make_frames(args, first, b, dev)
     rec_len = pipe.record_layout(b)[1]
-    gathered = torch.empty((world, rec_len), device=dev, dtype=torch.float32) if world > 1 and rank == 0 else None
+    # one gather buffer per in-flight pipeline: each pipeline's gather runs on its own stream, so a
+    # shared buffer would be a cross-stream write-after-write between steps in flight
+    gathered = [torch.empty((world, rec_len), device=dev, dtype=torch.float32) for _ in pipes] \
+        if world > 1 and rank == 0 else None
     torch.cuda.synchronize()
 
     def step(k, ev=None):
@@ -372,7 +375,7 @@ def main():
                 ev[0].record()
             out = pipes[j](frames[k % len(frames)])
             if world > 1:
-                gather_records(out["record"], gathered if rank == 0 else None)
+                gather_records(out["record"], gathered[j] if rank == 0 else None)
             if ev is not None:
                 ev[1].record()
         return out
@@ -399,7 +402,8 @@ def main():
     counts = out["count"].cpu() if det is not None else None
     if det is not None and world > 1 and rank == 0:  # every rank's shard arrived: the global batch's counts
         from rtdm.pipeline import unpack_record
-        counts = torch.cat([unpack_record(gathered[r], pipe, b)["count"].cpu() for r in range(world)])
+        last = gathered[(args.steps - 1) % len(pipes)]  # the buffer of the last timed step's pipeline
+        counts = torch.cat([unpack_record(last[r], pipe, b)["count"].cpu() for r in range(world)])
 
     # ---- roofline: per-launch hipEvents on the detector's launch streams, eager steps ----
     if det is None:
@@ -446,16 +450,33 @@ def main():
               "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tr["source"] if tr else None,
               "timing": f"hipEvents around each detector launch on its launch stream, {calls.value} eager steps "
                         f"after the timed region"}
-        # the whole implicit-GEMM family (every conv_pipe / conv_pipew instantiation: the
-        # dominant symbol above is one epilogue / tiling variant of it)
-        fam = [k for k in agg if k.startswith(("conv_pipe_", "conv_pipew_"))]
+        # the whole implicit-GEMM family: every conv_pipe* instantiation (conv_pipe_, conv_pipew_,
+        # conv_pipew0_ (the cursor-loop window kernels, e.g. the fused head), conv_pipewpp_, ...,
+        # int8 twins priced at the int8 peak); the dominant symbol above is one variant of it
+        fam = [k for k in agg if k.startswith("conv_pipe")]
         if fam:
             f_ms = sum(agg[k][0] for k in fam)
             f_flop = sum(agg[k][1] for k in fam)
-            f_ach = f_flop / (f_ms * 1e-3) / 1e12
-            rl["family"] = {"kernels": "conv_pipe*/conv_pipew* (all MFMA implicit-GEMM convs)",
-                            "achieved": round(f_ach, 2), "frac": round(f_ach / peak, 4),
+            f_peak_ms = sum(agg[k][1] / ((MFMA_I8_DENSE_PEAK_TOPS if "_i8" in k else MFMA_F16_DENSE_PEAK_TFLOPS) * 1e12)
+                            * 1e3 for k in fam)
+            rl["family"] = {"kernels": "conv_pipe* (all MFMA implicit-GEMM convs, every variant)",
+                            "symbols": sorted(fam),
+                            "achieved": round(f_flop / (f_ms * 1e-3) / 1e12, 2),
+                            "frac": round(f_peak_ms / f_ms, 4),
                             "ms_per_step": round(f_ms / max(1, calls.value), 4)}
+        # per-layer fractions of the big convs (>= 5 % of the step's conv FLOP), so a change in the
+        # dominant symbol's composition (which layers share one instantiation) cannot move them
+        tot_flop = sum(f for (_, _, f, _) in steps)
+        lay = {}
+        for (name, layer, flop, byt), t in zip(steps, ms):
+            if not name.startswith("conv_pipe") or flop < 0.05 * tot_flop or t <= 0:
+                continue
+            lms = t / max(1, calls.value)
+            lpk = MFMA_I8_DENSE_PEAK_TOPS if "_i8" in name else MFMA_F16_DENSE_PEAK_TFLOPS
+            ach = flop / (lms * 1e-3) / 1e12
+            lay[f"L{layer}"] = {"kernel": name, "gflop": round(flop / 1e9, 2), "ms": round(lms, 4),
+                                "achieved": round(ach, 1), "frac": round(ach / lpk, 4)}
+        rl["layers"] = lay
         if rank == 0:
             per_step = {f"L{layer}:{name}": round(t / max(1, calls.value), 4)
                         for (name, layer, flop, byt), t in zip(steps, ms)}
@@ -482,7 +503,7 @@ def main():
             o2 = up.submit(k, host[k % len(host)])
             if world > 1:
                 with torch.cuda.stream(streams[k % len(pipes)]):
-                    gather_records(o2["record"], gathered if rank == 0 else None)
+                    gather_records(o2["record"], gathered[k % len(pipes)] if rank == 0 else None)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

@@ -6,8 +6,9 @@ and the same printed result: class name + confidence = softmax(model output)[cls
 (the reference's double softmax, :77-80).  The image transform
 (Resize(int(1.14·S)) → CenterCrop(S) → ToTensor → Normalize, dataloaders/aider.py:412-431)
 runs on the GPU, Pillow-exact.  ``--trt`` has no TensorRT behind it: it adds a second
-prediction on the fp16 path (``--quant fp16``) or the fp32 path, which is what the
-reference's TRT engines were for.  Plotting (cv2/matplotlib) is replaced by ``--save``.
+prediction on the fp16 path (``--quant fp16``), the fp32 path, or the int8 path (``--quant
+int8``: int8 MFMA ACFF fusion GEMMs, calibrated on ``--calib`` frames), which is what the
+reference's TRT engines were for (README.md:32-40 promises the three schemes).  Plotting (cv2/matplotlib) is replaced by ``--save``.
 """
 import argparse
 import logging
@@ -19,7 +20,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import torch  # noqa: E402
 
 from rtdm.classifier import load_model  # noqa: E402
-from rtdm.cli import predict_frames, read_image_rgb, select_device  # noqa: E402
+from rtdm.cli import calibration_frames, predict_frames, read_image_rgb, select_device  # noqa: E402
 
 logger = logging.getLogger(__name__)
 
@@ -40,8 +41,10 @@ def main(argv=None):
     parser.add_argument('--weights', type=str, default=None, help='path to model weights')
     parser.add_argument('--no-cuda', action='store_true', help='disable CUDA (not supported: GPU-only runtime)')
     parser.add_argument('--trt', action='store_true', help='also run the reduced-precision path (TensorRT stand-in)')
-    parser.add_argument('--quant', type=str, default='fp16', choices=['fp16', 'fp32'],
+    parser.add_argument('--quant', type=str, default='fp16', choices=['fp16', 'fp32', 'int8'],
                         help='precision of the --trt path')
+    parser.add_argument('--calib', type=str, default=None,
+                        help='int8: directory (or image) of calibration frames; default: the input image')
     parser.add_argument('--save', type=str, default=None, help='write the annotated image here (replaces plt.show)')
     args = parser.parse_args(argv)
 
@@ -57,7 +60,9 @@ def main(argv=None):
     logger.info(f"Prediction: {prediction} ({confidence:.1f}%)")
     result = {"prediction": prediction, "confidence": confidence}
     if args.trt:
-        trt_model = load_model(args.model, args.weights, device, half=args.quant == 'fp16')
+        calib = calibration_frames(args.calib, [read_image_rgb(args.image)], device) \
+            if args.quant == 'int8' else None
+        trt_model = load_model(args.model, args.weights, device, quant=args.quant, calib=calib)
         trt_prediction, trt_confidence = predict(trt_model, args.image, device)
         logger.info(f"TensorRT Prediction: {trt_prediction} ({trt_confidence:.1f}%)")
         result.update({"trt_prediction": trt_prediction, "trt_confidence": trt_confidence})

@@ -7,7 +7,8 @@ Same flags (:133-153) and the same report: accuracy / F1 / precision / recall
 precision / recall / F1 from the confusion matrix (:106-130).  Also reports frames/s.
 Images are decoded on the host (Pillow; the reference's DataLoader workers), each one
 resized/cropped/normalised on the GPU (rtdm_preprocess_frames, Pillow-exact) and the
-batch classified in one rtdm_classify call.  ``--trt --quant fp16`` selects the fp16 path.
+batch classified in one rtdm_classify call.  ``--trt --quant fp16`` selects the fp16 path,
+``--trt --quant int8`` the int8 one (calibrated on ``--calib`` images).
 """
 import argparse
 import logging
@@ -22,7 +23,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from rtdm.classifier import CLASSES, load_model  # noqa: E402
-from rtdm.cli import classification_metrics, read_image_rgb, read_split_csv, select_device  # noqa: E402
+from rtdm.cli import (calibration_frames, classification_metrics, read_image_rgb, read_split_csv,  # noqa: E402
+                      select_device)
 from rtdm.preprocess import preprocess_frames  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -66,14 +68,21 @@ def main(argv=None):
     parser.add_argument('--num-workers', type=int, default=4)
     parser.add_argument('--no-cuda', action='store_true')
     parser.add_argument('--trt', action='store_true', help='fp16 path stand-in for TensorRT')
-    parser.add_argument('--quant', type=str, default='fp16', choices=['fp16', 'fp32'])
+    parser.add_argument('--quant', type=str, default='fp16', choices=['fp16', 'fp32', 'int8'])
+    parser.add_argument('--calib', type=str, default=None,
+                        help='int8: directory of calibration images; default: the first 64 test images')
     args = parser.parse_args(argv)
 
     device = select_device(args.no_cuda)
     logger.info(f"Using device: {device}")
     rows = read_split_csv(args.test_split)
     half = args.trt and args.quant == 'fp16'
-    model = load_model(args.model, args.weights, device, half=half)
+    quant = args.quant if args.trt else 'fp32'
+    calib = None
+    if quant == 'int8':
+        calib = calibration_frames(args.calib, (read_image_rgb(os.path.join(args.root_dir, r[0])) for r in rows[:64]),
+                                   device)
+    model = load_model(args.model, args.weights, device, quant=quant, calib=calib)
     metrics = evaluate_model(model, rows, args.root_dir, args.batch_size, device, args.num_workers, half)
 
     logger.info("\nEvaluation Results:")

@@ -6,7 +6,8 @@ the device: cv2.resize(frame, (--width, --height)) with its default INTER_LINEAR
 rtdm_resize_linear, OpenCV's algorithm restated), then the CLI transform + classifier
 (rtdm_classify on the uint8 frame, :62-107).  Video decoding
 (imutils/cv2) is not part of this stack: --video takes a directory of image frames or an
-.npy array [T,H,W,3] uint8; webcam capture is not available.  ``--batch`` > 1 classifies
+.npy array [T,H,W,3] uint8; webcam capture is not available.  ``--trt --quant int8`` runs the int8 path
+(calibrated on ``--calib`` images).  ``--batch`` > 1 classifies
 that many frames per call (throughput mode); the default 1 is the reference's per-frame loop.
 """
 import argparse
@@ -21,7 +22,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from rtdm.classifier import load_model  # noqa: E402
-from rtdm.cli import list_images, predict_frames, read_image_rgb, select_device  # noqa: E402
+from rtdm.cli import calibration_frames, list_images, predict_frames, read_image_rgb, select_device  # noqa: E402
 from rtdm.letterbox import resize_linear  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -48,13 +49,20 @@ def main(argv=None):
     parser.add_argument('--height', type=int, default=480)
     parser.add_argument('--no-cuda', action='store_true')
     parser.add_argument('--trt', action='store_true', help='fp16 path stand-in for TensorRT')
-    parser.add_argument('--quant', type=str, default='fp16', choices=['fp16', 'fp32'])
+    parser.add_argument('--quant', type=str, default='fp16', choices=['fp16', 'fp32', 'int8'])
+    parser.add_argument('--calib', type=str, default=None,
+                        help='int8: directory of calibration images; default: the first 16 stream frames')
     parser.add_argument('--batch', type=int, default=1, help='frames per classifier call')
     args = parser.parse_args(argv)
 
     device = select_device(args.no_cuda)
     logger.info(f"Using device: {device}")
-    model = load_model(args.model, args.weights, device, half=args.trt and args.quant == 'fp16')
+    quant = args.quant if args.trt else 'fp32'
+    calib = None
+    if quant == 'int8':
+        import itertools
+        calib = calibration_frames(args.calib, itertools.islice(frame_source(args.video), 16), device)
+    model = load_model(args.model, args.weights, device, quant=quant, calib=calib)
     fps_list, results = [], []
     prev = time.time()
     pending = []

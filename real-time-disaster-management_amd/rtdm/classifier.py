@@ -79,28 +79,35 @@ class _ACFFClassifier(torch.nn.Module):
         """int8 ACFF fusion GEMMs (the §8 int8 row for ErNET; the reference classifier has no
         int8 mode): activations stay fp16, the 1x1 fusion convs of the persistent and chained
         ACFF stages run on int8 MFMA with per-concat-channel activation scales calibrated on
-        `calib` (uint8 frames [N,H,W,3] or [N,3,S,S] inputs on the GPU, kept for handles
-        created later) folded into per-output-channel int8 weights."""
-        if not calib.is_cuda:
-            raise RuntimeError("calibration frames must be on the GPU")
-        self._calib = calib.contiguous()
+        `calib` (uint8 frames [N,H,W,3] or [N,3,S,S] inputs on the GPU, or a list of such
+        batches, e.g. frames of different sizes; kept for handles created later) folded into
+        per-output-channel int8 weights.  The activation maxima are taken over all of them."""
+        batches = list(calib) if isinstance(calib, (list, tuple)) else [calib]
+        if not batches:
+            raise ValueError("int8: no calibration frames")
+        for x in batches:
+            if not x.is_cuda:
+                raise RuntimeError("calibration frames must be on the GPU")
+        self._calib = [x.contiguous() for x in batches]
         self._dtype = L.RTDM_I8
         self._release()
         return self
 
     def _calibrate(self, h):
-        x = self._calib
-        if x.dtype == torch.uint8:
-            kind, hh, ww = L.RTDM_INPUT_FRAME_U8, x.shape[1], x.shape[2]
-        else:
-            kind = L.RTDM_INPUT_NCHW_F32 if x.dtype == torch.float32 else L.RTDM_INPUT_NCHW_F16
-            hh, ww = x.shape[2], x.shape[3]
         cap = self._handle_key[1]
-        with torch.cuda.device(x.device):
-            for i in range(0, x.shape[0], cap):
-                c = x[i:i + cap]
-                L.check(L.lib().rtdm_classifier_calibrate(h, L.ptr(c), kind, c.shape[0], hh, ww,
-                                                          1 if i == 0 else 0, L.stream_ptr()))
+        first = True
+        for x in self._calib:
+            if x.dtype == torch.uint8:
+                kind, hh, ww = L.RTDM_INPUT_FRAME_U8, x.shape[1], x.shape[2]
+            else:
+                kind = L.RTDM_INPUT_NCHW_F32 if x.dtype == torch.float32 else L.RTDM_INPUT_NCHW_F16
+                hh, ww = x.shape[2], x.shape[3]
+            with torch.cuda.device(x.device):
+                for i in range(0, x.shape[0], cap):
+                    c = x[i:i + cap]
+                    L.check(L.lib().rtdm_classifier_calibrate(h, L.ptr(c), kind, c.shape[0], hh, ww,
+                                                              1 if first else 0, L.stream_ptr()))
+                    first = False
 
     def _release(self):
         if self._handle is not None:
@@ -269,11 +276,25 @@ def read_weights(weights_path: str) -> dict:
     return ckpt
 
 
-def load_model(model_name: str, weights_path: str, device: torch.device, half: bool = False) -> _ACFFClassifier:
-    """aider-predict.py:22-45 / evaluate-classification-metrics.py:24-47 counterpart."""
+QUANTS = ("fp32", "fp16", "int8")
+
+
+def load_model(model_name: str, weights_path: str, device: torch.device, half: bool = False,
+               quant: str | None = None, calib=None) -> _ACFFClassifier:
+    """aider-predict.py:22-45 / evaluate-classification-metrics.py:24-47 counterpart.
+    `quant` (the README's --quant {fp32,fp16,int8}, README.md:32-40) overrides `half`; int8
+    needs `calib`: uint8 frames [N,H,W,3] on the device, or a list of such batches."""
     model = build_model(model_name)
     model.load_state_dict(read_weights(weights_path))
-    if half:
+    if quant is None:
+        quant = "fp16" if half else "fp32"
+    if quant not in QUANTS:
+        raise ValueError(f"quant must be one of {QUANTS}, got {quant!r}")
+    if quant == "fp16":
         model.half()
+    elif quant == "int8":
+        if calib is None:
+            raise ValueError("int8 needs calibration frames (--calib)")
+        model.int8(calib)
     model.eval()
     return model

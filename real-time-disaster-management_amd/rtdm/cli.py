@@ -99,3 +99,19 @@ def read_split_csv(path: str):
             except ValueError:  # header
                 continue
     return rows
+
+
+def calibration_frames(calib: str | None, fallback, device: torch.device, limit: int = 64):
+    """int8 calibration set of the CLIs (--quant int8): the images of `calib` (a directory or
+    one image; at most `limit`), uploaded as uint8 [1,H,W,3] device frames; without --calib,
+    the host RGB frames in `fallback` (the inputs themselves).  The reference's int8 TRT
+    engines were calibrated on a separate image set (tensorrt_inference/yolo/calibrator.py:
+    87-153); pass one with --calib for a calibration disjoint from the evaluated frames."""
+    if calib is not None:
+        imgs = [read_image_rgb(p) for p in list_images(calib)[:limit]]
+        if not imgs:
+            raise SystemExit(f"--calib {calib}: no images")
+    else:
+        logging.getLogger(__name__).warning("--quant int8 without --calib: calibrating on the input frames")
+        imgs = list(fallback)[:limit]
+    return [torch.from_numpy(np.ascontiguousarray(im)[None]).to(device) for im in imgs]

@@ -68,6 +68,25 @@ def test_split_csv_and_cpu_refused(tmp_path):
         select_device(no_cuda=True)
 
 
+def test_quant_flags_accept_int8(tmp_path, cls_weights):
+    """--quant {fp32,fp16,int8} on the three classifier CLIs (the reference README's three
+    schemes, disaster_detection/README.md:32-40); int8 without calibration frames is refused
+    before any device work."""
+    import argparse
+    from rtdm.classifier import load_model
+    for name in ("aider-predict", "evaluate-classification-metrics", "real-time-inference"):
+        src = open(os.path.join(PKG, name + ".py")).read()
+        assert "choices=['fp16', 'fp32', 'int8']" in src and "'--calib'" in src, name
+    sd = cls_weights["squeeze-ernet"]
+    wpath = tmp_path / "w.pt"
+    torch.save({k: torch.from_numpy(v) for k, v in sd.items()}, wpath)
+    with pytest.raises(ValueError):
+        load_model("squeeze-ernet", str(wpath), torch.device("cpu"), quant="int8")
+    with pytest.raises(ValueError):
+        load_model("squeeze-ernet", str(wpath), torch.device("cpu"), quant="int4")
+    assert argparse  # (parsers are exercised end to end by the GPU tests below)
+
+
 # ------------------------------------------------------------------ GPU --
 def _cls_oracle(name, sd, imgs):
     from oracle import classifier as OC
@@ -177,3 +196,59 @@ def test_real_time_inference_cli_matches_oracle(tmp_path, cls_weights):
     assert [r[0] for r in results] == [CLASSES[c] for c in cls]
     assert np.allclose([r[1] for r in results], conf, atol=1e-3)
     assert len(fps) == len(imgs)
+
+
+@pytest.mark.gpu
+def test_cli_quant_int8(tmp_path, cls_weights):
+    """--trt --quant int8 --calib DIR on aider-predict, evaluate-classification-metrics and
+    real-time-inference: the int8 classifier (int8 MFMA ACFF fusion GEMMs, calibrated on the
+    --calib images, disjoint from the evaluated ones) runs, and its class ids agree with the
+    fp32 oracle's wherever the oracle's top-2 logit gap exceeds 5 % of max|logit| (the §8d
+    int8 bar's non-tied frames)."""
+    from oracle import classifier as OC
+    from oracle import preprocess as P
+    from rtdm.classifier import CLASSES
+    from rtdm.synth import synth_frames
+    name = "ernet"
+    sd = cls_weights[name]
+    wpath = tmp_path / "w.pt"
+    torch.save({k: torch.from_numpy(v) for k, v in sd.items()}, wpath)
+    os.makedirs(tmp_path / "calib")
+    for i in range(12):
+        _write_png(tmp_path / "calib" / f"{i}.png", synth_frames(1, 260 + 3 * i, 300, seed=900 + i)[0])
+    os.makedirs(tmp_path / "img")
+    imgs, rows = [], []
+    for i in range(10):
+        im = synth_frames(1, 240 + 9 * i, 280, seed=700 + i)[0]
+        _write_png(tmp_path / "img" / f"{i}.png", im)
+        imgs.append(im)
+        rows.append(f"img/{i}.png,{i % 5}")
+    x = torch.from_numpy(np.stack([P.cli_transform(im, 240) for im in imgs]))
+    logits = OC.forward(name, sd, x)[0].numpy()
+    ref = logits.argmax(1)
+    top2 = np.sort(logits, 1)[:, -2:]
+    sure = (top2[:, 1] - top2[:, 0]) > 0.05 * np.abs(logits).max(1)
+    assert sure.sum() >= 5
+    cli = _load_cli("aider-predict")
+    for i in np.nonzero(sure)[0][:3]:
+        res = cli.main(["--model", name, "--image", str(tmp_path / "img" / f"{i}.png"), "--weights", str(wpath),
+                        "--trt", "--quant", "int8", "--calib", str(tmp_path / "calib")])
+        assert res["trt_prediction"] == CLASSES[ref[i]], (i, res)
+    (tmp_path / "split.csv").write_text("\n".join(rows) + "\n")
+    ev = _load_cli("evaluate-classification-metrics")
+    m = ev.main(["--model", name, "--weights", str(wpath), "--test-split", str(tmp_path / "split.csv"),
+                 "--root-dir", str(tmp_path), "--batch-size", "4", "--trt", "--quant", "int8",
+                 "--calib", str(tmp_path / "calib")])
+    acc_ref = float(np.mean([c == i % 5 for i, c in enumerate(ref)]))
+    assert abs(m["accuracy"] - acc_ref) <= float((~sure).sum()) / len(ref) + 1e-9, (m["accuracy"], acc_ref)
+    rt = _load_cli("real-time-inference")
+    results, _ = rt.main(["--model", name, "--weights", str(wpath), "--video", str(tmp_path / "img"),
+                          "--width", "640", "--height", "480", "--trt", "--quant", "int8",
+                          "--calib", str(tmp_path / "calib"), "--batch", "4"])
+    from oracle import letterbox as OL
+    xr = torch.from_numpy(np.stack([P.cli_transform(OL.resize_linear(im, 640, 480), 240) for im in imgs]))
+    lr = OC.forward(name, sd, xr)[0].numpy()
+    t2 = np.sort(lr, 1)[:, -2:]
+    sure_r = (t2[:, 1] - t2[:, 0]) > 0.05 * np.abs(lr).max(1)
+    got = [CLASSES.index(r[0]) for r in results]
+    assert all(g == r for g, r, s in zip(got, lr.argmax(1), sure_r) if s), (got, lr.argmax(1).tolist())

@@ -27,6 +27,9 @@ from conftest import cfg_text
 
 pytestmark = pytest.mark.gpu
 
+# SURVEY §8d's int8 detection bar applied literally (both directions, 1e-3 band)
+LITERAL_BAR = 0.97
+
 
 @pytest.fixture(scope="module")
 def dev():
@@ -43,21 +46,40 @@ def _iou(a, b):
     return inter / ((a[2] - a[0]) * (a[3] - a[1]) + (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1]) - inter)
 
 
-def _match(ref_io, io, conf=0.3, iou=0.4):
+def _match(ref_io, io, conf=0.3, iou=0.4, band=0.02):
+    """Recall-only detection match: fp32 survivors whose confidence exceeds conf + band that
+    have an int8 survivor of the same class at IoU >= 0.9 (the relaxed metric)."""
+    m, t, _, _ = match_both(ref_io, io, conf, iou, band)
+    return m, t
+
+
+def match_both(ref_io, io, conf=0.3, iou=0.4, band=1e-3):
+    """SURVEY §8d's detection match, both directions: (recall) fp32 survivors with an int8
+    survivor of the same class at IoU >= 0.9, and (precision) int8 survivors with such an fp32
+    survivor; a survivor whose confidence lies within `band` of the threshold is left out of
+    its own side's count (band 1e-3: the §8d fp16 survivor rule's band).
+    Returns (recall matches, fp32 survivors counted, precision matches, int8 survivors counted)."""
     from oracle import nms as ON
     ref = ON.non_max_suppression(ref_io, conf, iou)
     got = ON.non_max_suppression(io, conf, iou)
-    m = t = 0
-    for b in range(len(ref)):
-        r = np.zeros((0, 6), np.float32) if ref[b] is None else ref[b]
-        g = np.zeros((0, 6), np.float32) if got[b] is None else got[b]
-        r = r[r[:, 4] > conf + 0.02]
-        t += len(r)
-        for row in r:
-            same = g[g[:, 5] == row[5]]
+
+    def hits(a, b):
+        m = t = 0
+        for row in a[a[:, 4] > conf + band]:
+            t += 1
+            same = b[b[:, 5] == row[5]]
             if len(same) and _iou(row[:4], same[:, :4]).max() >= 0.9:
                 m += 1
-    return m, t
+        return m, t
+    rm = rt = pm = pt = 0
+    for k in range(len(ref)):
+        r = np.zeros((0, 6), np.float32) if ref[k] is None else ref[k]
+        g = np.zeros((0, 6), np.float32) if got[k] is None else got[k]
+        m, t = hits(r, g)
+        rm, rt = rm + m, rt + t
+        m, t = hits(g, r)
+        pm, pt = pm + m, pt + t
+    return rm, rt, pm, pt
 
 
 def _stats(io, ref):
@@ -116,9 +138,14 @@ def test_int8_detector_survey_bar(dev):
         assert g[0] <= 1.5 * f[0] + s and g[1] <= 1.5 * f[1] + s, (name, g, f)
     mh, t = _match(io32, io)
     me, _ = _match(io32, emu)
-    print(f"int8 detection match: HIP {mh}/{t} = {mh / t:.4f}, scheme model {me}/{t}")
+    print(f"int8 detection match (recall, 0.02 band): HIP {mh}/{t} = {mh / t:.4f}, scheme model {me}/{t}")
+    rm, rt, pm, pt = match_both(io32, io)
+    erm, _, epm, _ = match_both(io32, emu)
+    print(f"int8 detection match (SURVEY §8d literal, 1e-3 band): recall {rm}/{rt} = {rm / rt:.4f}, "
+          f"precision {pm}/{pt} = {pm / pt:.4f}; scheme model recall {erm}/{rt}, precision {epm}/{pt}")
     assert t >= 60, t
     assert mh / t >= 0.97, (mh, t)
+    assert rm / rt >= LITERAL_BAR and pm / pt >= LITERAL_BAR, (rm, rt, pm, pt)
 
 
 def test_int8_first_layer_vs_fp16(dev):
@@ -220,6 +247,8 @@ def test_int8_classifier_top1_vs_fp32(dev, name, cls_weights, cls_golden):
     assert e8.max() <= 1.5 * em.max() + 2e-3 and e8.mean() <= 1.5 * em.mean() + 1e-3
     assert a8 >= am - 0.01
     assert a8s >= 0.99
+    # SURVEY §8d literally: >= 99 % top-1 agreement over every frame
+    assert a8 >= 0.99, a8
 
 
 def test_int8_classifier_requires_calibration(dev, cls_weights):
