@@ -128,10 +128,6 @@ def build(args, world, rank):
 
     from rtdm import _lib as L
     L.check(L.lib().rtdm_set_tuning(b"two_streams", 1 if args.det_streams > 1 else 0))
-    # several batches in flight fill each other's idle CUs: plan conv tiles for CU-time, not for
-    # one launch's rounds (larger tiles; bit-identical either way).  Measured with 4 in flight
-    # (r03an): b8 31.8k -> 33.0k, b16 36.9k -> 39.3k frames/s
-    L.check(L.lib().rtdm_set_tuning(b"conv_pipe_cost", 1 if args.inflight > 1 else 0))
     for kv in filter(None, os.environ.get("RTDM_TUNE", "").split(",")):  # diagnostics: "key=v,key=v"
         k, v = kv.split("=")
         L.check(L.lib().rtdm_set_tuning(k.encode(), int(v)))
@@ -186,6 +182,12 @@ def build(args, world, rank):
                     det.half() if args.dtype == "f16" else det.int8(calib)
                 if use_cls:
                     cls.half() if args.dtype == "f16" else cls.int8(calib)
+        if use_det:
+            # several batches in flight fill each other's idle CUs: plan conv tiles for CU-time, not
+            # for one launch's rounds (larger tiles; bit-identical either way), on these detectors'
+            # own handles only (rtdm_detector_set_tuning).  Measured with 4 in flight (r03an): b8
+            # 31.8k -> 33.0k, b16 36.9k -> 39.3k frames/s
+            det.set_tuning("conv_pipe_cost", 1 if args.inflight > 1 else 0)
         pipes.append(TwoStagePipeline(cls, det, args.conf, args.iou, args.max_det, overlap=bool(args.overlap),
                                       priority=bool(args.priority), graphs=bool(args.graphs)))
     return pipes, text, stream, sd

@@ -120,24 +120,36 @@ const char* rtdm_last_error(void);
 /* gfx arch string the code objects were built for ("gfx950"). */
 const char* rtdm_build_arch(void);
 /* Kernel-selection knobs for A/B measurement (no reference counterpart; the
- * defaults are the tuned choice).  key "conv_pipe": 1 = pipelined 256x128
- * implicit GEMM for Cin%64==0 convs (default), 0 = conv_glds_f16 128x128;
- * key "fuse_head": 1 = conv -> 1x1 head conv -> [yolo] planned as one launch
- * (default), 0 = separate head conv (takes effect for handles created
- * afterwards); key "acff_persist": 1 = persistent ACFF kernel for the large
- * classifier maps (default), 0 = 8x8-tile fused ACFF kernel (at launch); key
- * "two_streams": 1 = detector head branches on a side stream (default), 0 = one
- * stream (takes effect for handles created afterwards).  conv_pipe variants, all
- * bit-identical to each other (at launch): "conv_pipe_bm" 0 = tile rows by the
- * cost model (default) | 256 | 128 | 64; "conv_pipe_win" 1 = window mode for
- * 3x3/s1 layers (default); "conv_pipe_korder" 1 = channel-block-outer K order
- * (default; 0 changes the fp32 summation order); "conv_pipe_pf" 1 = cross-tile
- * prologue prefetch (default; not with ping-pong); "conv_pipe_pp" 1 = ping-pong
- * K-loop (two wave groups alternating MFMA and memory phases; default 0: measured
- * 4-18 % slower per layer); "conv_pipe_wloop" 1 = tap-unrolled
- * 3x3 K-loop for the register-epilogue layers (default), 0 = the cursor loop;
- * "conv_pipe_walk" g = tile walk in N-groups of g panels (default 2, 0 = M-major). */
+ * defaults are the tuned choice).  rtdm_set_tuning sets the PROCESS DEFAULTS: a
+ * detector / classifier handle copies them when it is created, and each handle's
+ * copy can be changed afterwards with rtdm_detector_set_tuning /
+ * rtdm_classifier_set_tuning (every call on a handle runs with its own copy, so two
+ * handles in one process can differ, e.g. a latency and a throughput pipeline).
+ * Plan-time keys ("fuse_head", "two_streams") only act at handle creation.
+ * key "conv_pipe": 1 = pipelined 256x128 implicit GEMM for Cin%64==0 convs
+ * (default), 0 = conv_glds_f16 128x128; key "fuse_head": 1 = conv -> 1x1 head conv
+ * -> [yolo] planned as one launch (default), 0 = separate head conv; key
+ * "acff_persist": 1 = persistent ACFF kernel for the large classifier maps
+ * (default), 0 = 8x8-tile fused ACFF kernel; key "two_streams": 1 = detector head
+ * branches on a side stream (default), 0 = one stream.  conv_pipe variants, all
+ * bit-identical to each other: "conv_pipe_bm" 0 = tile rows by the cost model
+ * (default) | 256 | 128 | 64; "conv_pipe_cost" 0 = the cost model minimises one
+ * launch's rounds of tiles (latency, default) | 1 = CU-time (throughput, for several
+ * batches in flight); "conv_pipe_win" 1 = window mode for 3x3/s1 layers (default);
+ * "conv_pipe_korder" 1 = channel-block-outer K order (default; 0 changes the fp32
+ * summation order); "conv_pipe_pf" 1 = cross-tile prologue prefetch (default; not
+ * with ping-pong); "conv_pipe_pp" 1 = ping-pong K-loop (two wave groups
+ * alternating MFMA and memory phases; default 0: measured 4-18 % slower per layer,
+ * DESIGN.md §3.4); "conv_pipe_wloop" 1 = tap-unrolled 3x3 K-loop for the
+ * register-epilogue layers (default), 0 = the cursor loop; "conv_pipe_walk" g =
+ * tile walk in N-groups of g panels (default 2, 0 = M-major); "conv_wide" 1 = the
+ * 256x256-tile kernel where the cost model picks it (default) | 0 off | 2 always |
+ * 3 one round of wide tiles + a 256x128 tail; "conv_wide_eff" its cost-model rate
+ * (x100).  Unknown keys: RTDM_E_INVALID. */
 rtdm_status rtdm_set_tuning(const char* key, int value);
+/* The same keys on one handle's own copy (see above). */
+rtdm_status rtdm_detector_set_tuning(rtdm_detector h, const char* key, int value);
+rtdm_status rtdm_classifier_set_tuning(rtdm_classifier h, const char* key, int value);
 
 /* ---- classifier ------------------------------------------------------------ */
 /* params: the reference state_dict (e.g. weights/squeeze-ernet-state_dict.pt),

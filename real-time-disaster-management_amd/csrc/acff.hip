@@ -603,9 +603,7 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
   }
 }
 
-static int g_acff_persist = 1;
-int acff_persist_mode() { return g_acff_persist; }
-void set_acff_persist_mode(int v) { g_acff_persist = v < 0 ? 0 : v; }
+int acff_persist_mode() { return tune().acff_persist; }
 
 // Channel chunk of the persistent kernel for cin (0 = not eligible).
 int acff_persist_chunk(int cin, int cout_pad, int oh) {
@@ -1071,9 +1069,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
   }
 }
 
-static int g_acff_chain = 1;
-int acff_chain_mode() { return g_acff_chain; }
-void set_acff_chain_mode(int v) { g_acff_chain = v; }
+int acff_chain_mode() { return tune().acff_chain; }
 
 size_t acff_chain_lds(const AcffChainPlan& p) {
   size_t act = 0, ab = 0;

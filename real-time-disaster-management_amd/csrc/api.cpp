@@ -20,6 +20,49 @@ const char* get_error() { return g_last_error.c_str(); }
 
 using namespace rtdm;
 
+namespace rtdm {
+
+Tuning& default_tuning() {
+  static Tuning t = [] {
+    Tuning d;
+    if (const char* e = getenv("RTDM_CONV_PIPE")) d.conv_pipe = atoi(e);  // A/B runs
+    return d;
+  }();
+  return t;
+}
+static thread_local const Tuning* t_tuning = nullptr;
+const Tuning& tune() { return t_tuning ? *t_tuning : default_tuning(); }
+TuningScope::TuningScope(const Tuning* t) : prev(t_tuning) { t_tuning = t; }
+TuningScope::~TuningScope() { t_tuning = prev; }
+
+void tuning_set(Tuning& t, const char* key, int v) {
+  RTDM_REQUIRE(key, RTDM_E_INVALID, "set_tuning: NULL key");
+  const std::string k = key;
+  if (k == "conv_pipe") t.conv_pipe = v < 0 ? 0 : v;
+  else if (k == "conv_pipe_korder") t.pipe_korder = v ? 1 : 0;
+  else if (k == "conv_pipe_bm") t.pipe_bm = (v == 256 || v == 128 || v == 64) ? v : 0;
+  else if (k == "conv_pipe_win") t.pipe_win = v ? 1 : 0;
+  else if (k == "conv_pipe_pf") t.pipe_pf = v ? 1 : 0;
+  else if (k == "conv_pipe_pp") t.pipe_pp = v ? 1 : 0;
+  else if (k == "conv_pipe_walk") t.pipe_walk = v > 0 ? v : 0;
+  else if (k == "conv_pipe_cost") t.pipe_cost = v ? 1 : 0;
+  else if (k == "conv_pipe_wloop") t.pipe_wloop = v ? 1 : 0;
+  else if (k == "conv_wide") t.pipe_wide = v < 0 ? 0 : v;
+  else if (k == "conv_wide_eff") t.pipe_wide_eff = v > 0 ? v : 115;
+  else if (k == "head1x1") t.head1x1 = v ? 1 : 0;
+  else if (k == "dw3_tile") t.dw3_tile = v ? 1 : 0;
+  else if (k == "fuse_head") t.fuse_head = v ? 1 : 0;
+  else if (k == "two_streams") t.two_streams = v ? 1 : 0;
+  else if (k == "acff_persist") t.acff_persist = v < 0 ? 0 : v;
+  else if (k == "acff_chain") t.acff_chain = v;
+  else if (k == "stem_abl") t.stem_abl = v;
+  else if (k == "nms_variant") t.nms_variant = v;
+  else if (k == "resize_stream") t.resize_stream = v;
+  else throw Error{RTDM_E_INVALID, "set_tuning: unknown key " + k};
+}
+
+}  // namespace rtdm
+
 extern "C" {
 
 int rtdm_abi_version(void) { return RTDM_ABI_VERSION; }
@@ -29,47 +72,7 @@ const char* rtdm_last_error(void) { return get_error(); }
 const char* rtdm_build_arch(void) { return "gfx950"; }
 
 rtdm_status rtdm_set_tuning(const char* key, int value) {
-  return guard([&] {
-    RTDM_REQUIRE(key, RTDM_E_INVALID, "set_tuning: NULL key");
-    if (!strcmp(key, "conv_pipe"))
-      set_conv_pipe_mode(value);
-    else if (!strcmp(key, "conv_pipe_korder"))
-      set_pipe_korder(value);
-    else if (!strcmp(key, "conv_pipe_bm"))
-      set_pipe_bm(value);
-    else if (!strcmp(key, "conv_pipe_win"))
-      set_pipe_win(value);
-    else if (!strcmp(key, "conv_pipe_pf"))
-      set_pipe_pf(value);
-    else if (!strcmp(key, "conv_pipe_pp"))
-      set_pipe_pp(value);
-    else if (!strcmp(key, "conv_pipe_walk"))
-      set_pipe_walk(value);
-    else if (!strcmp(key, "conv_pipe_cost"))
-      set_pipe_cost(value);
-    else if (!strcmp(key, "conv_pipe_wloop"))
-      set_pipe_wloop(value);
-    else if (!strcmp(key, "head1x1"))
-      set_head1x1(value);
-    else if (!strcmp(key, "dw3_tile"))
-      set_dw3_tile(value);
-    else if (!strcmp(key, "fuse_head"))
-      set_fuse_head(value);
-    else if (!strcmp(key, "two_streams"))
-      set_two_streams_mode(value);
-    else if (!strcmp(key, "acff_persist"))
-      set_acff_persist_mode(value);
-    else if (!strcmp(key, "acff_chain"))
-      set_acff_chain_mode(value);
-    else if (!strcmp(key, "stem_abl"))
-      set_stem_abl(value);
-    else if (!strcmp(key, "nms_variant"))
-      set_nms_variant(value);
-    else if (!strcmp(key, "resize_stream"))
-      set_resize_stream_mode(value);
-    else
-      throw Error{RTDM_E_INVALID, std::string("set_tuning: unknown key ") + key};
-  });
+  return guard([&] { tuning_set(default_tuning(), key, value); });
 }
 
 rtdm_status rtdm_yolo_decode(const float* p, int n, int na, int no, int ny, int nx, const float* anchors, int img_h,

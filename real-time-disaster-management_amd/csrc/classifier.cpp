@@ -50,6 +50,7 @@ struct AcffStage {
 
 struct rtdm_classifier_s {
   int kind = 0, dtype = 0, S = 0, max_batch = 0, dev = 0;
+  rtdm::Tuning tuning;  // this handle's knobs (rtdm_classifier_set_tuning; the defaults at create)
   rtdm::DevBlob blob;
   rtdm::PackedConv stem;
   int stem_oh = 0, stem_cout = 0;
@@ -77,6 +78,7 @@ struct rtdm_classifier_s {
   static constexpr int kMaxSeg = 24;
   bool timing = false;
   int timing_cap = 0, timing_calls = 0, n_seg = 0, seg_n = 0;
+  std::vector<int> call_segs;  // launches recorded by each timed call
   std::vector<hipEvent_t> events;
   std::vector<std::string> seg_name;
   std::vector<double> seg_bytes;
@@ -371,6 +373,7 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
     if (h.timing_calls == 0) {
       h.seg_name.clear();
       h.seg_bytes.clear();
+      h.call_segs.assign(h.timing_cap, 0);
     }
     ++h.timing_calls;
   }
@@ -387,6 +390,7 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
     if (!ev) return;
     RTDM_HIP(hipEventRecord(ev[2 * si + 1], s));
     h.n_seg = ++si;
+    h.call_segs[h.timing_calls - 1] = si;
   };
   const double nb = (double)n;
   char* base = h.arena.as<char>();
@@ -673,6 +677,8 @@ rtdm_status rtdm_classifier_create(int kind, int dtype, const rtdm_param* params
     RTDM_REQUIRE(max_batch > 0, RTDM_E_INVALID, "classifier_create: max_batch must be > 0");
     RTDM_REQUIRE(params && n_params > 0, RTDM_E_INVALID, "classifier_create: no parameters");
     auto h = std::make_unique<rtdm_classifier_s>();
+    h->tuning = default_tuning();
+    TuningScope ts_(&h->tuning);
     h->kind = kind;
     h->int8 = dtype == RTDM_I8;
     h->dtype = h->int8 ? RTDM_F16 : dtype;  // int8 handles keep fp16 activations
@@ -685,12 +691,21 @@ rtdm_status rtdm_classifier_create(int kind, int dtype, const rtdm_param* params
   });
 }
 
+rtdm_status rtdm_classifier_set_tuning(rtdm_classifier h, const char* key, int value) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "classifier_set_tuning: NULL handle");
+    tuning_set(h->tuning, key, value);
+  });
+}
+
 rtdm_status rtdm_classifier_destroy(rtdm_classifier h) {
   return guard([&] { delete h; });
+    TuningScope ts_(h ? &h->tuning : nullptr);
 }
 
 rtdm_status rtdm_classifier_enable_timing(rtdm_classifier h, int max_calls) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "classifier_enable_timing: NULL handle");
     for (hipEvent_t e : h->events) (void)hipEventDestroy(e);
     h->events.clear();
@@ -707,8 +722,16 @@ rtdm_status rtdm_classifier_enable_timing(rtdm_classifier h, int max_calls) {
 rtdm_status rtdm_classifier_read_timing(rtdm_classifier h, double* ms_per_launch, double* bytes_per_launch,
                                         char* names, int name_stride, int* n_launches, int* calls) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "classifier_read_timing: NULL handle");
-    const int ns = h->timing_calls > 0 ? h->n_seg : 0;
+    // every timed call must have recorded the first call's launches (the names / bytes are the
+    // first call's): a call with another launch sequence (frames vs NCHW input, another
+    // chain mode) is refused, not summed into mismatched slots
+    const int ns = h->timing_calls > 0 ? (int)h->seg_name.size() : 0;
+    for (int c = 0; c < h->timing_calls; ++c)
+      RTDM_REQUIRE(h->call_segs[c] == ns, RTDM_E_INVALID,
+                   "classifier_read_timing: timed call " + std::to_string(c) + " recorded " +
+                       std::to_string(h->call_segs[c]) + " launches, the first " + std::to_string(ns));
     for (int i = 0; i < ns; ++i) {
       double t = 0.0;
       for (int c = 0; c < h->timing_calls; ++c) {
@@ -734,6 +757,7 @@ int rtdm_classifier_input_size(rtdm_classifier h) { return h ? h->S : 0; }
 
 int64_t rtdm_classifier_describe(rtdm_classifier h, char* buf, int64_t buf_len) {
   if (!h) return 0;
+  TuningScope ts_(&h->tuning);
   std::string s = "classifier S " + std::to_string(h->S) + " dtype " +
                   (h->int8 ? "i8" : h->dtype == RTDM_F16 ? "f16" : "f32") + " max_batch " +
                   std::to_string(h->max_batch) + "\n";
@@ -757,6 +781,7 @@ int64_t rtdm_classifier_describe(rtdm_classifier h, char* buf, int64_t buf_len) 
 rtdm_status rtdm_classifier_calibrate(rtdm_classifier h, const void* x, int x_kind, int n, int in_h, int in_w,
                                       int reset, void* stream) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "classifier_calibrate: NULL handle");
     RTDM_REQUIRE(h->int8, RTDM_E_INVALID, "classifier_calibrate: handle is not RTDM_I8");
     if (h->q_channels == 0) {
@@ -827,6 +852,7 @@ rtdm_status rtdm_classifier_calibrate(rtdm_classifier h, const void* x, int x_ki
 rtdm_status rtdm_classify(rtdm_classifier h, const void* x, int x_kind, int n, int in_h, int in_w, float* logits,
                           float* probs, void* stream) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "classify: NULL handle");
     run_classifier(*h, x, x_kind, n, in_h, in_w, logits, probs, (hipStream_t)stream);
   });

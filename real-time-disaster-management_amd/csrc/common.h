@@ -174,6 +174,46 @@ __device__ __forceinline__ void xcd_span(int bid, int nb, int ntiles, int& first
   step = (nb - x + 7) >> 3;
 }
 
+// Tuning knobs (rtdm_set_tuning keys in api.cpp): kernel-choice / A/B switches and the
+// cost-model objectives.  default_tuning() holds the process defaults; a detector / classifier
+// handle copies them when it is created (rtdm_*_set_tuning changes its own copy), and every
+// call on a handle runs under a TuningScope of the handle's set, so two handles in one process
+// can differ (e.g. a latency pipeline and a throughput pipeline).  tune() is the active set
+// (the calling thread's scope, else the defaults).
+struct Tuning {
+  int conv_pipe = 1;        // conv_pipe mode (1 the kernels; 0 off; > 1 diagnostics, conv_pipe.hip)
+  int stem_abl = 0;         // conv_stem3 ablations (diagnostics)
+  int head1x1 = 1;          // stand-alone YOLO head convs on head1x1_f16
+  int pipe_bm = 0;          // conv_pipe tile rows: 0 cost model, else forced 256 / 128 / 64
+  int pipe_cost = 0;        // conv_pipe / conv_wide tile objective: 0 latency (rounds), 1 throughput (CU-time)
+  int pipe_korder = 1;      // conv_pipe K order: 0 tap outer, 1 channel-block outer
+  int pipe_win = 1;         // conv_pipe window mode
+  int pipe_pf = 1;          // conv_pipe cross-tile prologue prefetch
+  int pipe_pp = 0;          // conv_pipe ping-pong K-loop schedule
+  int pipe_walk = 2;        // conv_pipe tile walk: N-panels per group (0 = M-major)
+  int pipe_wloop = 1;       // conv_pipe tap-unrolled 3x3 K-loops
+  int pipe_wide = 1;        // conv_wide: 0 off, 1 cost model, 2 all 256 x 256 tiles, 3 one round + 256 x 128 tail
+  int pipe_wide_eff = 115;  // conv_wide cost model: its K-loop rate per FLOP over conv_pipew's, x100
+  int dw3_tile = 1;         // YOLO-ACFF depthwise on the LDS-tiled kernel (1) or the vector one (0)
+  int resize_stream = 1;    // classifier preprocessing kernel
+  int nms_variant = 0;      // NMS diagnostics
+  int acff_persist = 1;     // acff_persist for the large-map ACFF stages (> 1: ablations)
+  int acff_chain = 1;       // acff_chain for the small-map suffix
+  int fuse_head = 1;        // fused YOLO head convs (plan time)
+  int two_streams = 1;      // detector head branches on a second stream (plan time)
+};
+Tuning& default_tuning();
+const Tuning& tune();
+struct TuningScope {
+  explicit TuningScope(const Tuning* t);
+  ~TuningScope();
+  TuningScope(const TuningScope&) = delete;
+  TuningScope& operator=(const TuningScope&) = delete;
+  const Tuning* prev;
+};
+// key -> knob (RTDM_E_INVALID on an unknown key)
+void tuning_set(Tuning& t, const char* key, int value);
+
 struct ConvArgs {
   const void* in = nullptr;
   int in_cs = 0, in_co = 0, in_kind = IN_NHWC;
@@ -194,7 +234,7 @@ struct ConvArgs {
   int pipe_corder = 0;           // conv_pipe_f16: channel-block-outer K order (set by launch_conv_pipe)
   int pipe_g = 0;                // conv_pipe: N-panels per tile-walk group (0: M-major walk; set at launch)
   int pipe_u = 1;                // conv_pipe: tap-unrolled loop for the per-tap-load 3x3 layers (set at launch)
-  int pipe_z = 0;                // always 0: conv_pipew's loop-carried opaque zero (keeps per-tap values in the loop)
+  int pipe_t0 = 0;               // conv_pipe: first tile of the launch (the tail of a conv_wide split)
   Epilogue e;
   // Fused YOLO head (conv_pipe_f16 only): a 1x1 conv over this conv's activated
   // output (cout <= 128 = one N tile), head_w fp16 [head_cout_pad][cout_pad] (k = c),
@@ -222,18 +262,13 @@ void launch_conv_pipe(const ConvArgs& a, hipStream_t s);
 bool head1x1_ok(const ConvArgs& a);
 void launch_head1x1(const ConvArgs& a, hipStream_t s);
 const char* head1x1_name(const ConvArgs& a);
-void set_head1x1(int v);  // conv.hip: 0 = stand-alone heads on conv_pipe (A/B)
 int conv_pipe_mode();
 int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 / 128 / 64)
-void set_pipe_bm(int v);                  // 0 = cost model, else forced
-void set_pipe_korder(int v);              // conv_pipe K order: 0 tap outer, 1 channel-block outer
-void set_pipe_win(int v);                 // conv_pipe window mode (3x3 s1 inputs staged once per channel block)
-void set_pipe_cost(int v);                // conv_pipe tile-rows objective: 0 latency (rounds), 1 throughput (CU-time)
-void set_pipe_wloop(int v);               // conv_pipe window mode: 1 = taps unrolled (default), 0 = cursor loop
-void set_pipe_walk(int v);                // conv_pipe tile walk: N-panels per group (0 = M-major)
-void set_pipe_pp(int v);                  // conv_pipe ping-pong K-loop schedule (f16)
-void set_pipe_pf(int v);                  // conv_pipe cross-tile prologue prefetch (register-epilogue layers)
 const char* conv_pipe_name(const ConvArgs& a);  // kernel symbol of that launch
+// conv_wide.hip: 256 x 256-tile window-mode twin of conv_pipew for the big 3x3 / s1 layers
+bool conv_wide_ok(const ConvArgs& a, int abl);
+int64_t conv_wide_tiles(const ConvArgs& a);
+void launch_conv_wide(const ConvArgs& a, int abl, int ntiles, int cus, hipStream_t s);
 // int8 twin (RTDM_I8): a.in = quantised contiguous int8 copy of the input, a.w8 int8
 // weights (per-channel activation scales folded in), a.deq per-output-channel scales
 bool conv_pipe_i8_ok(const ConvArgs& a);
@@ -241,14 +276,10 @@ void launch_conv_pipe_i8(const ConvArgs& a, hipStream_t s);
 const char* conv_pipe_i8_name(const ConvArgs& a);
 // diagnostics: conv_stem3 ablation builds (tools/ab_conv.py --key stem_abl)
 int stem_abl();
-void set_stem_abl(int v);
-void set_conv_pipe_mode(int v);
 // detector.cpp: plan conv -> 1x1 head -> [yolo] as one fused launch (default 1)
 int fuse_head();
-void set_fuse_head(int v);
 // detector.cpp: run independent branches (heads) on a second stream (default 1)
 int two_streams_mode();
-void set_two_streams_mode(int v);
 // Kernel symbol (template instantiation) launch_conv will pick for a / dtype.
 const char* conv_kernel_name(const ConvArgs& a, int dtype);
 // Row geometry helpers shared by host planners.
@@ -277,7 +308,6 @@ void launch_dw3_acff(const void* in, int in_cs, int in_co, int n, int h, int w, 
 void launch_dw3_sum(const void* in, int in_cs, int in_co, int n, int h, int w, int c, const float* wts,
                     const float* bsum, void* out, int dtype, hipStream_t s);
 bool dw3_sum_vec_ok(int c, int in_cs, int in_co, int dtype);
-void set_dw3_tile(int v);  // ops.hip: YOLO-ACFF depthwise on the LDS-tiled kernel (1) or the vector one (0)
 bool dw3_sum_tile_ok(int c, int in_cs, int in_co, int dtype);
 // acff.hip: fused ACFF block (dw3 -> concat -> 1x1 -> LeakyReLU -> BN affine -> opt. 2x2 pool), fp16
 bool acff_fused_ok(int cin, int cout_pad, int kpad);
@@ -315,9 +345,7 @@ void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in
                        int pool_pad, int ph, int pwid, const float* fcw, const float* fcb, float* logits, float* probs,
                        hipStream_t s, const AcffI8* q = nullptr /* [nst]; int8: k = branch*cin + c */);
 int acff_chain_mode();  // 1 = use acff_chain when the plan allows (default), 0 = per-stage kernels + tail
-void set_acff_chain_mode(int v);
 int acff_persist_mode();
-void set_acff_persist_mode(int v);
 void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, int stride, int pad, int zero_pad_rb,
                     View ov, int oh, int ow, int dtype, hipStream_t s);
 void launch_upsample(View iv, int n, int h, int w, int c, int f, View ov, int dtype, hipStream_t s);
@@ -344,7 +372,6 @@ struct ResizePlan {  // Pillow 8bpc antialiased bilinear, restricted to a center
 void build_resize_plan(ResizePlan& p, int in_h, int in_w, int out_size, bool upload);
 // 1 = streaming resize kernel (default), 0 = the staged band kernel (A/B knob)
 int resize_stream_mode();
-void set_resize_stream_mode(int v);
 // frames -> tmp (horizontal pass) -> out (vertical pass + crop + ToTensor + Normalize)
 void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_t* tmp, void* out,
                        int out_layout /*0: NHWC dtype, 1: NCHW f32*/, int dtype, hipStream_t s);
@@ -382,7 +409,6 @@ struct TrtYoloArgs {
 void launch_yolo_trt(const float* in, int n, const TrtYoloArgs& t, int nchw, float* out, hipStream_t s);
 
 size_t nms_workspace_size(int n, int n_anchors, int nc);
-void set_nms_variant(int v);  // diagnostics: bit 0 = bitonic sort only, bit 1 = no bitmask path
 void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label,
                 int agnostic, uint64_t class_mask, int max_det, void* ws, float* det, int32_t* idx,
                 int32_t* count, hipStream_t s);

@@ -1324,23 +1324,11 @@ static bool stem_ok(const ConvArgs& a) {
 // Pipelined 256x128 kernel (conv_pipe.hip) for the Cin % 64 == 0 layers; 0 = off
 // (conv_glds_f16 takes them).  RTDM_CONV_PIPE in the environment, or
 // rtdm_set_tuning("conv_pipe", v), for A/B runs.
-static int g_stem_abl = 0;
-int stem_abl() { return g_stem_abl; }
-void set_stem_abl(int v) { g_stem_abl = v; }
-static int g_conv_pipe = -1;
-int conv_pipe_mode() {
-  if (g_conv_pipe < 0) {
-    const char* e = getenv("RTDM_CONV_PIPE");
-    g_conv_pipe = e ? atoi(e) : 1;
-  }
-  return g_conv_pipe;
-}
-void set_conv_pipe_mode(int v) { g_conv_pipe = v < 0 ? 0 : v; }
+int stem_abl() { return tune().stem_abl; }
+int conv_pipe_mode() { return tune().conv_pipe; }
 
 // Stand-alone YOLO head convs on head1x1_f16 (head.hip); 0 = conv_pipe's decode epilogue
 // (rtdm_set_tuning("head1x1", v), for A/B runs; bit-identical either way).
-static int g_head1x1 = 1;
-void set_head1x1(int v) { g_head1x1 = v ? 1 : 0; }
 
 static bool use_pipe(const ConvArgs& a, int dtype) {
   return dtype == RTDM_F16 && (conv_pipe_mode() > 0 || a.head_w) && conv_pipe_ok(a);
@@ -1359,7 +1347,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     const int bn = direct_cfg(a.cout_pad).bn;
     return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
   }
-  if (dtype == RTDM_F16 && g_head1x1 && head1x1_ok(a)) return head1x1_name(a);
+  if (dtype == RTDM_F16 && tune().head1x1 && head1x1_ok(a)) return head1x1_name(a);
   if (use_pipe(a, dtype)) return conv_pipe_name(a);
   if (dtype == RTDM_F16 && glds_ok(a)) {
     static const char* names[2][2] = {{"conv_glds_f16<128,2>", "conv_glds_f16<128,3>"},
@@ -1404,7 +1392,7 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     launch_pool_small(a, s);
   } else if (dtype == RTDM_F16 && direct_ok(a)) {
     launch_direct(a, s);
-  } else if (dtype == RTDM_F16 && g_head1x1 && head1x1_ok(a)) {
+  } else if (dtype == RTDM_F16 && tune().head1x1 && head1x1_ok(a)) {
     launch_head1x1(a, s);
   } else if (use_pipe(a, dtype)) {
     launch_conv_pipe(a, s);

@@ -430,4 +430,145 @@ inline bool epi_lean_ok(const ConvArgs& a, bool allow_res = false) {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
+// Register epilogue of a lean conv_pipe / conv_wide tile (D^T accumulators: acc[tm][tn][r] =
+// output channel n_base + wn*CW + tn*16 + 4g + r of GEMM row m_base + wm*RW + tm*16 + fr;
+// RW / CW: rows / columns per wave).
+// Same per-element operations, in the same order, as epi_vec8_lean.
+// FIXED (cross-tile prefetch, see pipe_walk): the full-map output only (no pool / upsample,
+// no BN affine),
+// every store (and residual load) issued by every wave as a buffer op whose offset is out of
+// range for invalid lanes, so the epilogue issues exactly pipe_epi_ops() vector-memory ops and
+// the next tile can wait on its prefetched stage with an exact vmcnt.
+template <bool RES, int FM, int FN>
+__host__ __device__ constexpr int pipe_epi_ops() {
+  return FM * FN * (RES ? 2 : 1);
+}
+template <bool RES, int FM, int FN, int RW, int CW, bool FIXED = false, typename AccT, int NDQ>
+__device__ __forceinline__ void pipe_epi_regs(const ConvArgs& a, int m_base, int n_base, int wm, int wn, int lane,
+                                              const AccT (&acc)[FM][FN], const f4 (&rb)[FN], const f4 (&dq4)[NDQ]) {
+  constexpr bool I8 = !std::is_same_v<AccT, f4>;
+  const Epilogue& e = a.e;
+  const int fr = lane & 15, g = lane >> 4;
+  const bool leaky = e.act == ACT_LEAKY;
+  const float slope = e.slope;
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  typedef int i2 __attribute__((ext_vector_type(2)));
+  if constexpr (FIXED) {
+    // byte offsets < 2^31 - 16 (pipe_pf_ok); 0x7FFFFFF8 is past num_records: no-op store / zero load
+    const __amdgpu_buffer_rsrc_t rs_o =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((_Float16*)e.full.ptr + e.full.co), 0, 0x7FFFFFF0, 0x00020000);
+    __amdgpu_buffer_rsrc_t rs_r = rs_o;
+    if constexpr (RES)
+      rs_r = __builtin_amdgcn_make_buffer_rsrc((void*)((const _Float16*)e.res.ptr + e.res.co), 0, 0x7FFFFFF0,
+                                               0x00020000);
+#pragma unroll
+    for (int tm = 0; tm < FM; ++tm) {
+      const int m = m_base + wm * RW + tm * 16 + fr;
+      const bool mv = m < a.M;
+      int n = 0, oy = 0, ox = 0;
+      if (mv) row_to_pix(a, m, n, oy, ox);
+      const int pix = (n * a.oh + oy) * a.ow + ox;
+#pragma unroll
+      for (int tn = 0; tn < FN; ++tn) {
+        const int c0 = n_base + wn * CW + tn * 16 + 4 * g;
+        const bool ok = mv && c0 < a.cout;
+        f4 t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if constexpr (I8)
+            t[r] = (float)acc[tm][tn][r] * dq4[NDQ == FN ? tn : 0][r];
+          else
+            t[r] = acc[tm][tn][r];
+          t[r] = t[r] + rb[tn][r];
+          t[r] = leaky ? (t[r] > 0.f ? t[r] : t[r] * slope) : t[r];
+        }
+        if constexpr (RES) {
+          const int ro = ok ? (pix * e.res.cs + c0) * 2 : 0x7FFFFFF8;
+          const h4 rv = __builtin_bit_cast(h4, __builtin_amdgcn_raw_buffer_load_b64(rs_r, ro, 0, 0));
+          // the unconditional add would contract with the LeakyReLU product into
+          // fma(t, slope, r) (fp-contract=fast); the other epilogues round t * slope first
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            asm volatile("" : "+v"(t[r]));
+            t[r] += (float)rv[r];
+          }
+        }
+        h4 hv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hv[r] = (_Float16)t[r];
+        const int oo = ok ? (pix * e.full.cs + c0) * 2 : 0x7FFFFFF8;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i2, hv), rs_o, oo, 0, 0);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int tm = 0; tm < FM; ++tm) {
+    const int m = m_base + wm * RW + tm * 16 + fr;
+    const bool mv = m < a.M;
+    int n = 0, oy = 0, ox = 0;
+    if (mv) row_to_pix(a, m, n, oy, ox);
+    const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
+#pragma unroll
+    for (int tn = 0; tn < FN; ++tn) {
+      const int c0 = n_base + wn * CW + tn * 16 + 4 * g;
+      const bool cv = c0 < a.cout;  // cout % 8 == 0 (epi_lean_ok): all 4 or none
+      f4 t;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (I8)
+          t[r] = (float)acc[tm][tn][r] * dq4[NDQ == FN ? tn : 0][r];
+        else
+          t[r] = acc[tm][tn][r];
+        t[r] = t[r] + rb[tn][r];
+        t[r] = leaky ? (t[r] > 0.f ? t[r] : t[r] * slope) : t[r];
+      }
+      if (e.scale && cv) {
+        const f4 sc = *(const f4*)(e.scale + c0), sh = *(const f4*)(e.shift + c0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[r] = t[r] * sc[r] + sh[r];
+      }
+      if constexpr (RES) {
+        if (mv && cv) {
+          const h4 rv = *(const h4*)((const _Float16*)e.res.ptr + pix * e.res.cs + e.res.co + c0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t[r] += (float)rv[r];
+        }
+      }
+      h4 hv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hv[r] = (_Float16)t[r];
+      if (mv && cv) {
+        if (e.full.ptr) *(h4*)((_Float16*)e.full.ptr + pix * e.full.cs + e.full.co + c0) = hv;
+        if (e.up.ptr) {
+          const int uw = a.ow * 2;
+          const size_t u0 = ((size_t)n * a.oh * 2 + 2 * oy) * uw + 2 * ox;
+          _Float16* up = (_Float16*)e.up.ptr + e.up.co + c0;
+          *(h4*)(up + u0 * e.up.cs) = hv;
+          *(h4*)(up + (u0 + 1) * e.up.cs) = hv;
+          *(h4*)(up + (u0 + uw) * e.up.cs) = hv;
+          *(h4*)(up + (u0 + uw + 1) * e.up.cs) = hv;
+        }
+      }
+      if (e.pool.ptr) {  // quad order: rows 4q..4q+3 = lanes fr 4q..4q+3 (a DPP quad)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = t[r];
+          v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false)));
+          v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)));
+          t[r] = v;
+        }
+        if (mv && cv && (fr & 3) == 0) {
+          const size_t pp = ((size_t)n * a.qh + (oy >> 1)) * a.qw + (ox >> 1);
+          h4 pv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pv[r] = (_Float16)t[r];
+          *(h4*)((_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0) = pv;
+        }
+      }
+    }
+  }
+}
+
+
 }  // namespace rtdm

@@ -26,6 +26,8 @@
 // with the fused epilogues of conv_epi.h).
 #include "conv_epi.h"
 
+#include <algorithm>
+#include <mutex>
 #include <set>
 #include <string>
 #include <type_traits>
@@ -117,146 +119,6 @@ __device__ __forceinline__ void head_epi4(const ConvArgs& a, int m0, int c, f4 v
       o = __frcp_rn(1.f + __expf(-x));
     const size_t row = (size_t)n * e.io_rows + e.io_off + (size_t)ai * plane + (size_t)oy * a.ow + ox;
     e.io[row * e.no + k] = o;
-  }
-}
-
-// Register epilogue of a lean conv_pipe tile (D^T accumulators: acc[tm][tn][r] = output
-// channel n_base + wn*BN/WN + tn*16 + 4g + r of GEMM row m_base + wm*BM/WM + tm*16 + fr).
-// Same per-element operations, in the same order, as epi_vec8_lean.
-// FIXED (cross-tile prefetch, see pipe_walk): the full-map output only (no pool / upsample,
-// no BN affine),
-// every store (and residual load) issued by every wave as a buffer op whose offset is out of
-// range for invalid lanes, so the epilogue issues exactly pipe_epi_ops() vector-memory ops and
-// the next tile can wait on its prefetched stage with an exact vmcnt.
-template <bool RES, int FM, int FN>
-__host__ __device__ constexpr int pipe_epi_ops() {
-  return FM * FN * (RES ? 2 : 1);
-}
-template <bool RES, int FM, int FN, int WM, int WN, int BM, bool FIXED = false, typename AccT, int NDQ>
-__device__ __forceinline__ void pipe_epi_regs(const ConvArgs& a, int m_base, int n_base, int wm, int wn, int lane,
-                                              const AccT (&acc)[FM][FN], const f4 (&rb)[FN], const f4 (&dq4)[NDQ]) {
-  constexpr bool I8 = !std::is_same_v<AccT, f4>;
-  constexpr int BN = kPBN;
-  const Epilogue& e = a.e;
-  const int fr = lane & 15, g = lane >> 4;
-  const bool leaky = e.act == ACT_LEAKY;
-  const float slope = e.slope;
-  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-  typedef int i2 __attribute__((ext_vector_type(2)));
-  if constexpr (FIXED) {
-    // byte offsets < 2^31 - 16 (pipe_pf_ok); 0x7FFFFFF8 is past num_records: no-op store / zero load
-    const __amdgpu_buffer_rsrc_t rs_o =
-        __builtin_amdgcn_make_buffer_rsrc((void*)((_Float16*)e.full.ptr + e.full.co), 0, 0x7FFFFFF0, 0x00020000);
-    __amdgpu_buffer_rsrc_t rs_r = rs_o;
-    if constexpr (RES)
-      rs_r = __builtin_amdgcn_make_buffer_rsrc((void*)((const _Float16*)e.res.ptr + e.res.co), 0, 0x7FFFFFF0,
-                                               0x00020000);
-#pragma unroll
-    for (int tm = 0; tm < FM; ++tm) {
-      const int m = m_base + wm * (BM / WM) + tm * 16 + fr;
-      const bool mv = m < a.M;
-      int n = 0, oy = 0, ox = 0;
-      if (mv) row_to_pix(a, m, n, oy, ox);
-      const int pix = (n * a.oh + oy) * a.ow + ox;
-#pragma unroll
-      for (int tn = 0; tn < FN; ++tn) {
-        const int c0 = n_base + wn * (BN / WN) + tn * 16 + 4 * g;
-        const bool ok = mv && c0 < a.cout;
-        f4 t;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if constexpr (I8)
-            t[r] = (float)acc[tm][tn][r] * dq4[NDQ == FN ? tn : 0][r];
-          else
-            t[r] = acc[tm][tn][r];
-          t[r] = t[r] + rb[tn][r];
-          t[r] = leaky ? (t[r] > 0.f ? t[r] : t[r] * slope) : t[r];
-        }
-        if constexpr (RES) {
-          const int ro = ok ? (pix * e.res.cs + c0) * 2 : 0x7FFFFFF8;
-          const h4 rv = __builtin_bit_cast(h4, __builtin_amdgcn_raw_buffer_load_b64(rs_r, ro, 0, 0));
-          // the unconditional add would contract with the LeakyReLU product into
-          // fma(t, slope, r) (fp-contract=fast); the other epilogues round t * slope first
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            asm volatile("" : "+v"(t[r]));
-            t[r] += (float)rv[r];
-          }
-        }
-        h4 hv;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) hv[r] = (_Float16)t[r];
-        const int oo = ok ? (pix * e.full.cs + c0) * 2 : 0x7FFFFFF8;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i2, hv), rs_o, oo, 0, 0);
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int tm = 0; tm < FM; ++tm) {
-    const int m = m_base + wm * (BM / WM) + tm * 16 + fr;
-    const bool mv = m < a.M;
-    int n = 0, oy = 0, ox = 0;
-    if (mv) row_to_pix(a, m, n, oy, ox);
-    const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
-#pragma unroll
-    for (int tn = 0; tn < FN; ++tn) {
-      const int c0 = n_base + wn * (BN / WN) + tn * 16 + 4 * g;
-      const bool cv = c0 < a.cout;  // cout % 8 == 0 (epi_lean_ok): all 4 or none
-      f4 t;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr (I8)
-          t[r] = (float)acc[tm][tn][r] * dq4[NDQ == FN ? tn : 0][r];
-        else
-          t[r] = acc[tm][tn][r];
-        t[r] = t[r] + rb[tn][r];
-        t[r] = leaky ? (t[r] > 0.f ? t[r] : t[r] * slope) : t[r];
-      }
-      if (e.scale && cv) {
-        const f4 sc = *(const f4*)(e.scale + c0), sh = *(const f4*)(e.shift + c0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) t[r] = t[r] * sc[r] + sh[r];
-      }
-      if constexpr (RES) {
-        if (mv && cv) {
-          const h4 rv = *(const h4*)((const _Float16*)e.res.ptr + pix * e.res.cs + e.res.co + c0);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) t[r] += (float)rv[r];
-        }
-      }
-      h4 hv;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) hv[r] = (_Float16)t[r];
-      if (mv && cv) {
-        if (e.full.ptr) *(h4*)((_Float16*)e.full.ptr + pix * e.full.cs + e.full.co + c0) = hv;
-        if (e.up.ptr) {
-          const int uw = a.ow * 2;
-          const size_t u0 = ((size_t)n * a.oh * 2 + 2 * oy) * uw + 2 * ox;
-          _Float16* up = (_Float16*)e.up.ptr + e.up.co + c0;
-          *(h4*)(up + u0 * e.up.cs) = hv;
-          *(h4*)(up + (u0 + 1) * e.up.cs) = hv;
-          *(h4*)(up + (u0 + uw) * e.up.cs) = hv;
-          *(h4*)(up + (u0 + uw + 1) * e.up.cs) = hv;
-        }
-      }
-      if (e.pool.ptr) {  // quad order: rows 4q..4q+3 = lanes fr 4q..4q+3 (a DPP quad)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = t[r];
-          v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false)));
-          v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)));
-          t[r] = v;
-        }
-        if (mv && cv && (fr & 3) == 0) {
-          const size_t pp = ((size_t)n * a.qh + (oy >> 1)) * a.qw + (ox >> 1);
-          h4 pv;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) pv[r] = (_Float16)t[r];
-          *(h4*)((_Float16*)e.pool.ptr + pp * e.pool.cs + e.pool.co + c0) = pv;
-        }
-      }
-    }
   }
 }
 
@@ -625,12 +487,14 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     for (int r = 0; r < 8; ++r) wtab |= (uint32_t)((g ^ ((wm * (BM / WM) + fr + r) & 7)) & 7) << (3 * r);
   }
   const int lrow = (wm * (BM / WM) + fr) * BK * 2;
-  // The per-tap values derive from a loop-carried zero (zo *= a.pipe_z, which the host keeps
-  // 0; the compiler cannot know it), advanced in every body: otherwise the compiler hoists
-  // the 9 taps' shifts, weight-column offsets and tap-validity masks out of the channel-block
-  // loop, and the SGPRs / VGPRs they need spill (VGPR-lane reloads in the loop, scratch
-  // reloads whose vmcnt(0) drain the LDS-DMA pipeline).
-  int zo = a.pipe_z;
+  // The per-tap values derive from an opaque zero zo, re-made opaque in every body by an empty
+  // asm the compiler cannot see through (it must assume any value): otherwise the compiler
+  // hoists the 9 taps' shifts, weight-column offsets and tap-validity masks out of the
+  // channel-block loop, and the SGPRs / VGPRs they need spill (VGPR-lane reloads in the loop,
+  // scratch reloads whose vmcnt(0) drain the LDS-DMA pipeline).  (Round 3 used a loop-carried
+  // zo *= a.pipe_z with a host-side zero, which a compiler that specialised on the argument
+  // could have seen through.)
+  int zo = 0;
   auto waddr = [&](auto tt_, int par) {
     constexpr int TT = decltype(tt_)::value, KH = TT / 3, KW = TT % 3;
     const int iw_o = a.iw + zo;
@@ -799,8 +663,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       // ops of K-block s + 2 issued here (ABL bits 8192 / 16384: diagnostics without the window
       // slices / without the B loads)
       constexpr int VMS = STG ? ((ABL & 16384) ? 0 : NB) + (WIN ? (WOP && !(ABL & 8192) ? 1 : 0) : NA) : 0;
-      zo *= a.pipe_z;  // (a product, not a sum: an affine zo would be strength-reduced into
-                       // one induction register per derived value)
+      asm volatile("" : "+s"(zo));  // opaque: any value, as far as the compiler knows
       if constexpr (!(ABL & 2)) {
         if constexpr (WIN)
           wread1(std::integral_constant<int, T % 3>{});
@@ -1009,9 +872,9 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
         prologue_issue(make_geo(next));
         __builtin_amdgcn_sched_barrier(0);
       }
-      pipe_epi_regs<RES_, FM, FN, WM, WN, BM, true>(a, m_base, n_base, wm, wn, lane, acc, rb, dq4);
+      pipe_epi_regs<RES_, FM, FN, BM / WM, BN / WN, true>(a, m_base, n_base, wm, wn, lane, acc, rb, dq4);
     } else {
-      pipe_epi_regs<RES_, FM, FN, WM, WN, BM>(a, m_base, n_base, wm, wn, lane, acc, rb, dq4);
+      pipe_epi_regs<RES_, FM, FN, BM / WM, BN / WN>(a, m_base, n_base, wm, wn, lane, acc, rb, dq4);
     }
     return;
   }
@@ -1217,9 +1080,11 @@ __device__ __forceinline__ int pipe_tile_map(const ConvArgs& a, int t, int ntile
 
 template <int ABL, int BM, bool I8, bool WIN>
 __device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem_raw, int ntiles, bool pf) {
+  // tiles [a.pipe_t0, ntiles) (pipe_t0 > 0: the 256 x 128 tail of a conv_wide split)
   const int nb = gridDim.x, xcd = blockIdx.x & 7, l = blockIdx.x >> 3;
-  const int q = ntiles >> 3, r = ntiles & 7;
-  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int cnt = ntiles - a.pipe_t0;
+  const int q = cnt >> 3, r = cnt & 7;
+  const int lo = a.pipe_t0 + (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q);
   const int hi = lo + q + (xcd < r ? 1 : 0);
   const int bx = (nb - xcd + 7) >> 3;  // workgroups on this XCD (>= 1: this one)
   if constexpr (WIN) {  // the zero area: written once, outside every epilogue's LDS use
@@ -1299,45 +1164,46 @@ static int pipe_cus() {
 // fixed prologue / epilogue; the launch takes ceil(tiles / CUs) such rounds.  The
 // smallest estimated time wins (ties: the larger tile).  rtdm_set_tuning("conv_pipe_bm",
 // 256 | 128 | 64) forces one (0 = this model).  Batch-invariant: only the tiling changes.
-static int g_pipe_bm = 0;
-void set_pipe_bm(int v) { g_pipe_bm = (v == 256 || v == 128 || v == 64) ? v : 0; }
-static int pipe_bm_nk(const ConvArgs& a, int nk);
+static int pipe_bm_nk(const ConvArgs& a, int nk, double* est = nullptr);
 int pipe_bm(const ConvArgs& a) { return pipe_bm_nk(a, a.kpad / kPBK); }
 // Objective of the tile-rows model: 0 = latency (rounds of tiles over the CUs: a launch that
 // has the GPU to itself), 1 = throughput (CU-time: tiles x per-tile time, for several batches
 // in flight whose launches fill each other's idle CUs).  rtdm_set_tuning("conv_pipe_cost", v);
 // bench.py sets 1 with more than one batch in flight.  Throughput favours 256-row tiles:
 // b8 31.8k -> 33.0k, b16 36.9k -> 39.3k frames/s with 4 in flight (r03an, forced 256 rows).
-static int g_pipe_cost = 0;
-void set_pipe_cost(int v) { g_pipe_cost = v ? 1 : 0; }
 static bool pipe_win_ok(const ConvArgs& a, int bm);
-static int pipe_bm_nk(const ConvArgs& a, int nk) {
+static bool pipe_unroll(int abl);
+static int pipe_abl(const ConvArgs& a);
+static int pipe_bm_nk(const ConvArgs& a, int nk, double* est) {
   const bool head = a.head_w != nullptr;
-  if (g_pipe_bm && !(head && g_pipe_bm == 64)) return g_pipe_bm;
+  if (est) *est = 1e300;
+  if (tune().pipe_bm && !(head && tune().pipe_bm == 64)) return tune().pipe_bm;
   const int ntn = a.cout_pad / kPBN, cus = pipe_cus();
   static const int bms[3] = {256, 128, 64};
   // 256-row tiles of window-mode layers run the tap-unrolled window loop: ~1.2x the K-loop
   // rate of the per-tap-load 256-row tiles (b64 L10 / L14 on 256-row window tiles 0.0614 /
   // 0.0682 ms against 0.0664 / 0.0710 on the 128-row tiles this model picked without it, r03ak)
-  const double eff[3] = {!head && pipe_win_ok(a, 256) ? 1.2 : 1.0, 0.85, 0.65};
+  // (only when that launch will run the unrolled window loop: register-epilogue layers, no
+  // ping-pong; the LDS-epilogue window layers run the cursor loop, launch_abl_w0)
+  const double eff[3] = {!head && pipe_win_ok(a, 256) && pipe_unroll(pipe_abl(a)) && !tune().pipe_pp ? 1.2 : 1.0, 0.85,
+                         0.65};
   const double ovh = 3.0 + (head ? 4.0 : 0.0);
   int best = 256;
   double best_t = 1e300;
   for (int i = 0; i < (head ? 2 : 3); ++i) {
     const int64_t tiles = (int64_t)((a.M + bms[i] - 1) / bms[i]) * ntn;
-    const double rounds = g_pipe_cost ? (double)tiles : (double)((tiles + cus - 1) / cus);
+    const double rounds = tune().pipe_cost ? (double)tiles : (double)((tiles + cus - 1) / cus);
     const double t = rounds * (bms[i] / 256.0 * nk / eff[i] + ovh * bms[i] / 256.0 + 1.0);
     if (t < best_t * 0.97) {
       best_t = t;
       best = bms[i];
     }
   }
+  if (est) *est = best_t;
   return best;
 }
 
-static int g_pipe_korder = 1;
-void set_pipe_korder(int v) { g_pipe_korder = v ? 1 : 0; }
-static int g_pipe_korder_get() { return g_pipe_korder; }
+static int g_pipe_korder_get() { return tune().pipe_korder; }
 
 // Epilogue instantiation (ABL) of a launch: 8 fused head; 1024 stand-alone YOLO head
 // (decode into io only, epi_vec8_io); lean layers 640 (register
@@ -1357,10 +1223,8 @@ static int pipe_abl(const ConvArgs& a) {
 // 128-row tiles' 16 MFMAs per K-block the window addressing VALU costs more than the
 // A loads it saves, measured +10 % on yolov4-tiny L10 / L14).  rtdm_set_tuning("conv_pipe_win", 0)
 // turns it off (bit-identical either way).
-static int g_pipe_win = 1;
-void set_pipe_win(int v) { g_pipe_win = v ? 1 : 0; }
 static bool pipe_win_ok(const ConvArgs& a, int bm) {
-  return g_pipe_win && bm == 256 && a.cin % 64 == 0 && a.ks == 3 && a.stride == 1 && a.pad == 1 && !a.quad && a.pipe_corder &&
+  return tune().pipe_win && bm == 256 && a.cin % 64 == 0 && a.ks == 3 && a.stride == 1 && a.pad == 1 && !a.quad && a.pipe_corder &&
          a.ih == a.oh && a.iw == a.ow && bm + 2 * a.iw + 2 <= kWinRows &&
          (int64_t)a.n * a.ih * a.iw * a.in_cs * 2 < (1ll << 30);  // (the window op's 2^31 skip)
 }
@@ -1371,18 +1235,13 @@ static bool pipe_win_ok(const ConvArgs& a, int bm) {
 // front of them.  Needs nk >= NSt - 1 and byte offsets of the output / residual views
 // below 2^31 - 16 (the epilogue's fixed-count buffer ops).  rtdm_set_tuning("conv_pipe_pf", 0)
 // turns it off (bit-identical either way).
-static int g_pipe_pf = 1;
-void set_pipe_pf(int v) { g_pipe_pf = v ? 1 : 0; }
 // Ping-pong schedule (ABL bit 2048, f16 only): rtdm_set_tuning("conv_pipe_pp", 1) turns it
 // on (bit-identical either way; measured slower, so off by default).
-static int g_pipe_pp = 0;
-void set_pipe_pp(int v) { g_pipe_pp = v ? 1 : 0; }
 
 // Tile walk (pipe_tile_map): N-panels per group; 0 = the M-major walk.  rtdm_set_tuning(
 // "conv_pipe_walk", g).  Bit-identical for every g (only the order tiles run in changes).
 // Default 2: yolov4-tiny@608 b64 L12 (8 N-panels) fetches 39 % fewer bytes past L2 (PMC
 // FETCH_SIZE, r03l) at the same time (0.2007 vs 0.2009 ms).
-static int g_pipe_walk = 2;
 // 3x3 K-loops: 1 = taps unrolled (default: WLOOP for window mode, the run-time uloop path for
 // the per-tap-load layers), 0 = the generic cursor loop (window mode: ABL bit 4096; A/B
 // diagnostics).  rtdm_set_tuning("conv_pipe_wloop", v); bit-identical either way.
@@ -1391,17 +1250,14 @@ static int g_pipe_walk = 2;
 // measured 2-3 % slower with it at b64 (r03aa: L6 0.1047 -> 0.1081 ms, L28 0.2592 -> 0.2662):
 // their kernels hold more registers across the loop and the unrolled loop's spill reloads
 // land in the tile prologue.
-static int g_pipe_wloop = 1;
-void set_pipe_wloop(int v) { g_pipe_wloop = v ? 1 : 0; }
-static bool pipe_unroll(int abl) { return g_pipe_wloop && (abl & 512) != 0; }
-void set_pipe_walk(int v) { g_pipe_walk = v > 0 ? v : 0; }
+static bool pipe_unroll(int abl) { return tune().pipe_wloop && (abl & 512) != 0; }
 static int pipe_walk_g(const ConvArgs& a) {
   const int ntn = a.cout_pad / kPBN;
-  return g_pipe_walk > 0 && g_pipe_walk < ntn && ntn % g_pipe_walk == 0 ? g_pipe_walk : 0;
+  return tune().pipe_walk > 0 && tune().pipe_walk < ntn && ntn % tune().pipe_walk == 0 ? tune().pipe_walk : 0;
 }
 
 static bool pipe_pf_ok(const ConvArgs& a, int abl, int nk) {
-  if (!g_pipe_pf || nk < kPNS - 1 || (abl & 2048)) return false;
+  if (!tune().pipe_pf || nk < kPNS - 1 || (abl & 2048)) return false;
   if (abl == 8) return true;  // fused head: prefetch after the head GEMM, before the decode
   if (!(abl & 512) || !a.e.full.ptr || a.e.pool.ptr || a.e.up.ptr || a.e.scale) return false;
   const int64_t pix = (int64_t)a.n * a.oh * a.ow;
@@ -1409,6 +1265,50 @@ static bool pipe_pf_ok(const ConvArgs& a, int abl, int nk) {
   if ((pix * a.e.full.cs) * 2 >= lim) return false;
   if (a.e.res.ptr && (pix * a.e.res.cs) * 2 >= lim) return false;
   return true;
+}
+
+// conv_wide (conv_wide.hip): 256 x 256 tiles for the window-mode register-epilogue layers.
+// A wide tile is two 256 x 128 tiles' work; it runs them at wide_eff x the K-loop rate (64 x 128
+// per wave: 3/4 of the LDS read bytes, half the barriers and 5/6 of the LDS-DMA ops per FLOP),
+// but there are half as many, so a launch of U wide tiles over the CUs quantises twice as coarsely.
+// Options, in the units of pipe_bm_nk (latency objective: rounds of tiles over the CUs; throughput
+// objective: CU-time):
+//   * the best conv_pipe tiling alone (pipe_bm_nk);
+//   * all wide tiles;
+//   * split: whole rounds of wide tiles, then the remaining wide units as 256 x 128 conv_pipew
+//     tiles (twice as many, so they fill the last round twice as evenly) in a second launch.
+// Returns the wide tiles of the first launch (0: conv_pipe alone); *split: a tail follows.
+// rtdm_set_tuning("conv_wide", 0 off | 1 model | 2 all wide | 3 split), ("conv_wide_eff", x100).
+static int wide_plan(const ConvArgs& a, bool* split) {
+  *split = false;
+  if (!tune().pipe_wide || tune().pipe_pp || conv_pipe_mode() != 1 || a.head_w || !conv_wide_ok(a, pipe_abl(a))) return 0;
+  const int64_t U = conv_wide_tiles(a);
+  const int cus = pipe_cus();
+  const bool can_split = a.cout_pad % 256 == 0 && U > cus;  // tail tile t = 2 x its wide unit
+  if (tune().pipe_wide == 2) return (int)U;
+  if (tune().pipe_wide == 3) {
+    *split = can_split;
+    return can_split ? (int)(U / cus) * cus : (int)U;
+  }
+  const int nk = a.kpad / kPBK;
+  double small = 0.0;
+  pipe_bm_nk(a, nk, &small);  // the best conv_pipe tiling (window credit included)
+  const double ovh = 3.0;
+  const double ts = nk / 1.2 + ovh + 1.0;                                     // a 256 x 128 window tile
+  const double tw = 2.0 * nk / (1.2 * tune().pipe_wide_eff / 100.0) + 2.0 * ovh + 1.0;  // a 256 x 256 tile
+  auto rounds = [&](int64_t t) { return tune().pipe_cost ? (double)t : (double)((t + cus - 1) / cus); };
+  const double all = rounds(U) * tw;
+  double sp = 1e300;
+  if (can_split && !tune().pipe_cost) {
+    const int64_t full = U / cus, rem = U - full * cus;
+    sp = full * tw + rounds(2 * rem) * ts;
+  }
+  if (std::min(all, sp) >= small * 0.97) return 0;
+  if (sp < all) {
+    *split = true;
+    return (int)((U / cus) * cus);
+  }
+  return (int)U;
 }
 
 #define RTDM_PIPE_KERNEL(NAME)                                                                  \
@@ -1471,7 +1371,7 @@ static void launch_abl_w0(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int
 
 template <int BM>
 static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid, bool win) {
-  const int abl = pipe_abl(a) | (g_pipe_pp ? 2048 : 0), pf = pipe_pf_ok(a, abl, a.kpad / kPBK) ? 1 : 0;
+  const int abl = pipe_abl(a) | (tune().pipe_pp ? 2048 : 0), pf = pipe_pf_ok(a, abl, a.kpad / kPBK) ? 1 : 0;
   if constexpr (BM >= 128) {
     if (win && BM == 256 && !pipe_unroll(abl) && !(abl & 2048))
       return launch_abl_w0<conv_pipew_f16_k, BM>(abl, grid, s, a, ntiles, pf);
@@ -1483,6 +1383,8 @@ static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 gr
 // kernel symbol of a launch, e.g. conv_pipew_f16<640,256> (the ping-pong schedule, ABL bit
 // 2048, as conv_pipewpp_f16<640,256>); the strings live in a set (stable pointers)
 static const char* pipe_name(bool i8, bool win, int abl, int bm) {
+  static std::mutex mu;  // (handles may be planned on several threads)
+  std::lock_guard<std::mutex> lk(mu);
   static std::set<std::string> names;
   char b[48];
   snprintf(b, sizeof b, "conv_pipe%s%s_%s<%d,%d>", win ? ((abl & 4096) ? "w0" : "w") : "", (abl & 2048) ? "pp" : "",
@@ -1493,11 +1395,19 @@ static const char* pipe_name(bool i8, bool win, int abl, int bm) {
 const char* conv_pipe_name(const ConvArgs& a_in) {
   ConvArgs a = a_in;
   a.pipe_corder = g_pipe_korder_get() && a.ks == 3 && a.cin % 64 == 0 ? 1 : 0;
+  {
+    bool split = false;
+    if (wide_plan(a, &split) > 0) {  // (the step's time covers the tail launch too)
+      static const char* names[2][2] = {{"conv_wide_f16<640>", "conv_wide_f16<640>+tail"},
+                                        {"conv_wide_f16<896>", "conv_wide_f16<896>+tail"}};
+      return names[pipe_abl(a) == 896][split ? 1 : 0];
+    }
+  }
   const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
   const bool abl_mode = a.head_w || conv_pipe_mode() <= 1 || conv_pipe_mode() == 13;
   const bool win = abl_mode && pipe_win_ok(a, bm);
   return pipe_name(false, win,
-                   pipe_abl(a) | (abl_mode && g_pipe_pp ? 2048 : 0) | (win && !pipe_unroll(pipe_abl(a)) && !g_pipe_pp ? 4096 : 0),
+                   pipe_abl(a) | (abl_mode && tune().pipe_pp ? 2048 : 0) | (win && !pipe_unroll(pipe_abl(a)) && !tune().pipe_pp ? 4096 : 0),
                    bm);
 }
 
@@ -1509,9 +1419,25 @@ const char* conv_pipe_name(const ConvArgs& a_in) {
 
 void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
   ConvArgs a = a_in;
-  a.pipe_corder = g_pipe_korder && a.ks == 3 && a.cin % 64 == 0 ? 1 : 0;
+  a.pipe_corder = tune().pipe_korder && a.ks == 3 && a.cin % 64 == 0 ? 1 : 0;
   a.pipe_g = pipe_walk_g(a);
   a.pipe_u = pipe_unroll(pipe_abl(a)) ? 1 : 0;
+  {
+    bool split = false;
+    const int nw = wide_plan(a, &split);
+    if (nw > 0) {
+      launch_conv_wide(a, pipe_abl(a), nw, pipe_cus(), s);
+      if (split) {  // the remaining wide units as 256 x 128 window tiles [2 nw, 2 U) of the M-major walk
+        ConvArgs b = a;
+        b.pipe_g = 0;
+        b.pipe_t0 = 2 * nw;
+        const int nt2 = (int)(2 * conv_wide_tiles(a));
+        const int cnt = nt2 - b.pipe_t0;
+        launch_pipe_bm<256>(b, s, nt2, dim3((unsigned)(cnt < pipe_cus() ? cnt : pipe_cus())), true);
+      }
+      return;
+    }
+  }
   const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
   const int64_t nt = (int64_t)((a.M + bm - 1) / bm) * (a.cout_pad / kPBN);
   RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
@@ -1587,15 +1513,16 @@ bool conv_pipe_i8_ok(const ConvArgs& a) {
 
 const char* conv_pipe_i8_name(const ConvArgs& a_in) {
   ConvArgs a = a_in;
-  a.pipe_corder = g_pipe_korder && a.ks == 3 ? 1 : 0;
+  a.pipe_corder = tune().pipe_korder && a.ks == 3 ? 1 : 0;
   const int bm = pipe_bm_nk(a, a.kpad / 128);
-  return pipe_name(true, pipe_win_ok(a, bm), pipe_abl(a), bm);
+  const bool win = pipe_win_ok(a, bm);
+  return pipe_name(true, win, pipe_abl(a) | (win && !pipe_unroll(pipe_abl(a)) ? 4096 : 0), bm);
 }
 
 void launch_conv_pipe_i8(const ConvArgs& a_in, hipStream_t s) {
   ConvArgs a = a_in;
   RTDM_REQUIRE(conv_pipe_i8_ok(a), RTDM_E_INVALID, "conv_pipe_i8: unsupported layer");
-  a.pipe_corder = g_pipe_korder && a.ks == 3 ? 1 : 0;
+  a.pipe_corder = tune().pipe_korder && a.ks == 3 ? 1 : 0;
   a.pipe_g = pipe_walk_g(a);
   a.pipe_u = pipe_unroll(pipe_abl(a)) ? 1 : 0;
   const int bm = pipe_bm_nk(a, a.kpad / 128);
@@ -1606,7 +1533,9 @@ void launch_conv_pipe_i8(const ConvArgs& a_in, hipStream_t s) {
   const bool win = pipe_win_ok(a, bm);
   const int abl = pipe_abl(a), pf = pipe_pf_ok(a, abl, a.kpad / 128) ? 1 : 0;
   if (bm == 256) {
-    if (win)
+    if (win && !pipe_unroll(abl))  // the cursor window loop, as the f16 path (launch_pipe_bm)
+      launch_abl_w0<conv_pipew_i8_k, 256>(abl, grid, s, a, ntiles, pf);
+    else if (win)
       launch_abl<conv_pipew_i8_k, 256>(abl, grid, s, a, ntiles, pf);
     else
       launch_abl<conv_pipe_i8_k, 256>(abl, grid, s, a, ntiles, pf);

@@ -167,6 +167,7 @@ struct YoloHead {
 
 struct rtdm_detector_s {
   int img_h = 0, img_w = 0, dtype = 0, max_batch = 0, dev = 0;
+  rtdm::Tuning tuning;  // this handle's knobs (rtdm_detector_set_tuning; the defaults at create)
   bool planning_only = true;
   // RTDM_I8: activations fp16 (dtype = RTDM_F16) in the arena; the Cin % 128 == 0 convs
   // run conv_pipe_i8 on a per-channel int8 copy of their input once calibrated
@@ -214,9 +215,7 @@ struct rtdm_detector_s {
 
 namespace rtdm {
 
-static int g_fuse_head = 1;
-int fuse_head() { return g_fuse_head; }
-void set_fuse_head(int v) { g_fuse_head = v ? 1 : 0; }
+int fuse_head() { return tune().fuse_head; }
 
 static size_t esize_of(int dtype) { return dtype == RTDM_F16 ? 2 : 4; }
 
@@ -1117,9 +1116,7 @@ static void step_info(const rtdm_detector_s& h, const Step& st, std::string& nam
 // (FLOP + 312 FLOP per HBM byte ~ time at the chip's peaks) stays on the
 // producer's stream and the others run on the other stream — in the YOLO
 // graphs these are the detection-head branches, which then overlap the trunk.
-static int g_two_streams = 1;
-int two_streams_mode() { return g_two_streams; }
-void set_two_streams_mode(int v) { g_two_streams = v ? 1 : 0; }
+int two_streams_mode() { return tune().two_streams; }
 
 static void schedule_streams(rtdm_detector_s& h) {
   const int ns = (int)h.steps.size();
@@ -1255,6 +1252,8 @@ rtdm_status rtdm_detector_create(const char* cfg_text, int img_h, int img_w, int
                  "detector_create: bad dtype");
     RTDM_REQUIRE(max_batch > 0, RTDM_E_INVALID, "detector_create: max_batch must be > 0");
     auto h = std::make_unique<rtdm_detector_s>();
+    h->tuning = default_tuning();
+    TuningScope ts_(&h->tuning);  // the plan (fused heads, streams) follows this handle's knobs
     h->img_h = img_h;
     h->img_w = img_w;
     h->int8 = dtype == RTDM_I8;
@@ -1271,12 +1270,21 @@ rtdm_status rtdm_detector_create(const char* cfg_text, int img_h, int img_w, int
   });
 }
 
+rtdm_status rtdm_detector_set_tuning(rtdm_detector h, const char* key, int value) {
+  return guard([&] {
+    RTDM_REQUIRE(h, RTDM_E_INVALID, "detector_set_tuning: NULL handle");
+    tuning_set(h->tuning, key, value);
+  });
+}
+
 rtdm_status rtdm_detector_destroy(rtdm_detector h) {
   return guard([&] { delete h; });
+    TuningScope ts_(h ? &h->tuning : nullptr);
 }
 
 rtdm_status rtdm_detector_get_info(rtdm_detector h, rtdm_detector_info* info) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h && info, RTDM_E_INVALID, "detector_get_info: NULL argument");
     info->img_h = h->img_h;
     info->img_w = h->img_w;
@@ -1293,6 +1301,7 @@ rtdm_status rtdm_detector_get_info(rtdm_detector h, rtdm_detector_info* info) {
 
 int64_t rtdm_detector_describe(rtdm_detector h, char* buf, int64_t buf_len) {
   if (!h) return 0;
+  TuningScope ts_(&h->tuning);
   const std::string s = describe(*h);
   const int64_t need = (int64_t)s.size() + 1;
   if (buf && buf_len >= need) std::memcpy(buf, s.c_str(), need);
@@ -1304,6 +1313,7 @@ int rtdm_detector_num_steps(rtdm_detector h) { return h ? (int)h->steps.size() :
 rtdm_status rtdm_detector_step_info(rtdm_detector h, int step, char* name, int name_len, int* layer,
                                     double* flop_per_image, double* bytes_per_image) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h && step >= 0 && step < (int)h->steps.size(), RTDM_E_INVALID, "step_info: bad step");
     std::string nm;
     double f = 0, b = 0;
@@ -1320,6 +1330,7 @@ rtdm_status rtdm_detector_step_info(rtdm_detector h, int step, char* name, int n
 
 rtdm_status rtdm_detector_enable_timing(rtdm_detector h, int max_calls) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h && !h->planning_only, RTDM_E_INVALID, "enable_timing: bad handle");
     for (hipEvent_t e : h->events) (void)hipEventDestroy(e);
     h->events.clear();
@@ -1334,6 +1345,7 @@ rtdm_status rtdm_detector_enable_timing(rtdm_detector h, int max_calls) {
 
 rtdm_status rtdm_detector_read_timing(rtdm_detector h, double* ms_per_step, int* calls) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "read_timing: NULL handle");
     const size_t ns = h->steps.size();
     for (size_t i = 0; i < ns; ++i) ms_per_step[i] = 0.0;
@@ -1352,6 +1364,7 @@ rtdm_status rtdm_detector_read_timing(rtdm_detector h, double* ms_per_step, int*
 
 rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float* io, void* stream) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "detect: NULL handle");
     run_detector(*h, x, x_kind, n, io, (hipStream_t)stream);
   });
@@ -1359,6 +1372,7 @@ rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float
 
 rtdm_status rtdm_detector_calibrate(rtdm_detector h, const void* x, int x_kind, int n, int reset, void* stream) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "calibrate: NULL handle");
     RTDM_REQUIRE(h->int8, RTDM_E_INVALID, "calibrate: handle is not RTDM_I8");
     if (h->n_q == 0) {
@@ -1421,6 +1435,7 @@ rtdm_status rtdm_detector_calibrate(rtdm_detector h, const void* x, int x_kind, 
 
 rtdm_status rtdm_detect_raw(rtdm_detector h, const void* x, int x_kind, int n, float* p, void* stream) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "detect_raw: NULL handle");
     run_detector(*h, x, x_kind, n, p, (hipStream_t)stream, 1);
   });
@@ -1428,6 +1443,7 @@ rtdm_status rtdm_detect_raw(rtdm_detector h, const void* x, int x_kind, int n, f
 
 rtdm_status rtdm_detect_trt(rtdm_detector h, const void* x, int x_kind, int n, float* dets, void* stream) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "detect_trt: NULL handle");
     RTDM_REQUIRE(!h->planning_only, RTDM_E_INVALID, "detect_trt: handle was created without weights");
     RTDM_REQUIRE(n >= 0 && n <= h->max_batch, RTDM_E_CAPACITY, "detect_trt: batch exceeds max_batch");
@@ -1465,6 +1481,7 @@ rtdm_status rtdm_detect_trt(rtdm_detector h, const void* x, int x_kind, int n, f
 rtdm_status rtdm_detector_layer_output(rtdm_detector h, int layer, int n, float* out, int64_t out_numel, int* c,
                                        int* hgt, int* wid, void* stream) {
   return guard([&] {
+    TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "layer_output: NULL handle");
     RTDM_REQUIRE(layer >= 0 && layer < (int)h->defs.size(), RTDM_E_INVALID, "layer_output: bad layer");
     const int t = h->layer_tensor[layer];

@@ -318,10 +318,8 @@ __global__ __launch_bounds__(256, 2) void dw3_sum_tile_kernel(const _Float16* __
   }
 }
 
-static int g_dw3_tile = 1;  // 0: the per-pixel vector kernel (same sum order, for A/B and tests)
-void set_dw3_tile(int v) { g_dw3_tile = v ? 1 : 0; }
 bool dw3_sum_tile_ok(int c, int in_cs, int in_co, int dtype) {
-  return g_dw3_tile && dtype == RTDM_F16 && c % kDwCS == 0 && in_cs % 8 == 0 && in_co % 8 == 0;
+  return tune().dw3_tile && dtype == RTDM_F16 && c % kDwCS == 0 && in_cs % 8 == 0 && in_co % 8 == 0;
 }
 
 bool dw3_sum_vec_ok(int c, int in_cs, int in_co, int dtype) {
@@ -1200,9 +1198,7 @@ __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __res
   }
 }
 
-static int g_resize_stream = 1;
-int resize_stream_mode() { return g_resize_stream; }
-void set_resize_stream_mode(int v) { g_resize_stream = v; }
+int resize_stream_mode() { return tune().resize_stream; }
 
 // LDS of the staged kernel: coefficients + bounds + band source rows + band tmp rows.
 static size_t resize_staged_lds(const ResizePlan& p, int col_bytes16) {
@@ -1877,8 +1873,6 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
 #undef NMS_STAMP
 }
 
-static int g_nms_variant = 0;
-void set_nms_variant(int v) { g_nms_variant = v; }
 void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label, int agnostic,
                 uint64_t class_mask, int max_det, void* ws, float* det, int32_t* idx, int32_t* count,
                 hipStream_t s) {
@@ -1889,7 +1883,7 @@ void launch_nms(const float* io, int n, int n_anchors, int no, float conf, doubl
   hipLaunchKernelGGL(nms_cand_kernel, dim3(nms_nblk(n_anchors), n), dim3(kNmsCandBlk), 0, s, io, n_anchors, no, conf,
                      multi_label, class_mask, ws, cap);
   hipLaunchKernelGGL(nms_kernel, dim3(n), dim3(kNmsThreads), 0, s, io, n_anchors, no, conf, iou, multi_label,
-                     agnostic, class_mask, max_det, ws, cap, det, idx, count, g_nms_variant);
+                     agnostic, class_mask, max_det, ws, cap, det, idx, count, tune().nms_variant);
   RTDM_HIP(hipGetLastError());
 }
 

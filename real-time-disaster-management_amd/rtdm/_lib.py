@@ -56,6 +56,8 @@ SIGNATURES = {
     "rtdm_last_error": (c_char_p, []),
     "rtdm_build_arch": (c_char_p, []),
     "rtdm_set_tuning": (c_int, [c_char_p, c_int]),
+    "rtdm_detector_set_tuning": (c_int, [c_void_p, c_char_p, c_int]),
+    "rtdm_classifier_set_tuning": (c_int, [c_void_p, c_char_p, c_int]),
     "rtdm_classifier_create": (c_int, [c_int, c_int, POINTER(rtdm_param), c_int, c_int, POINTER(c_void_p)]),
     "rtdm_classifier_destroy": (c_int, [c_void_p]),
     "rtdm_classifier_input_size": (c_int, [c_void_p]),

@@ -144,12 +144,23 @@ class _ACFFClassifier(torch.nn.Module):
                                                ctypes.byref(h)))
         self._handle = h
         self._handle_key = (key, cap)
+        for k, v in getattr(self, "tuning", {}).items():
+            L.check(L.lib().rtdm_classifier_set_tuning(h, k.encode(), int(v)))
         # a new device handle: cached hipGraphs that captured the old one must not replay
         # (rtdm.pipeline keys its graphs on this counter, never on the handle address)
         self.handle_generation = getattr(self, "handle_generation", 0) + 1
         if self._dtype == L.RTDM_I8:
             self._calibrate(h)
         return h
+
+    def set_tuning(self, key: str, value: int):
+        """One knob of rtdm_set_tuning for this model's handles only."""
+        if not hasattr(self, "tuning"):
+            self.tuning = {}
+        self.tuning[key] = int(value)
+        if self._handle is not None:
+            L.check(L.lib().rtdm_classifier_set_tuning(self._handle, key.encode(), int(value)))
+        return self
 
     def describe(self, n: int = 1) -> str:
         """Text dump of the launch plan (one line per ACFF block: kernel, int8) of a handle for n."""

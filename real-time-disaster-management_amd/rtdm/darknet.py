@@ -69,6 +69,7 @@ class Darknet(torch.nn.Module):
         self._dtype = L.RTDM_F32
         self._handle = None
         self._handle_key = None
+        self.tuning = {}  # this model's own knobs (rtdm_detector_set_tuning), re-applied to every new handle
         self.info = self._plan_info()
         self.version = np.array([0, 2, 5], dtype=np.int32)
         self.seen = np.array([0], dtype=np.int64)
@@ -174,12 +175,23 @@ class Darknet(torch.nn.Module):
                                              self._stream.size, cap, ctypes.byref(h)))
         self._handle = h
         self._handle_key = (key, cap)
+        for k, v in self.tuning.items():
+            L.check(L.lib().rtdm_detector_set_tuning(h, k.encode(), int(v)))
         # a new device handle: cached hipGraphs that captured the old one must not replay
         # (rtdm.pipeline keys its graphs on this counter, never on the handle address)
         self.handle_generation = getattr(self, "handle_generation", 0) + 1
         if self._dtype == L.RTDM_I8:
             self._calibrate(h)
         return h
+
+    def set_tuning(self, key: str, value: int):
+        """One launch-time knob of rtdm_set_tuning for this model only (its handles; the
+        process defaults and other models are unchanged): e.g. ("conv_pipe_cost", 1) plans the
+        conv tiles for throughput when several batches are in flight."""
+        self.tuning[key] = int(value)
+        if self._handle is not None:
+            L.check(L.lib().rtdm_detector_set_tuning(self._handle, key.encode(), int(value)))
+        return self
 
     # ---------------------------------------------------------------- forward --
     def forward(self, x: torch.Tensor, out: torch.Tensor | None = None, stream=None):
