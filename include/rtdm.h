@@ -142,10 +142,10 @@ const char* rtdm_build_arch(void);
  * alternating MFMA and memory phases; default 0: measured 4-18 % slower per layer,
  * DESIGN.md §3.4); "conv_pipe_wloop" 1 = tap-unrolled 3x3 K-loop for the
  * register-epilogue layers (default), 0 = the cursor loop; "conv_pipe_walk" g =
- * tile walk in N-groups of g panels (default 2, 0 = M-major); "conv_wide" 1 = the
- * 256x256-tile kernel where the cost model picks it (default) | 0 off | 2 always |
- * 3 one round of wide tiles + a 256x128 tail; "conv_wide_eff" its cost-model rate
- * (x100).  Unknown keys: RTDM_E_INVALID. */
+ * tile walk in N-groups of g panels (default 2, 0 = M-major); "conv_wide" 0 = off
+ * (default: the 256x256-tile kernel measured slower) | 1 = where the
+ * cost model picks it | 2 always | 3 one round of wide tiles + a 256x128 tail;
+ * "conv_wide_eff" its cost-model rate (x100).  Unknown keys: RTDM_E_INVALID. */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 /* The same keys on one handle's own copy (see above). */
 rtdm_status rtdm_detector_set_tuning(rtdm_detector h, const char* key, int value);

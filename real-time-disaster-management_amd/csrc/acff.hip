@@ -888,13 +888,16 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
             bpre[ks][1] = *(const h8*)(wrow + (size_t)16 * st.kpad + ks * 32);
           }
       }
-      for (int i = tid; i < ((a.abl & 1) ? 0 : M * CG); i += kChainThreads) {
-        const int m = i / CG, v = i - m * CG;
+      // one (pixel m, 8-channel group v) item: bias, then the 9 taps in (kh, kw) order (fp32
+      // FMAs, acff_fused's sequence) -> the A chunk (fp16, or int8 quantised)
+      auto dw_item = [&](int m, int v, const f4 (&wk)[9][2], const f4 (&bk)[2]) {
         const int oy = m / OH, ox = m - oy * OH;
         float t[8];
-        const float4 b0 = *(const float4*)(bb + v * 8), b1 = *(const float4*)(bb + v * 8 + 4);
-        t[0] = b0.x; t[1] = b0.y; t[2] = b0.z; t[3] = b0.w;
-        t[4] = b1.x; t[5] = b1.y; t[6] = b1.z; t[7] = b1.w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          t[j] = bk[0][j];
+          t[4 + j] = bk[1][j];
+        }
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
@@ -902,16 +905,13 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
             const int y = oy + 1 + (kh - 1) * d, x = ox + 1 + (kw - 1) * d;
             h8 xv = h8{0, 0, 0, 0, 0, 0, 0, 0};
             if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)H) xv = *(const h8*)(X + (size_t)(y * H + x) * C + v * 8);
-            const float* wp = wb + (kh * 3 + kw) * C + v * 8;
-            const float4 w0 = *(const float4*)wp, w1 = *(const float4*)(wp + 4);
-            t[0] = fmaf(w0.x, (float)xv[0], t[0]);
-            t[1] = fmaf(w0.y, (float)xv[1], t[1]);
-            t[2] = fmaf(w0.z, (float)xv[2], t[2]);
-            t[3] = fmaf(w0.w, (float)xv[3], t[3]);
-            t[4] = fmaf(w1.x, (float)xv[4], t[4]);
-            t[5] = fmaf(w1.y, (float)xv[5], t[5]);
-            t[6] = fmaf(w1.z, (float)xv[6], t[6]);
-            t[7] = fmaf(w1.w, (float)xv[7], t[7]);
+            const f4& w0 = wk[kh * 3 + kw][0];
+            const f4& w1 = wk[kh * 3 + kw][1];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              t[j] = fmaf(w0[j], (float)xv[j], t[j]);
+              t[4 + j] = fmaf(w1[j], (float)xv[4 + j], t[4 + j]);
+            }
           }
         if constexpr (I8) {
           const float* ip = wsm + 30 * C + br * C + v * 8;
@@ -936,6 +936,25 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
             for (int j = 0; j < 8; ++j)
               if (t[j] != 0.f) atomicMax(st.amax + br * C + v * 8 + j, __float_as_uint(fabsf(t[j])));
           }
+        }
+      };
+      auto wtaps = [&](int v, f4 (&wk)[9][2], f4 (&bk)[2]) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          wk[k][0] = *(const f4*)(wb + k * C + v * 8);
+          wk[k][1] = *(const f4*)(wb + k * C + v * 8 + 4);
+        }
+        bk[0] = *(const f4*)(bb + v * 8);
+        bk[1] = *(const f4*)(bb + v * 8 + 4);
+      };
+      if (!(a.abl & 1)) {
+        // a thread keeps one channel group (its 72 tap weights + 8 biases in registers) and
+        // walks the pixels: per tap one 16-byte LDS read (the activation) instead of three
+        const int pstep = kChainThreads / CG, v = tid % CG;
+        if (tid < pstep * CG) {
+          f4 wk[9][2], bk[2];
+          wtaps(v, wk, bk);
+          for (int m = tid / CG; m < M; m += pstep) dw_item(m, v, wk, bk);
         }
       }
       __syncthreads();

@@ -192,7 +192,7 @@ struct Tuning {
   int pipe_pp = 0;          // conv_pipe ping-pong K-loop schedule
   int pipe_walk = 2;        // conv_pipe tile walk: N-panels per group (0 = M-major)
   int pipe_wloop = 1;       // conv_pipe tap-unrolled 3x3 K-loops
-  int pipe_wide = 1;        // conv_wide: 0 off, 1 cost model, 2 all 256 x 256 tiles, 3 one round + 256 x 128 tail
+  int pipe_wide = 0;        // conv_wide: 0 off (default: measured slower, r04b), 1 cost model, 2 all 256 x 256 tiles, 3 one round + 256 x 128 tail
   int pipe_wide_eff = 115;  // conv_wide cost model: its K-loop rate per FLOP over conv_pipew's, x100
   int dw3_tile = 1;         // YOLO-ACFF depthwise on the LDS-tiled kernel (1) or the vector one (0)
   int resize_stream = 1;    // classifier preprocessing kernel

@@ -207,34 +207,34 @@ def test_tuning_is_per_handle():
     """the knobs a plan reads are per handle.  rtdm_set_tuning sets the process
     defaults a handle copies at creation; rtdm_detector_set_tuning changes one handle only.
     Checked through the kernel each step would launch (step_info names, host-side planning):
-    yolov4-tiny@608 at b64 plans L12 on conv_wide (latency objective: one round of 256 x 256
-    tiles + a 256 x 128 tail), and on conv_pipew with conv_wide off."""
+    yolov4-tiny@608 at b64 plans L12 on conv_pipew by default (conv_wide off), and on conv_wide
+    (latency objective: one round of 256 x 256 tiles + a 256 x 128 tail) with conv_wide 1."""
     from rtdm import _lib as L
     lib = L.lib()
     h1, _, _ = _plan("yolov4-tiny-aider-416", 608)
     h2, _, _ = _plan("yolov4-tiny-aider-416", 608)
     try:
         n1 = _step_names(h1)
-        assert "conv_wide_f16<640>+tail" in n1 and "conv_wide_f16<640>" in n1, n1
-        L.check(lib.rtdm_detector_set_tuning(h2, b"conv_wide", 0))
+        assert not any(n.startswith("conv_wide") for n in n1) and "conv_pipew_f16<640,256>" in n1, n1
+        L.check(lib.rtdm_detector_set_tuning(h2, b"conv_wide", 1))
         n2 = _step_names(h2)
-        assert not any(n.startswith("conv_wide") for n in n2) and "conv_pipew_f16<640,256>" in n2, n2
+        assert "conv_wide_f16<640>+tail" in n2 and "conv_wide_f16<640>" in n2, n2
         assert _step_names(h1) == n1  # the other handle is unchanged
         L.check(lib.rtdm_detector_set_tuning(h2, b"conv_wide", 2))  # all wide, no tail
         n3 = _step_names(h2)
         assert "conv_wide_f16<640>" in n3 and "conv_wide_f16<640>+tail" not in n3, n3
         assert lib.rtdm_detector_set_tuning(h2, b"no_such_key", 1) != 0
         # process defaults: a handle created after rtdm_set_tuning copies them; older ones keep theirs
-        L.check(lib.rtdm_set_tuning(b"conv_wide", 0))
+        L.check(lib.rtdm_set_tuning(b"conv_wide", 1))
         try:
             h3, _, _ = _plan("yolov4-tiny-aider-416", 608)
             try:
-                assert not any(n.startswith("conv_wide") for n in _step_names(h3))
+                assert any(n.startswith("conv_wide") for n in _step_names(h3))
             finally:
                 lib.rtdm_detector_destroy(h3)
             assert _step_names(h1) == n1
         finally:
-            L.check(lib.rtdm_set_tuning(b"conv_wide", 1))
+            L.check(lib.rtdm_set_tuning(b"conv_wide", 0))
     finally:
         lib.rtdm_detector_destroy(h1)
         lib.rtdm_detector_destroy(h2)

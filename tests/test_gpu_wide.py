@@ -44,7 +44,7 @@ def test_wide_tiles_bit_identical(case):
             outs[v] = m(x)[0].cpu()
             names[v] = _names(m, b)
     finally:
-        L.check(L.lib().rtdm_set_tuning(b"conv_wide", 1))
+        L.check(L.lib().rtdm_set_tuning(b"conv_wide", 0))
     assert not any(n.startswith("conv_wide") for n in names[0]), names[0]
     assert any(n.startswith("conv_wide") for n in names[2]), names[2]
     if cfg.startswith("yolov3-aider"):
@@ -69,7 +69,7 @@ def test_wide_plan_at_bench_batch():
             if v == 1:
                 names = _names(m, 64)
     finally:
-        L.check(L.lib().rtdm_set_tuning(b"conv_wide", 1))
+        L.check(L.lib().rtdm_set_tuning(b"conv_wide", 0))
     print("b64 plan:", [n for n in names if "conv" in n])
     assert sum(n.startswith("conv_wide") for n in names) >= 2, names
     assert torch.equal(outs[0], outs[1])

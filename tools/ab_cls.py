@@ -35,13 +35,13 @@ m.half()
 frames = torch.from_numpy(synth_frames(args.batch, 608, 608)).cuda()
 outs, times = {}, {v: [] for v in vals}
 for v in vals:
-    L.check(L.lib().rtdm_set_tuning(args.key.encode(), v))
+    m.set_tuning(args.key, v)  # the handle's own knob (tuning is copied per handle)
     for _ in range(3):
         p = m.classify_frames(frames) if hasattr(m, "classify_frames") else None
     torch.cuda.synchronize()
 for r in range(args.rounds):
     for v in vals:
-        L.check(L.lib().rtdm_set_tuning(args.key.encode(), v))
+        m.set_tuning(args.key, v)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(args.iters):
