@@ -56,6 +56,7 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "acff_persist") t.acff_persist = v < 0 ? 0 : v;
   else if (k == "acff_chain") t.acff_chain = v;
   else if (k == "stem_abl") t.stem_abl = v;
+  else if (k == "stem_fuse") t.stem_fuse = v < 0 ? 0 : v;
   else if (k == "nms_variant") t.nms_variant = v;
   else if (k == "resize_stream") t.resize_stream = v;
   else throw Error{RTDM_E_INVALID, "set_tuning: unknown key " + k};

@@ -182,7 +182,8 @@ __device__ __forceinline__ void xcd_span(int bid, int nb, int ntiles, int& first
 // (the calling thread's scope, else the defaults).
 struct Tuning {
   int conv_pipe = 1;        // conv_pipe mode (1 the kernels; 0 off; > 1 diagnostics, conv_pipe.hip)
-  int stem_abl = 0;         // conv_stem3 ablations (diagnostics)
+  int stem_abl = 0;         // conv_stem3 / conv_stem_pool2 ablations (diagnostics)
+  int stem_fuse = 0;        // pooled stem + the next 16 -> 32 pooled conv as one conv_stem_pool2 launch (1; off: measured slower, r04e)
   int head1x1 = 1;          // stand-alone YOLO head convs on head1x1_f16
   int pipe_bm = 0;          // conv_pipe tile rows: 0 cost model, else forced 256 / 128 / 64
   int pipe_cost = 0;        // conv_pipe / conv_wide tile objective: 0 latency (rounds), 1 throughput (CU-time)
@@ -265,6 +266,9 @@ const char* head1x1_name(const ConvArgs& a);
 int conv_pipe_mode();
 int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 / 128 / 64)
 const char* conv_pipe_name(const ConvArgs& a);  // kernel symbol of that launch
+// stem_fused.hip: pooled stem (Cin 3 -> 16) + the 16 -> 32 3x3 pooled conv reading its map, one launch
+bool stem_pool2_ok(const ConvArgs& a0, const ConvArgs& a2);
+void launch_stem_pool2(const ConvArgs& a0, const ConvArgs& a2, int abl, hipStream_t s);
 // conv_wide.hip: 256 x 256-tile window-mode twin of conv_pipew for the big 3x3 / s1 layers
 bool conv_wide_ok(const ConvArgs& a, int abl);
 int64_t conv_wide_tiles(const ConvArgs& a);

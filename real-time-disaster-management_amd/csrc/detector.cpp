@@ -113,6 +113,9 @@ struct Step {
   int full_t = -1, pool_t = -1, up_t = -1, res_t = -1;
   int yolo = -1;  // index into yolo heads
   bool quad = false;
+  // fused stem pair (stem_fused.hip): this pooled stem's pooled map is read by the next step
+  // only, so both run as one conv_stem_pool2 launch when its shapes fit (stem_pool2_ok)
+  bool fuse2 = false;
   float slope = 0.1f;  // LeakyReLU slope: 0.1 Darknet conv (models.py:40), 0.01 ACFF (:291)
   // [acff] (models.py:46-55, ACFF :265-315): this ST_CONV is the 1x1 fusion over the
   // ST_DW3 map b1+b2+b3 with the fused_conv weights [F][C]; BN is the post-activation
@@ -192,6 +195,7 @@ struct rtdm_detector_s {
   rtdm::DevBuf zero;  // 256 zero bytes: padding source of the glds conv kernel
   rtdm::DevBuf raw_buf;  // raw head rows for rtdm_detect_trt (allocated on first use)
   int last_n = 0;
+  std::vector<int> fused_away;  // tensors the last rtdm_detect call never wrote (fused stem pairs)
   // optional per-step timing: events[call][2*step + {0,1}] recorded around each step
   // on the stream it runs on
   bool timing = false;
@@ -700,6 +704,21 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     RTDM_REQUIRE(wptr == n_floats, RTDM_E_INVALID,
                  "darknet weights: stream has " + std::to_string(n_floats) + " floats, cfg needs " +
                      std::to_string(wptr));
+  // ---- fused stem pairs: a pooled stem whose pooled map (own buffer, not a concat slice)
+  //      only the next step reads ----
+  for (size_t i = 0; i + 1 < h.steps.size(); ++i) {
+    Step& a = h.steps[i];
+    const Step& b = h.steps[i + 1];
+    if (a.kind != ST_CONV || b.kind != ST_CONV || a.in_t >= 0 || a.pool_t < 0 || a.full_t >= 0 || a.up_t >= 0 ||
+        a.yolo >= 0 || a.head || b.in_t != a.pool_t || b.res_t == a.pool_t)
+      continue;
+    bool other = h.tensors[a.pool_t].home >= 0;
+    for (size_t j = 0; j < h.steps.size() && !other; ++j)
+      if (j != i + 1 && (h.steps[j].in_t == a.pool_t || h.steps[j].res_t == a.pool_t)) other = true;
+    for (const Tensor& t : h.tensors)
+      if (t.home == a.pool_t) other = true;
+    a.fuse2 = !other;
+  }
   // ---- own buffers for materialised tensors that are not homed in a concat ----
   size_t off = 0;
   for (Tensor& t : h.tensors) {
@@ -858,6 +877,78 @@ static View tensor_view(const rtdm_detector_s& h, int t) {
   return View{base + x.off * es * h.max_batch, x.c, 0};
 }
 
+// Run-time arguments of a conv step (views of this call's buffers).
+static ConvArgs run_args(rtdm_detector_s& h, const Step& st, const void* x, int in_kind, int n, float* io, int raw) {
+  ConvArgs a;
+  if (st.in_t < 0) {
+    a.in = x;
+    a.in_kind = in_kind;
+  } else {
+    const View v = tensor_view(h, st.in_t);
+    a.in = v.ptr;
+    a.in_cs = v.cs;
+    a.in_co = v.co;
+    a.in_kind = IN_NHWC;
+  }
+  a.n = n;
+  a.ih = st.ih;
+  a.iw = st.iw;
+  a.cin = st.cin;
+  a.ks = st.ks;
+  a.stride = st.stride;
+  a.pad = st.pad;
+  a.oh = st.oh;
+  a.ow = st.ow;
+  a.cout = st.cout;
+  a.quad = st.quad ? 1 : 0;
+  conv_set_rows(a);
+  a.w = h.blob.at<void>(st.pc.w_off);
+  a.kpad = st.pc.kpad;
+  a.cout_pad = st.pc.cout_pad;
+  a.e.bias = h.blob.at<float>(st.pc.b_off);
+  a.e.act = st.act;
+  a.e.slope = st.slope;
+  if (st.pc.s_off != SIZE_MAX) {
+    a.e.scale = h.blob.at<float>(st.pc.s_off);
+    a.e.shift = h.blob.at<float>(st.pc.t_off);
+  }
+  a.e.full = tensor_view(h, st.full_t);
+  a.e.pool = tensor_view(h, st.pool_t);
+  a.e.up = tensor_view(h, st.up_t);
+  a.e.res = tensor_view(h, st.res_t);
+  if (st.head) {
+    const YoloHead& y = h.heads[st.yolo];
+    a.head_w = h.blob.at<void>(st.hpc.w_off);
+    a.head_cout = st.head_cout;
+    a.head_e.bias = h.blob.at<float>(st.hpc.b_off);
+    a.head_e.act = st.head_act;
+    a.head_e.slope = 0.1f;
+    a.head_e.io = io;
+    a.head_e.io_rows = h.n_anchors_total;
+    a.head_e.io_off = y.io_off;
+    a.head_e.na = y.na;
+    a.head_e.no = y.no;
+    a.head_e.ystride = y.ystride;
+    a.head_e.anchor_vec = h.blob.at<float>(y.anchor_off);
+    a.head_e.raw = raw;
+  } else if (st.yolo >= 0) {
+    const YoloHead& y = h.heads[st.yolo];
+    a.e.io = io;
+    a.e.io_rows = h.n_anchors_total;
+    a.e.io_off = y.io_off;
+    a.e.na = y.na;
+    a.e.no = y.no;
+    a.e.ystride = y.ystride;
+    a.e.anchor_vec = h.blob.at<float>(y.anchor_off);
+    a.e.raw = raw;
+  }
+  // the mfma/valu choice was fixed when the weights were packed
+  a.w_f32 = st.pc.mfma ? 0 : 1;
+  a.w_stem = h.blob.at<void>(st.pc.stem_off);
+  a.zero = h.zero.p;
+  return a;
+}
+
 static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, float* io, hipStream_t s,
                          int raw = 0) {
   RTDM_REQUIRE(!h.planning_only, RTDM_E_INVALID, "detect: handle was created without weights");
@@ -887,6 +978,8 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
     RTDM_HIP(hipStreamWaitEvent(h.side, h.fork_ev, 0));
   }
   hipStream_t s0 = s;
+  bool fused_next = false;
+  h.fused_away.clear();
   for (size_t si = 0; si < h.steps.size(); ++si) {
     const Step& st = h.steps[si];
     s = two && st.stream == 1 ? h.side : s0;
@@ -894,75 +987,24 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       for (int d : st.deps)
         if (h.steps[d].stream != st.stream) RTDM_HIP(hipStreamWaitEvent(s, h.step_ev[d], 0));
     if (ev) RTDM_HIP(hipEventRecord(ev[2 * si], s));
-    if (st.kind == ST_CONV) {
-      ConvArgs a;
-      if (st.in_t < 0) {
-        a.in = x;
-        a.in_kind = in_kind;
-      } else {
-        const View v = tensor_view(h, st.in_t);
-        a.in = v.ptr;
-        a.in_cs = v.cs;
-        a.in_co = v.co;
-        a.in_kind = IN_NHWC;
+    if (fused_next) {  // this step ran inside the previous step's launch (conv_stem_pool2)
+      fused_next = false;
+    } else if (st.kind == ST_CONV) {
+      ConvArgs a = run_args(h, st, x, in_kind, n, io, raw);
+      if (st.fuse2 && tune().stem_fuse && st.q < 0 && h.steps[si + 1].q < 0) {
+        const Step& nx = h.steps[si + 1];
+        const ConvArgs b = run_args(h, nx, x, in_kind, n, io, raw);
+        if ((!two || nx.stream == st.stream) && stem_pool2_ok(a, b)) {
+          if (two)
+            for (int d : nx.deps)
+              if (h.steps[d].stream != nx.stream) RTDM_HIP(hipStreamWaitEvent(s, h.step_ev[d], 0));
+          launch_stem_pool2(a, b, stem_abl(), s);
+          fused_next = true;
+          h.fused_away.push_back(st.pool_t);
+        }
       }
-      a.n = n;
-      a.ih = st.ih;
-      a.iw = st.iw;
-      a.cin = st.cin;
-      a.ks = st.ks;
-      a.stride = st.stride;
-      a.pad = st.pad;
-      a.oh = st.oh;
-      a.ow = st.ow;
-      a.cout = st.cout;
-      a.quad = st.quad ? 1 : 0;
-      conv_set_rows(a);
-      a.w = h.blob.at<void>(st.pc.w_off);
-      a.kpad = st.pc.kpad;
-      a.cout_pad = st.pc.cout_pad;
-      a.e.bias = h.blob.at<float>(st.pc.b_off);
-      a.e.act = st.act;
-      a.e.slope = st.slope;
-      if (st.pc.s_off != SIZE_MAX) {
-        a.e.scale = h.blob.at<float>(st.pc.s_off);
-        a.e.shift = h.blob.at<float>(st.pc.t_off);
-      }
-      a.e.full = tensor_view(h, st.full_t);
-      a.e.pool = tensor_view(h, st.pool_t);
-      a.e.up = tensor_view(h, st.up_t);
-      a.e.res = tensor_view(h, st.res_t);
-      if (st.head) {
-        const YoloHead& y = h.heads[st.yolo];
-        a.head_w = h.blob.at<void>(st.hpc.w_off);
-        a.head_cout = st.head_cout;
-        a.head_e.bias = h.blob.at<float>(st.hpc.b_off);
-        a.head_e.act = st.head_act;
-        a.head_e.slope = 0.1f;
-        a.head_e.io = io;
-        a.head_e.io_rows = h.n_anchors_total;
-        a.head_e.io_off = y.io_off;
-        a.head_e.na = y.na;
-        a.head_e.no = y.no;
-        a.head_e.ystride = y.ystride;
-        a.head_e.anchor_vec = h.blob.at<float>(y.anchor_off);
-        a.head_e.raw = raw;
-      } else if (st.yolo >= 0) {
-        const YoloHead& y = h.heads[st.yolo];
-        a.e.io = io;
-        a.e.io_rows = h.n_anchors_total;
-        a.e.io_off = y.io_off;
-        a.e.na = y.na;
-        a.e.no = y.no;
-        a.e.ystride = y.ystride;
-        a.e.anchor_vec = h.blob.at<float>(y.anchor_off);
-        a.e.raw = raw;
-      }
-      // the mfma/valu choice was fixed when the weights were packed
-      a.w_f32 = st.pc.mfma ? 0 : 1;
-      a.w_stem = h.blob.at<void>(st.pc.stem_off);
-      a.zero = h.zero.p;
-      if (st.q >= 0 && h.calibrating) {
+      if (fused_next) {
+      } else if (st.q >= 0 && h.calibrating) {
         launch_chan_absmax(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, h.amax.as<unsigned>() + st.amax_off, s);
         launch_conv(a, h.dtype, s);
       } else if (st.q >= 0) {
@@ -1017,62 +1059,68 @@ static View view_geom(const rtdm_detector_s& h, int t) {
 }
 
 // Kernel symbol, FLOPs and compulsory HBM bytes per image of one step.
+// Geometry-only arguments of a conv step (placeholder pointers) for kernel selection.
+static ConvArgs geom_args(const rtdm_detector_s& h, const Step& st) {
+  ConvArgs a;
+  a.in_kind = st.in_t < 0 ? IN_FRAME_U8 : IN_NHWC;
+  a.cout_pad = st.pc.cout_pad;
+  a.w_f32 = st.pc.mfma ? 0 : 1;
+  a.cin = st.cin;
+  a.ks = st.ks;
+  a.stride = st.stride;
+  a.pad = st.pad;
+  a.ih = st.ih;
+  a.iw = st.iw;
+  a.oh = st.oh;
+  a.ow = st.ow;
+  a.quad = st.quad ? 1 : 0;
+  a.w_stem = st.pc.stem_off != SIZE_MAX ? (const void*)1 : nullptr;
+  a.zero = (const void*)64;
+  a.kpad = st.pc.kpad;
+  a.cout = st.cout;
+  // the kernel instance depends on the batch (conv_pipe tile rows): the last
+  // rtdm_detect call's, max_batch before any
+  a.n = h.last_n > 0 ? h.last_n : h.max_batch;
+  conv_set_rows(a);
+  a.e.bias = (const float*)64;
+  a.e.act = st.act;
+  a.e.slope = st.slope;  // kernel choice depends on it (pool_small_ok)
+  if (st.pc.s_off != SIZE_MAX) {
+    a.e.scale = (const float*)64;
+    a.e.shift = (const float*)64;
+  }
+  if (st.in_t >= 0) {
+    const View iv = view_geom(h, st.in_t);
+    a.in_cs = iv.cs;
+    a.in_co = iv.co;
+  }
+  a.e.full = view_geom(h, st.full_t);
+  a.e.pool = view_geom(h, st.pool_t);
+  a.e.up = view_geom(h, st.up_t);
+  a.e.res = view_geom(h, st.res_t);
+  if (st.head) {
+    a.head_w = (const void*)64;
+    a.head_cout = st.head_cout;
+    a.head_e.io = (float*)64;
+    a.head_e.bias = (const float*)64;
+  } else if (st.yolo >= 0) {
+    a.e.io = (float*)64;
+    a.e.no = h.heads[st.yolo].no;
+  }
+  if (st.pc.mfma) a.w = (const void*)64;
+  if (st.q >= 0) {
+    a.in_cs = st.cin;
+    a.in_co = 0;
+    a.w8 = (const void*)64;
+    a.deq = (const float*)64;
+  }
+  return a;
+}
+
 static void step_info(const rtdm_detector_s& h, const Step& st, std::string& name, double& flop, double& bytes) {
   const double es = (double)esize_of(h.dtype);
   if (st.kind == ST_CONV) {
-    ConvArgs a;
-    a.in_kind = st.in_t < 0 ? IN_FRAME_U8 : IN_NHWC;
-    a.cout_pad = st.pc.cout_pad;
-    a.w_f32 = st.pc.mfma ? 0 : 1;
-    a.cin = st.cin;
-    a.ks = st.ks;
-    a.stride = st.stride;
-    a.pad = st.pad;
-    a.ih = st.ih;
-    a.iw = st.iw;
-    a.oh = st.oh;
-    a.ow = st.ow;
-    a.quad = st.quad ? 1 : 0;
-    a.w_stem = st.pc.stem_off != SIZE_MAX ? (const void*)1 : nullptr;
-    a.zero = (const void*)64;
-    a.kpad = st.pc.kpad;
-    a.cout = st.cout;
-    // the kernel instance depends on the batch (conv_pipe tile rows): the last
-    // rtdm_detect call's, max_batch before any
-    a.n = h.last_n > 0 ? h.last_n : h.max_batch;
-    conv_set_rows(a);
-    a.e.bias = (const float*)64;
-    a.e.act = st.act;
-    a.e.slope = st.slope;  // kernel choice depends on it (pool_small_ok)
-    if (st.pc.s_off != SIZE_MAX) {
-      a.e.scale = (const float*)64;
-      a.e.shift = (const float*)64;
-    }
-    if (st.in_t >= 0) {
-      const View iv = view_geom(h, st.in_t);
-      a.in_cs = iv.cs;
-      a.in_co = iv.co;
-    }
-    a.e.full = view_geom(h, st.full_t);
-    a.e.pool = view_geom(h, st.pool_t);
-    a.e.up = view_geom(h, st.up_t);
-    a.e.res = view_geom(h, st.res_t);
-    if (st.head) {
-      a.head_w = (const void*)64;
-      a.head_cout = st.head_cout;
-      a.head_e.io = (float*)64;
-      a.head_e.bias = (const float*)64;
-    } else if (st.yolo >= 0) {
-      a.e.io = (float*)64;
-      a.e.no = h.heads[st.yolo].no;
-    }
-    if (st.pc.mfma) a.w = (const void*)64;
-    if (st.q >= 0) {
-      a.in_cs = st.cin;
-      a.in_co = 0;
-      a.w8 = (const void*)64;
-      a.deq = (const float*)64;
-    }
+    const ConvArgs a = geom_args(h, st);
     name = st.q >= 0 ? conv_pipe_i8_name(a) : conv_kernel_name(a, h.dtype);
     flop = 2.0 * st.oh * st.ow * (double)st.cout * st.cin * st.ks * st.ks +
            (st.head ? 2.0 * st.oh * st.ow * (double)st.head_cout * st.cout : 0.0);
@@ -1318,6 +1366,30 @@ rtdm_status rtdm_detector_step_info(rtdm_detector h, int step, char* name, int n
     std::string nm;
     double f = 0, b = 0;
     step_info(*h, h->steps[step], nm, f, b);
+    // a fused stem pair (run_detector's conv_stem_pool2 choice, for u8 frame inputs): the first
+    // step reports the launch (both layers' FLOPs; frame in, the second pooled map out), the
+    // second an empty step
+    const auto fused_pair = [&](int i) {
+      if (i < 0 || i + 1 >= (int)h->steps.size()) return false;
+      const Step& a = h->steps[i];
+      const Step& c = h->steps[i + 1];
+      return a.fuse2 && tune().stem_fuse && a.q < 0 && c.q < 0 && (!(h->two_streams && h->side) || c.stream == a.stream) &&
+             stem_pool2_ok(geom_args(*h, a), geom_args(*h, c));
+    };
+    if (fused_pair(step)) {
+      const Step& a = h->steps[step];
+      const Step& c = h->steps[step + 1];
+      std::string n2;
+      double f2 = 0, b2 = 0;
+      step_info(*h, c, n2, f2, b2);
+      nm = "conv_stem_pool2";
+      f += f2;
+      b = (double)a.ih * a.iw * 3.0 + (double)(c.oh / 2) * (c.ow / 2) * c.cout * (double)esize_of(h->dtype);
+    } else if (fused_pair(step - 1)) {
+      nm = "conv_stem_pool2:fused";
+      f = 0;
+      b = 0;
+    }
     if (name && name_len > 0) {
       std::strncpy(name, nm.c_str(), name_len - 1);
       name[name_len - 1] = 0;
@@ -1492,6 +1564,9 @@ rtdm_status rtdm_detector_layer_output(rtdm_detector h, int layer, int n, float*
     if (hgt) *hgt = x.h;
     if (wid) *wid = x.w;
     if (!out) return;
+    RTDM_REQUIRE(std::find(h->fused_away.begin(), h->fused_away.end(), t) == h->fused_away.end(), RTDM_E_UNSUPPORTED,
+                 "layer_output: layer " + std::to_string(layer) +
+                     " output was fused away in the last detect (conv_stem_pool2; rtdm_detector_set_tuning stem_fuse 0 keeps it)");
     RTDM_REQUIRE(n > 0 && n <= h->last_n, RTDM_E_INVALID, "layer_output: n exceeds the last detect batch");
     RTDM_REQUIRE(out_numel >= (int64_t)n * x.c * x.h * x.w, RTDM_E_CAPACITY, "layer_output: out too small");
     launch_to_nchw_f32(tensor_view(*h, t), n, x.h, x.w, x.c, out, h->dtype, (hipStream_t)stream);

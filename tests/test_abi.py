@@ -238,3 +238,26 @@ def test_tuning_is_per_handle():
     finally:
         lib.rtdm_detector_destroy(h1)
         lib.rtdm_detector_destroy(h2)
+
+
+def test_stem_pair_fusion_planned():
+    """yolov4-tiny@608: layers 0-3 (pooled stem + pooled 16 -> 32 conv) plan as one
+    conv_stem_pool2 launch (the second step reports as fused), per handle switchable."""
+    from rtdm import _lib as L
+    lib = L.lib()
+    h, _, _ = _plan("yolov4-tiny-aider-416", 608)
+    try:
+        L.check(lib.rtdm_detector_set_tuning(h, b"stem_fuse", 1))  # opt-in (default off)
+        n = _step_names(h)
+        assert n[0] == "conv_stem_pool2" and n[1] == "conv_stem_pool2:fused", n[:3]
+        L.check(lib.rtdm_detector_set_tuning(h, b"stem_fuse", 0))
+        n0 = _step_names(h)
+        assert n0[0].startswith("conv_stem3<true") and n0[1].startswith("conv3_pool_small<16,32"), n0[:3]
+    finally:
+        lib.rtdm_detector_destroy(h)
+    h, _, _ = _plan("yolov4-tiny-swish", 416)  # swish stem: not the lean epilogue, no fusion
+    try:
+        L.check(lib.rtdm_detector_set_tuning(h, b"stem_fuse", 1))
+        assert "conv_stem_pool2" not in _step_names(h)
+    finally:
+        lib.rtdm_detector_destroy(h)
