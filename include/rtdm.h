@@ -128,7 +128,8 @@ const char* rtdm_build_arch(void);
  * Plan-time keys ("fuse_head", "two_streams") only act at handle creation.
  * key "conv_pipe": 1 = pipelined 256x128 implicit GEMM for Cin%64==0 convs
  * (default), 0 = conv_glds_f16 128x128; key "fuse_head": 1 = conv -> 1x1 head conv
- * -> [yolo] planned as one launch (default), 0 = separate head conv; key
+ * -> [yolo] planned as one launch, 0 = separate head conv (default: the conv then runs
+ * the tap-unrolled window loop and head1x1_f16 the head, measured faster); key
  * "acff_persist": 1 = persistent ACFF kernel for the large classifier maps
  * (default), 0 = 8x8-tile fused ACFF kernel; key "two_streams": 1 = detector head
  * branches on a side stream (default), 0 = one stream.  conv_pipe variants, all

@@ -200,7 +200,7 @@ struct Tuning {
   int nms_variant = 0;      // NMS diagnostics
   int acff_persist = 1;     // acff_persist for the large-map ACFF stages (> 1: ablations)
   int acff_chain = 1;       // acff_chain for the small-map suffix
-  int fuse_head = 1;        // fused YOLO head convs (plan time)
+  int fuse_head = 0;        // fused YOLO head convs (plan time; 0: the 3x3 on the unrolled window kernel + head1x1_f16, measured faster r04h)
   int two_streams = 1;      // detector head branches on a second stream (plan time)
 };
 Tuning& default_tuning();

@@ -21,7 +21,8 @@ namespace {
 constexpr int kHeadCh = 4;  // 32-deep K steps per chunk (128 K)
 }
 
-template <int FM>
+// ONE: Cin == 128, one K chunk (no second register set: FM 4 then fits 2 waves per SIMD)
+template <int FM, bool ONE = false>
 __global__ __launch_bounds__(256) void head1x1_f16(ConvArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int fr = lane & 15, g = lane >> 4;
@@ -48,7 +49,7 @@ __global__ __launch_bounds__(256) void head1x1_f16(ConvArgs a) {
 #pragma unroll
     for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = f4{0.f, 0.f, 0.f, 0.f};
 
-  h8 a0[kHeadCh][FM], b0[kHeadCh][2], a1[kHeadCh][FM], b1[kHeadCh][2];
+  h8 a0[kHeadCh][FM], b0[kHeadCh][2], a1[ONE ? 1 : kHeadCh][FM], b1[ONE ? 1 : kHeadCh][2];
   auto load = [&](int k0, h8(&A)[kHeadCh][FM], h8(&B)[kHeadCh][2]) {
 #pragma unroll
     for (int s = 0; s < kHeadCh; ++s) {
@@ -69,14 +70,21 @@ __global__ __launch_bounds__(256) void head1x1_f16(ConvArgs a) {
   };
   const int K = a.cin, CK = 32 * kHeadCh;
   load(0, a0, b0);
-  int k0 = 0;
-  for (; k0 + 2 * CK <= K; k0 += 2 * CK) {
-    load(k0 + CK, a1, b1);
+  if constexpr (ONE) {
+    (void)a1;
+    (void)b1;
+    __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
     mma(a0, b0);
-    if (k0 + 2 * CK < K) load(k0 + 2 * CK, a0, b0);
-    mma(a1, b1);
+  } else {
+    int k0 = 0;
+    for (; k0 + 2 * CK <= K; k0 += 2 * CK) {
+      load(k0 + CK, a1, b1);
+      mma(a0, b0);
+      if (k0 + 2 * CK < K) load(k0 + 2 * CK, a0, b0);
+      mma(a1, b1);
+    }
+    if (k0 < K) mma(a0, b0);  // odd chunk count: the last chunk was loaded into a0/b0
   }
-  if (k0 < K) mma(a0, b0);  // odd chunk count: the last chunk was loaded into a0/b0
 
   // ---- decode (epi_io_decode's per-element operations) and io stores.  Accumulator
   //      acc[tm][tn][j] = row m_base + 16 tm + 4 g + j, head channel 16 tn + fr. ----
@@ -139,17 +147,26 @@ static int head_fm(const ConvArgs& a) {
       v = 256;
     return v;
   }();
+  // more rows per wave once the grid has them to spare: a wave's loads are all issued before
+  // its first MFMA, so its bytes in flight (16 FM rows x Cin) set the launch's memory-level
+  // parallelism (yolov4-tiny@608 b64 L29, 369664 x 128: FM 2 -> 4)
+  if (a.cin == 128 && (a.M + 255) / 256 >= 4 * cus) return 4;
   return (a.M + 127) / 128 >= 2 * cus ? 2 : 1;  // 2 fragments per wave once the grid is >= 2 per CU
 }
 
-const char* head1x1_name(const ConvArgs& a) { return head_fm(a) == 2 ? "head1x1_f16<2>" : "head1x1_f16<1>"; }
+const char* head1x1_name(const ConvArgs& a) {
+  const int fm = head_fm(a);
+  return fm == 4 ? "head1x1_f16<4>" : fm == 2 ? "head1x1_f16<2>" : "head1x1_f16<1>";
+}
 
 void launch_head1x1(const ConvArgs& a, hipStream_t s) {
   RTDM_REQUIRE(head1x1_ok(a), RTDM_E_INVALID, "head1x1: unsupported layer");
   const int fm = head_fm(a);
   const int64_t blocks = ((int64_t)a.M + 64 * fm - 1) / (64 * fm);
   RTDM_REQUIRE(blocks < (1ll << 31), RTDM_E_CAPACITY, "head1x1: grid too large");
-  if (fm == 2)
+  if (fm == 4)
+    hipLaunchKernelGGL((head1x1_f16<4, true>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  else if (fm == 2)
     hipLaunchKernelGGL((head1x1_f16<2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((head1x1_f16<1>), dim3((unsigned)blocks), dim3(256), 0, s, a);

@@ -392,7 +392,7 @@ def test_detector_fused_head_matches_unfused(dev, cfg, size):
             assert ("head1x1" in m.describe()) == bool(fuse)
             outs[fuse] = io.cpu()
     finally:
-        L.check(L.lib().rtdm_set_tuning(b"fuse_head", 1))
+        L.check(L.lib().rtdm_set_tuning(b"fuse_head", 0))
     assert torch.equal(outs[0], outs[1])
 
 
