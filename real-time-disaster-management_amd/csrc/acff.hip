@@ -799,7 +799,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     const _Float16* src = a.in + (size_t)img * h * h * a.in_cs + a.in_co;
     for (int i = tid; i < h * h * CG; i += kChainThreads) {
       const int px = i / CG, v = i - px * CG;
-      *(uint4*)(buf[0] + (size_t)px * C + v * 8) = *(const uint4*)(src + (size_t)px * a.in_cs + v * 8);
+      *(uint4*)(buf[0] + (size_t)px * (C + 8) + v * 8) = *(const uint4*)(src + (size_t)px * a.in_cs + v * 8);
     }
   }
   int cur = 0;
@@ -904,7 +904,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
           for (int kw = 0; kw < 3; ++kw) {
             const int y = oy + 1 + (kh - 1) * d, x = ox + 1 + (kw - 1) * d;
             h8 xv = h8{0, 0, 0, 0, 0, 0, 0, 0};
-            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)H) xv = *(const h8*)(X + (size_t)(y * H + x) * C + v * 8);
+            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)H) xv = *(const h8*)(X + (size_t)(y * H + x) * (C + 8) + v * 8);
             const f4& w0 = wk[kh * 3 + kw][0];
             const f4& w1 = wk[kh * 3 + kw][1];
 #pragma unroll
@@ -1016,7 +1016,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
           if (m < M) {
             float x = (I8 ? (float)acc[tm][j][r] * dq : (float)acc[tm][j][r]) + bc;
             x = x > 0.f ? x : x * a.slope;
-            Y[(size_t)m * st.cout + c] = (_Float16)fmaf(x, sc, sh);
+            Y[(size_t)m * (st.cout + 8) + c] = (_Float16)fmaf(x, sc, sh);  // pixel stride cout + 8
           }
         }
       }
@@ -1032,12 +1032,17 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
   float* conv = (float*)At;  // [5][hw]
   // conv2 1x1 (c -> 5): one (output, pixel) pair per thread, weights from LDS, four partial
   // sums over the channels (was a wave per pixel with shuffle reductions)
+  // (pixel stride c + 8 halfs: consecutive pixels' lanes read distinct banks; with stride c
+  // every lane of a 16-lane group hit the same four)
   float* w2s = wsm;  // [5][c], the stage taps are dead
+  const int nf = 5 * a.ph * a.pw;
+  float* fcs = wsm + 5 * c;  // [5][nf] fc weights, staged with w2 (the fc read them from global)
   for (int i = tid; i < 5 * c; i += kChainThreads) w2s[i] = a.w2[i];
+  for (int i = tid; i < 5 * nf; i += kChainThreads) fcs[i] = a.fcw[i];
   __syncthreads();
   for (int t = tid; t < 5 * hw; t += kChainThreads) {
     const int o = t / hw, p = t - o * hw;
-    const _Float16* x = X + (size_t)p * c;
+    const _Float16* x = X + (size_t)p * (c + 8);
     const float* w = w2s + o * c;
     float s4[4] = {0.f, 0.f, 0.f, 0.f};
     for (int ch = 0; ch < c; ch += 8) {
@@ -1052,7 +1057,6 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
   }
   __syncthreads();
   float* feat = conv + 5 * hw;  // [5*ph*pw]
-  const int nf = 5 * a.ph * a.pw;
   for (int t = tid; t < nf; t += kChainThreads) {
     const int o = t / (a.ph * a.pw);
     const int r = t - o * a.ph * a.pw;
@@ -1073,7 +1077,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
   float* lg = feat + nf;
   if (tid < 5) {
     float s1 = 0.f;
-    for (int q = 0; q < nf; ++q) s1 = fmaf(feat[q], a.fcw[tid * nf + q], s1);
+    for (int q = 0; q < nf; ++q) s1 = fmaf(feat[q], fcs[tid * nf + q], s1);
     s1 += a.fcb[tid];
     lg[tid] = s1;
     if (a.logits) a.logits[img * 5 + tid] = s1;
@@ -1095,8 +1099,8 @@ size_t acff_chain_lds(const AcffChainPlan& p) {
   int cmax = 0;
   for (int i = 0; i < p.nst; ++i) {
     const int h = p.h[i], oh = h - 2;
-    act = std::max(act, (size_t)h * h * p.cin[i] * 2);
-    act = std::max(act, (size_t)oh * oh * p.cout[i] * 2);
+    act = std::max(act, (size_t)h * h * (p.cin[i] + 8) * 2);  // pixel stride C + 8 (banks)
+    act = std::max(act, (size_t)oh * oh * (p.cout[i] + 8) * 2);
     ab = std::max(ab, (size_t)oh * oh * (p.cin[i] + 8) * 2);
     cmax = std::max(cmax, p.cin[i]);
   }
@@ -1123,7 +1127,7 @@ bool acff_chain_ok(const AcffChainPlan& p) {
   int cmax = 0;
   for (int i = 0; i < p.nst; ++i) cmax = std::max(cmax, p.cin[i]);
   const int clast = p.cout[p.nst - 1];
-  if (cmax > 128 || clast % 8 != 0 || 5 * clast > 30 * cmax) return false;  // register prefetch, tail in wsm
+  if (cmax > 128 || clast % 8 != 0 || 5 * clast + 5 * 5 * 16 > 30 * cmax) return false;  // register prefetch; tail conv2 + fc weights in wsm
   return acff_chain_lds(p) <= 160 * 1024;
 }
 
@@ -1171,8 +1175,8 @@ void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in
   size_t act = 0, ab = 0;
   for (int i = 0; i < p.nst; ++i) {
     const int h = p.h[i], oh = h - 2;
-    act = std::max(act, (size_t)h * h * p.cin[i] * 2);
-    act = std::max(act, (size_t)oh * oh * p.cout[i] * 2);
+    act = std::max(act, (size_t)h * h * (p.cin[i] + 8) * 2);  // pixel stride C + 8 (banks)
+    act = std::max(act, (size_t)oh * oh * (p.cout[i] + 8) * 2);
     ab = std::max(ab, (size_t)oh * oh * (p.cin[i] + 8) * 2);
   }
   const int ohl = p.h[p.nst - 1] - 2;

@@ -102,16 +102,19 @@ __global__ __launch_bounds__(256) void head1x1_f16(ConvArgs a) {
     sh[tn] = (e.scale && cv[tn]) ? e.shift[c] : 0.f;
     anc[tn] = (cv[tn] && !e.raw && (kk[tn] == 2 || kk[tn] == 3)) ? e.anchor_vec[2 * ai[tn] + (kk[tn] - 2)] : 0.f;
   }
-  const size_t plane = (size_t)a.oh * a.ow;
+  // decoded values -> the wave's LDS tile T[c][px] (px stride 16 FM + 1: a store's 16 channel
+  // lanes hit distinct banks), then each anchor plane's 16 FM pixels x no values leave as one
+  // contiguous run of io (consecutive lanes, consecutive dwords) instead of 4-byte scatters
+  constexpr int PX = 16 * FM, PXS = PX + 1;
+  __shared__ float hs_tile[4][32 * PXS];
+  float* T = hs_tile[wid];
 #pragma unroll
   for (int tm = 0; tm < FM; ++tm)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int m = m_base + tm * 16 + 4 * g + j;
-      if (m >= a.M) continue;
+      const int px = tm * 16 + 4 * g + j;
       int n, oy, ox;
-      row_to_pix(a, m, n, oy, ox);
-      const size_t pix_io = (size_t)n * e.io_rows + e.io_off + (size_t)oy * a.ow + ox;
+      row_to_pix(a, min(m_base + px, a.M - 1), n, oy, ox);
 #pragma unroll
       for (int tn = 0; tn < 2; ++tn) {
         if (!cv[tn]) continue;
@@ -128,9 +131,33 @@ __global__ __launch_bounds__(256) void head1x1_f16(ConvArgs a) {
           o = (__expf(x) * anc[tn]) * e.ystride;
         else
           o = __frcp_rn(1.f + __expf(-x));
-        e.io[(pix_io + (size_t)ai[tn] * plane) * e.no + k] = o;
+        T[(tn * 16 + fr) * PXS + px] = o;
       }
     }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const int rows = min(PX, a.M - m_base), no = e.no, na = a.cout / no;
+  const size_t plane = (size_t)a.oh * a.ow;
+  int n0, oy0, ox0;
+  row_to_pix(a, m_base, n0, oy0, ox0);
+  const int p0 = oy0 * a.ow + ox0;
+  const bool one_image = p0 + rows <= (int)plane;  // the wave's rows are consecutive pixels of one image
+  const int ne = rows * no;
+  for (int ai = 0; ai < na; ++ai) {
+    const float* Ta = T + ai * no * PXS;
+    float* dst = e.io + ((size_t)n0 * e.io_rows + e.io_off + (size_t)ai * plane + p0) * no;
+    for (int el = lane; el < ne; el += 64) {
+      const int px = el / no, k = el - px * no;
+      const float v = Ta[k * PXS + px];
+      if (one_image) {
+        dst[el] = v;
+      } else {
+        int n, oy, ox;
+        row_to_pix(a, m_base + px, n, oy, ox);
+        e.io[((size_t)n * e.io_rows + e.io_off + (size_t)ai * plane + (size_t)oy * a.ow + ox) * no + k] = v;
+      }
+    }
+  }
 }
 
 bool head1x1_ok(const ConvArgs& a) {

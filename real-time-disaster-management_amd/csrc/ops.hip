@@ -1057,12 +1057,14 @@ __global__ __launch_bounds__(256) void resize_staged_kernel(const uint8_t* __res
 constexpr int kRsBand = 16;   // output rows per block (= kResizeBand: ResizePlan::band_rows)
 constexpr int kRsTaps = 7;    // max taps per pass (ksize) held unrolled
 constexpr int kRsDepth = 6;   // input rows in flight (buffer->LDS) per wave
-constexpr int kRsRing = 8;    // LDS ring slots (>= kRsDepth + 2), power of two
+constexpr int kRsDepth2 = 4;  // rows in flight with rows taken in pairs (RP 2)
+constexpr int kRsRing = 8;    // LDS ring slots (>= kRsDepth + 2, >= kRsDepth2 + 4), power of two
 constexpr int kRsRowB = 2048; // ring slot bytes: 128 16-byte chunks (2 issuing waves)
 
 // ABL (diagnostic builds only, outputs wrong when non-zero): 1 = no H-pass LDS reads,
 // 2 = no V pass / output stores (one store per thread), 4 = no row DMA.
-template <typename T, int ABL>
+// RP: input rows per wait + barrier (1 or 2)
+template <typename T, int ABL, int RP = 2>
 __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __restrict__ frames, int in_h, int in_w,
                                                             int row_first, int out, int kh_size, int kv_size,
                                                             int col_first, int c0b, int v16, int band_rows,
@@ -1127,39 +1129,63 @@ __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __res
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_t)(ring + slot * rstride + wid * 1024), 16, vo, 0, 0, 0);
     }
   };
-#pragma unroll
-  for (int q = 0; q < kRsDepth; ++q) issue(r0 + q, q);
-  int slot = 0, islot = kRsDepth;
-  for (int r = r0; r < r1; ++r) {
-    issue(r + kRsDepth, islot);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRsDepth) : "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
+  // the H pass of one landed row (ring slot sl) into himg row r - r0
+  auto hpass = [&](int r, int sl) {
     int s0 = 1 << (kPrecisionBits - 1), s1 = s0, s2 = s0;
     if constexpr ((ABL & 1) != 0) {
       himg[(r - r0) * 256 + xx] = (uint32_t)(r + xx);
     } else {
-    // the 21 tap bytes from 7 aligned dword reads, realigned with v_alignbyte (a
-    // byte-granular or misaligned wide LDS read costs far more than this)
-    const uint32_t* dw = (const uint32_t*)(ring + slot * rstride + (xoff & ~3));
-    const int sh = xoff & 3;
-    uint32_t d[7], wv[6];
+      // the 21 tap bytes from 7 aligned dword reads, realigned with v_alignbyte (a
+      // byte-granular or misaligned wide LDS read costs far more than this)
+      const uint32_t* dw = (const uint32_t*)(ring + sl * rstride + (xoff & ~3));
+      const int sh = xoff & 3;
+      uint32_t d[7], wv[6];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) d[k] = dw[k];
+      for (int k = 0; k < 7; ++k) d[k] = dw[k];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) wv[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+      for (int k = 0; k < 6; ++k) wv[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
 #pragma unroll
-    for (int t = 0; t < kRsTaps; ++t) {
-      // bytes x non-negative 22-bit weights: 24-bit multiplies (full rate)
-      const int b0 = 3 * t, b1 = 3 * t + 1, b2 = 3 * t + 2;
-      s0 += (int)__umul24((wv[b0 >> 2] >> (8 * (b0 & 3))) & 255u, kx[t]);
-      s1 += (int)__umul24((wv[b1 >> 2] >> (8 * (b1 & 3))) & 255u, kx[t]);
-      s2 += (int)__umul24((wv[b2 >> 2] >> (8 * (b2 & 3))) & 255u, kx[t]);
+      for (int t = 0; t < kRsTaps; ++t) {
+        // bytes x non-negative 22-bit weights: 24-bit multiplies (full rate)
+        const int b0 = 3 * t, b1 = 3 * t + 1, b2 = 3 * t + 2;
+        s0 += (int)__umul24((wv[b0 >> 2] >> (8 * (b0 & 3))) & 255u, kx[t]);
+        s1 += (int)__umul24((wv[b1 >> 2] >> (8 * (b1 & 3))) & 255u, kx[t]);
+        s2 += (int)__umul24((wv[b2 >> 2] >> (8 * (b2 & 3))) & 255u, kx[t]);
+      }
+      himg[(r - r0) * 256 + xx] = (uint32_t)clip8(s0) | ((uint32_t)clip8(s1) << 8) | ((uint32_t)clip8(s2) << 16);
     }
-    himg[(r - r0) * 256 + xx] = (uint32_t)clip8(s0) | ((uint32_t)clip8(s1) << 8) | ((uint32_t)clip8(s2) << 16);
+  };
+  if constexpr (RP == 2) {
+    // rows in pairs: one wait + barrier per two rows, two independent H-pass chains per thread.
+    // kRsDepth2 rows in flight; row r + D (+1) goes to the slot read for row r + D - 8 (- 7) <=
+    // r - 3, finished before the previous pair's barrier
+#pragma unroll
+    for (int q = 0; q < kRsDepth2; ++q) issue(r0 + q, q);
+    int slot = 0, islot = kRsDepth2;
+    for (int r = r0; r < r1; r += 2) {
+      issue(r + kRsDepth2, islot);
+      issue(r + kRsDepth2 + 1, (islot + 1) & (kRsRing - 1));
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRsDepth2) : "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      hpass(r, slot);
+      if (r + 1 < r1) hpass(r + 1, (slot + 1) & (kRsRing - 1));  // (row r1 - r0 is the zero row)
+      slot = (slot + 2) & (kRsRing - 1);
+      islot = (islot + 2) & (kRsRing - 1);
     }
-    slot = (slot + 1) & (kRsRing - 1);
-    islot = (islot + 1) & (kRsRing - 1);
+  } else {
+#pragma unroll
+    for (int q = 0; q < kRsDepth; ++q) issue(r0 + q, q);
+    int slot = 0, islot = kRsDepth;
+    for (int r = r0; r < r1; ++r) {
+      issue(r + kRsDepth, islot);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRsDepth) : "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      hpass(r, slot);
+      slot = (slot + 1) & (kRsRing - 1);
+      islot = (islot + 1) & (kRsRing - 1);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1227,8 +1253,10 @@ void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_
     const int blocks = n * ((p.out + kRsBand - 1) / kRsBand);
     const int m = resize_stream_mode();
     if (m > 1 && !(out_layout == 1 || dtype == RTDM_F32)) {  // diagnostic ablations (tools/ab_cls.py)
+      // 2..5 ablations; 6: one row per wait + barrier (the pre-r04 loop, A/B)
       auto k = m == 2 ? resize_stream_kernel<_Float16, 1> : m == 3 ? resize_stream_kernel<_Float16, 2>
-             : m == 4 ? resize_stream_kernel<_Float16, 4> : resize_stream_kernel<_Float16, 7>;
+             : m == 4 ? resize_stream_kernel<_Float16, 4> : m == 6 ? resize_stream_kernel<_Float16, 0, 1>
+                                                                  : resize_stream_kernel<_Float16, 7>;
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, s, frames, p.in_h, p.in_w, p.row_first, p.out, p.ksize_h,
                          p.ksize_v, p.col_first, c0b, v16, p.band_rows, p.bounds_h.as<int>(), p.coef_h.as<int>(),
                          p.bounds_v.as<int>(), p.coef_v.as<int>(), (_Float16*)out, 0);
