@@ -279,7 +279,10 @@ typedef const __attribute__((address_space(4))) float* cfloat_p;
 
 template <int CC>
 struct AcffPGeom {
-  static constexpr int TH = 8, TW = 16, HH = TH + 6, HW = TW + 6, NPIX = TH * TW;
+  // HW: staged halo columns, 2 past the 22 the taps read: with a row pitch of 24 pixels the
+  // quad-ordered depthwise reads of a 16-lane group fall in 16 distinct 4-bank slots (at 22,
+  // 2-way conflicts: 25 % of the kernel's LDS cycles, PMC r04c)
+  static constexpr int TH = 8, TW = 16, HH = TH + 6, HW = TW + 8, NPIX = TH * TW;
   static constexpr int PS = CC + 8;                    // halo pixel stride (halfs)
   static constexpr int CG = CC / 8;                    // 8-channel groups per chunk
   static constexpr int KC = (3 * CC + 31) / 32 * 32;   // K per chunk (zero-padded)

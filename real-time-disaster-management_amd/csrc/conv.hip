@@ -1067,7 +1067,10 @@ __global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
 // --------------------------------------------------------------------------
 template <int CIN, int COUT, int TH, int WROWS, int WCH>
 __global__ __launch_bounds__(256, CIN == 16 || WCH == 1 ? 3 : 2) void conv3_pool_small(ConvArgs a) {  // 3 blocks per CU (<= 168 registers): CIN 16, and CIN 32 with one 16-channel tile per wave (WCH 1: half the weight registers; with WCH 2 it would spill)
-  constexpr int TW = 16, HW = TW + 2, PS = CIN + 8;
+  // PS: halo pixel stride (halfs).  Cin 32: 48, so the B-fragment reads of a 16-lane group
+  // (16 pixels x 2 channel groups) fall in 16 distinct 4-bank slots (at 40: 2-way conflicts,
+  // half the kernel's LDS cycles, PMC r04f)
+  constexpr int TW = 16, HW = TW + 2, PS = CIN == 32 ? 48 : CIN + 8;
   constexpr int CG = CIN / 8;                // 8-channel groups per tap
   constexpr int NQ = 9 * CG;                 // 8-channel groups in K
   constexpr int NKS = (NQ + 3) / 4;          // 32-deep k-steps
