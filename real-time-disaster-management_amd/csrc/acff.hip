@@ -781,6 +781,7 @@ struct AcffChainArgs {
   float* logits;
   float* probs;
   int abl;  // diagnostics (wrong outputs): 1 no depthwise, 2 no 1x1 MFMA, 4 no tail
+  unsigned long long* stamps;  // diagnostics (acff_chain mode 16): block 0's s_memtime at each phase
 };
 
 template <int MODE>  // 0 fp16, 1 int8 1x1 fusion, 2 fp16 + calibration
@@ -790,6 +791,12 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int img = blockIdx.x;
+  int nst_ = 0;
+  auto stamp = [&]() {
+    if (a.stamps && img == 0 && tid == 0) a.stamps[nst_] = __builtin_amdgcn_s_memtime();
+    ++nst_;
+  };
+  stamp();
   _Float16* buf[2] = {(_Float16*)chain_lds, (_Float16*)(chain_lds + a.act_bytes)};
   _Float16* At = (_Float16*)(chain_lds + 2 * a.act_bytes);
   int8_t* const At8 = (int8_t*)At;  // int8 A chunk [M][C + 16] bytes (inside the fp16 one)
@@ -854,6 +861,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
       }
     }
     __syncthreads();  // input map + dw weights ready; the previous stage's A reads are done
+    stamp();
     const _Float16* X = buf[cur];
     _Float16* Y = buf[cur ^ 1];
     const int wn = st.cout_pad >> 5, wm = 8 / wn;  // wave grid: wm (M) x wn (N), 32 channels per wave
@@ -961,6 +969,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
         }
       }
       __syncthreads();
+      stamp();
       // this branch's K slice: k = br*C + [0, C)
       auto kstep8 = [&](int ks, const i32x4& b0, const i32x4& b1) {
 #pragma unroll
@@ -1003,6 +1012,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
       }
       if (br == 2 && si + 1 < a.nst) wstore(a.st[si + 1], wpre);  // this stage's taps are no longer read
       __syncthreads();  // the A chunk is rewritten by the next branch
+      stamp();
     }
     // epilogue: bias -> LeakyReLU -> BN affine -> fp16 map Y [M][cout]
 #pragma unroll
@@ -1027,6 +1037,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     cur ^= 1;
   }
   __syncthreads();
+  stamp();
   if (a.abl & 4) return;
   // ---- tail on the last map: [hw][c], c = last cout ----
   const int h = a.nst > 0 ? a.st[a.nst - 1].h - 2 : a.st[0].h, hw = h * h;
@@ -1043,6 +1054,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
   for (int i = tid; i < 5 * c; i += kChainThreads) w2s[i] = a.w2[i];
   for (int i = tid; i < 5 * nf; i += kChainThreads) fcs[i] = a.fcw[i];
   __syncthreads();
+  stamp();
   for (int t = tid; t < 5 * hw; t += kChainThreads) {
     const int o = t / hw, p = t - o * hw;
     const _Float16* x = X + (size_t)p * (c + 8);
@@ -1059,6 +1071,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     conv[o * hw + p] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   }
   __syncthreads();
+  stamp();
   float* feat = conv + 5 * hw;  // [5*ph*pw]
   for (int t = tid; t < nf; t += kChainThreads) {
     const int o = t / (a.ph * a.pw);
@@ -1077,6 +1090,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     feat[t] = sum / 25.f;
   }
   __syncthreads();
+  stamp();
   float* lg = feat + nf;
   if (tid < 5) {
     float s1 = 0.f;
@@ -1086,6 +1100,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     if (a.logits) a.logits[img * 5 + tid] = s1;
   }
   __syncthreads();
+  stamp();
   if (tid < 5 && a.probs) {
     float mx = lg[0];
     for (int k = 1; k < 5; ++k) mx = fmaxf(mx, lg[k]);
@@ -1093,6 +1108,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     for (int k = 0; k < 5; ++k) sum += expf(lg[k] - mx);
     a.probs[img * 5 + tid] = expf(lg[tid] - mx) / sum;
   }
+  stamp();
 }
 
 int acff_chain_mode() { return tune().acff_chain; }
@@ -1148,7 +1164,10 @@ void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in
   a.in_cs = in_cs;
   a.in_co = in_co;
   a.nst = acff_chain_mode() == 2 ? 0 : p.nst;  // 2: tail only (diagnostics; stages skipped -> wrong)
-  a.abl = acff_chain_mode() >= 8 ? (acff_chain_mode() - 8) & 7 : 0;  // 8 + bits: ablations (diagnostics)
+  a.abl = acff_chain_mode() >= 8 && acff_chain_mode() < 16 ? (acff_chain_mode() - 8) & 7 : 0;  // 8 + bits: ablations
+  static unsigned long long* stamps_dev = nullptr;  // mode 16: phase timestamps of block 0 (diagnostics)
+  if (acff_chain_mode() == 16 && !stamps_dev) RTDM_HIP(hipMalloc(&stamps_dev, 64 * sizeof(unsigned long long)));
+  a.stamps = acff_chain_mode() == 16 ? stamps_dev : nullptr;
   for (int i = 0; i < p.nst; ++i) {
     AcffChainStage& t = a.st[i];
     t.dw_wt = dw_wt[i];
@@ -1202,6 +1221,14 @@ void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in
   else
     hipLaunchKernelGGL(acff_chain<0>, dim3(n), dim3(kChainThreads), lds, s, a);
   RTDM_HIP(hipGetLastError());
+  if (a.stamps) {  // diagnostics: print block 0's phase durations (synchronises the stream)
+    unsigned long long h[64] = {};
+    RTDM_HIP(hipMemcpyAsync(h, a.stamps, sizeof h, hipMemcpyDeviceToHost, s));
+    RTDM_HIP(hipStreamSynchronize(s));
+    fprintf(stderr, "acff_chain phases (s_memtime ticks, n=%d):", n);
+    for (int i = 1; i < 64 && h[i] >= h[i - 1] && h[i]; ++i) fprintf(stderr, " %llu", h[i] - h[i - 1]);
+    fprintf(stderr, "\n");
+  }
 }
 
 }  // namespace rtdm
