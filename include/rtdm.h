@@ -146,7 +146,9 @@ const char* rtdm_build_arch(void);
  * tile walk in N-groups of g panels (default 2, 0 = M-major); "conv_wide" 0 = off
  * (default: the 256x256-tile kernel measured slower) | 1 = where the
  * cost model picks it | 2 always | 3 one round of wide tiles + a 256x128 tail;
- * "conv_wide_eff" its cost-model rate (x100).  Unknown keys: RTDM_E_INVALID. */
+ * "conv_wide_eff" its cost-model rate (x100); "stem_fuse" 1 = a pooled Cin-3 stem and the
+ * 16 -> 32 pooled 3x3 conv reading its map as one conv_stem_pool2 launch (bit-identical;
+ * default 0: measured slower).  Unknown keys: RTDM_E_INVALID. */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 /* The same keys on one handle's own copy (see above). */
 rtdm_status rtdm_detector_set_tuning(rtdm_detector h, const char* key, int value);
