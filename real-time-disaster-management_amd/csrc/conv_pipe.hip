@@ -1285,7 +1285,7 @@ static int wide_plan(const ConvArgs& a, bool* split) {
   const int64_t U = conv_wide_tiles(a);
   const int cus = pipe_cus();
   const bool can_split = a.cout_pad % 256 == 0 && U > cus;  // tail tile t = 2 x its wide unit
-  if (tune().pipe_wide == 2) return (int)U;
+  if (tune().pipe_wide == 2 || tune().pipe_wide >= 10) return (int)U;  // (>= 10: all wide, diagnostic ablations)
   if (tune().pipe_wide == 3) {
     *split = can_split;
     return can_split ? (int)(U / cus) * cus : (int)U;

@@ -61,7 +61,8 @@ __device__ __forceinline__ void wunroll(F&& f, std::integer_sequence<int, I...>)
 }  // namespace
 
 // One 256 x 256 output tile.  RES: the fused shortcut add (ABL 896).
-template <bool RES>
+// DG (diagnostics, wrong outputs): 1 no in-loop weight loads, 2 no in-loop window loads
+template <bool RES, int DG = 0>
 __device__ __forceinline__ void wide_tile(const ConvArgs& a, unsigned char* smem, int tile) {
   constexpr int FM = 4, FN = 8;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -248,8 +249,8 @@ __device__ __forceinline__ void wide_tile(const ConvArgs& a, unsigned char* smem
         mfma_a(acc[tm][tn], fb[tn], fa1[tm]);
       fb[tn] = rd(bh0 + tn * 2048);
       if constexpr (STG) {
-        if (tn < 4) stage_b1(cb2, T2, (cb + T) & 1, z, tn);
-        if (WOP && tn == 4) stage_w(T, cb + 1, z);
+        if (!(DG & 1) && tn < 4) stage_b1(cb2, T2, (cb + T) & 1, z, tn);
+        if (!(DG & 2) && WOP && tn == 4) stage_w(T, cb + 1, z);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -283,7 +284,7 @@ __device__ __forceinline__ void wide_tile(const ConvArgs& a, unsigned char* smem
   pipe_epi_regs<RES, FM, FN, 64, 128>(a, mb, n_base, wm, wn, lane, acc, rb, dq4);
 }
 
-template <int ABL>
+template <int ABL, int DG = 0>
 __global__ __launch_bounds__(512, 1) void conv_wide_f16(ConvArgs a, int ntiles) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[kWSmem];
   if (threadIdx.x < 64) reinterpret_cast<u32x4*>(smem + kWOffZ)[threadIdx.x] = u32x4{0u, 0u, 0u, 0u};
@@ -295,7 +296,7 @@ __global__ __launch_bounds__(512, 1) void conv_wide_f16(ConvArgs a, int ntiles) 
   const int bx = (nb - xcd + 7) >> 3;
   for (int t = lo + l; t < hi; t += bx) {
     __syncthreads();  // the previous tile's LDS reads are done (and, first, the zero area is written)
-    wide_tile<(ABL & 256) != 0>(a, smem, t);
+    wide_tile<(ABL & 256) != 0, DG>(a, smem, t);
   }
 }
 
@@ -319,8 +320,15 @@ void launch_conv_wide(const ConvArgs& a, int abl, int ntiles, int cus, hipStream
   RTDM_REQUIRE(conv_wide_ok(a, abl), RTDM_E_INVALID, "conv_wide: unsupported layer");
   RTDM_REQUIRE(ntiles > 0 && ntiles <= conv_wide_tiles(a), RTDM_E_INVALID, "conv_wide: bad tile count");
   const dim3 grid((unsigned)(ntiles < cus ? ntiles : cus));
+  const int dg = tune().pipe_wide >= 10 ? tune().pipe_wide - 10 : 0;  // conv_wide 11 / 12 / 13: ablations
   if (abl == 896)
     hipLaunchKernelGGL((conv_wide_f16<896>), grid, dim3(512), 0, s, a, ntiles);
+  else if (dg == 1)
+    hipLaunchKernelGGL((conv_wide_f16<640, 1>), grid, dim3(512), 0, s, a, ntiles);
+  else if (dg == 2)
+    hipLaunchKernelGGL((conv_wide_f16<640, 2>), grid, dim3(512), 0, s, a, ntiles);
+  else if (dg == 3)
+    hipLaunchKernelGGL((conv_wide_f16<640, 3>), grid, dim3(512), 0, s, a, ntiles);
   else
     hipLaunchKernelGGL((conv_wide_f16<640>), grid, dim3(512), 0, s, a, ntiles);
   RTDM_HIP(hipGetLastError());
