@@ -157,6 +157,8 @@ __global__ __launch_bounds__(256) void acff_fused(AcffArgs a) {
         }
       h8 o;
 #pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(acc[j]));  // (f32 sums round on their own)
+#pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (_Float16)acc[j];
       *(h8*)(At + m * LS + br * a.cin + c0 + v * 8) = o;
     }
@@ -939,6 +941,10 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
           *(uint2*)(At8 + (size_t)m * AS8 + v * 8) = make_uint2(lo, hi);
         } else {
           h8 o;
+          // (opaque: the f32 sums round to fp16 on their own, as in the per-stage kernels,
+          // instead of folding the last tap's FMA into an fp16-result mix op)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(t[j]));
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] = (_Float16)t[j];
           *(h8*)(At + (size_t)m * AS + v * 8) = o;

@@ -202,6 +202,7 @@ struct Tuning {
   int acff_chain = 1;       // acff_chain for the small-map suffix
   int fuse_head = 0;        // fused YOLO head convs (plan time; 0: the 3x3 on the unrolled window kernel + head1x1_f16, measured faster r04h)
   int two_streams = 1;      // detector head branches on a second stream (plan time)
+  int conv_c32 = 1;         // conv3_c32 for the Cin-32 3x3 convs (conv_c32.hip)
 };
 Tuning& default_tuning();
 const Tuning& tune();
@@ -269,6 +270,10 @@ const char* conv_pipe_name(const ConvArgs& a);  // kernel symbol of that launch
 // stem_fused.hip: pooled stem (Cin 3 -> 16) + the 16 -> 32 3x3 pooled conv reading its map, one launch
 bool stem_pool2_ok(const ConvArgs& a0, const ConvArgs& a2);
 void launch_stem_pool2(const ConvArgs& a0, const ConvArgs& a2, int abl, hipStream_t s);
+// conv_c32.hip: persistent Cin-32 3x3 kernel (stride 1 / 2, Cout 64, optional residual)
+bool c32_ok(const ConvArgs& a);
+void launch_c32(const ConvArgs& a, hipStream_t s);
+const char* c32_name(const ConvArgs& a);
 // conv_wide.hip: 256 x 256-tile window-mode twin of conv_pipew for the big 3x3 / s1 layers
 bool conv_wide_ok(const ConvArgs& a, int abl);
 int64_t conv_wide_tiles(const ConvArgs& a);

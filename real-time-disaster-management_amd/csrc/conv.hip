@@ -1346,6 +1346,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
   }
   if (dtype == RTDM_F16 && pool_small_ok(a))
     return a.cin == 16 ? "conv3_pool_small<16,32,16,4,2>" : "conv3_pool_small<32,64,8,8,1>";
+  if (dtype == RTDM_F16 && c32_ok(a)) return c32_name(a);
   if (dtype == RTDM_F16 && direct_ok(a)) {
     const int bn = direct_cfg(a.cout_pad).bn;
     return bn == 128 ? "conv3_direct<4,2>" : bn == 64 ? "conv3_direct<4,4>" : "conv3_direct<2,4>";
@@ -1393,6 +1394,8 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     }
   } else if (dtype == RTDM_F16 && pool_small_ok(a)) {
     launch_pool_small(a, s);
+  } else if (dtype == RTDM_F16 && c32_ok(a)) {
+    launch_c32(a, s);
   } else if (dtype == RTDM_F16 && direct_ok(a)) {
     launch_direct(a, s);
   } else if (dtype == RTDM_F16 && tune().head1x1 && head1x1_ok(a)) {

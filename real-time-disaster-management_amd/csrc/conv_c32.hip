@@ -1,0 +1,210 @@
+// Cin-32 3x3 convolutions (Darknet-53's stride-2 conv 32 -> 64 and the first residual
+// block's 3x3 32 -> 64 + shortcut, yolov3 / yolov3-spp L1 and L3): a persistent MFMA kernel
+// with the layer's weights resident in LDS and the input tile's halo staged once per tile.
+//
+// Replaces: nn.Conv2d(32, 64, 3, stride s, pad 1) + folded BatchNorm + LeakyReLU 0.1 of
+// victim_localization/yolov3/models.py:23-44 as run by Darknet.forward (:345-347), with the
+// shortcut add (:349-354) fused.
+//
+// These layers move ~6 bytes of HBM per MAC-row and do little arithmetic (K = 288): the
+// generic implicit-GEMM tiles (conv_mfma: 128 x 64, K-blocks of 64 gathered per tap through
+// registers) and the direct kernel (16 x 16 tiles, one Cin chunk, 8-byte NHWC stores) ran
+// them at 0.11 / 0.14 ms per b16 416 frame batch, 2-3x their HBM time.  Here:
+//   * a workgroup (4 waves) loads the 64 x 288 weights into LDS once and walks output tiles
+//     (TH x 16 pixels, grid-stride), so the weights are not re-read per tile;
+//   * per tile the (TH-1)S+3 x 15S+3 halo (32 channels = 4 x 16 B per pixel) is staged
+//     through registers: the next tile's halo loads are issued before this tile's MFMAs;
+//   * K step = one tap's 32 channels = one v_mfma_f32_16x16x32_f16 k-depth: A = 16 weight
+//     rows from LDS, B = 16 pixels of a tile row read at the tap's offset in the halo;
+//   * the weight rows are stored so that MFMA row i of N-fragment n is output channel
+//     (i/4)*16 + 4n + i%4: a lane's 4 fragments then hold 16 consecutive channels of one
+//     pixel (channels 16g .. 16g+15), stored as two 16-byte vectors (4 lanes = one 128-byte
+//     pixel line) after bias -> LeakyReLU -> (+ residual), epi_vec8_lean's operations.
+// LDS pitches (pixel 48 / 40 halfs for stride 1 / 2, weight row 304 halfs, weight rows in
+// fragment order) put the 16 lanes of each ds_read_b128 group on distinct bank slots.
+// K order per output: taps 0..8, each tap's 32 channels inside one MFMA, as conv_mfma's
+// K-blocks (k = tap*32 + c) and conv3_direct's k-steps.
+#include "conv_epi.h"
+
+#include <algorithm>
+
+namespace rtdm {
+
+constexpr int kC32TW = 16;  // tile columns (one fragment of pixels)
+constexpr int kC32WP = 304;  // weight row pitch (halfs)
+
+template <int S>
+struct C32Geom {
+  static constexpr int TH = S == 1 ? 16 : 8;  // tile rows (4 waves x RW rows)
+  static constexpr int RW = TH / 4;
+  static constexpr int HR = (TH - 1) * S + 3, HW = (kC32TW - 1) * S + 3;
+  static constexpr int PP = S == 1 ? 48 : 40;
+  static constexpr int HALO = HR * HW * PP;        // halfs
+  static constexpr int NVEC = HR * HW * 4;         // 16-byte vectors per halo
+  static constexpr int NV = (NVEC + 255) / 256;    // per thread
+  static constexpr size_t LDS = (size_t)(HALO + 64 * kC32WP) * 2;
+};
+
+template <int S, bool RES>
+__global__ __launch_bounds__(256) void conv3_c32(ConvArgs a, int ntiles) {
+  using G = C32Geom<S>;
+  extern __shared__ __attribute__((aligned(16))) _Float16 c32_lds[];
+  _Float16* const hs = c32_lds;
+  _Float16* const ws = c32_lds + G::HALO;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int tx_n = (a.ow + kC32TW - 1) / kC32TW, ty_n = (a.oh + G::TH - 1) / G::TH;
+  const _Float16* __restrict__ in = (const _Float16*)a.in + a.in_co;
+
+  auto tile_of = [&](int t, int& n, int& ty, int& tx) {
+    tx = t % tx_n;
+    const int t2 = t / tx_n;
+    ty = t2 % ty_n;
+    n = t2 / ty_n;
+  };
+  auto hload = [&](int t, u32x4 (&r)[G::NV]) {
+    int n, ty, tx;
+    tile_of(t, n, ty, tx);
+    const int iy0 = ty * G::TH * S - 1, ix0 = tx * kC32TW * S - 1;
+#pragma unroll
+    for (int k = 0; k < G::NV; ++k) {
+      const int v = tid + k * 256;
+      const int pix = v >> 2, c = v & 3;
+      const int hr = pix / G::HW, col = pix - hr * G::HW;
+      const int y = iy0 + hr, x = ix0 + col;
+      const bool ok = v < G::NVEC && (unsigned)y < (unsigned)a.ih && (unsigned)x < (unsigned)a.iw;
+      r[k] = u32x4{0u, 0u, 0u, 0u};
+      if (ok) r[k] = *(const u32x4*)(in + ((size_t)(n * a.ih + y) * a.iw + x) * a.in_cs + c * 8);
+    }
+  };
+  auto hstore = [&](const u32x4 (&r)[G::NV]) {
+#pragma unroll
+    for (int k = 0; k < G::NV; ++k) {
+      const int v = tid + k * 256;
+      if (v < G::NVEC) *(u32x4*)(hs + (v >> 2) * G::PP + (v & 3) * 8) = r[k];
+    }
+  };
+
+  int t = blockIdx.x;
+  u32x4 pre[G::NV];
+  if (t < ntiles) hload(t, pre);
+  // weights -> LDS, row q = 16n + i holds output channel (i/4)*16 + 4n + i%4 (k = tap*32 + c)
+  for (int v = tid; v < 64 * 36; v += 256) {
+    const int q = v / 36, kv = v - q * 36;
+    const int n = q >> 4, i = q & 15;
+    const int co = (i >> 2) * 16 + 4 * n + (i & 3);
+    *(u32x4*)(ws + q * kC32WP + kv * 8) = *(const u32x4*)((const _Float16*)a.w + (size_t)co * a.kpad + kv * 8);
+  }
+  // this lane's 16 channels: bias
+  const Epilogue& e = a.e;
+  const int c0 = 16 * g;
+  const bool cval = c0 < a.cout;  // cout % 16 == 0 (c32_ok)
+  float bias[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) bias[q] = cval && e.bias ? e.bias[c0 + q] : 0.f;
+  const bool leaky = e.act == ACT_LEAKY;
+
+  for (; t < ntiles; t += gridDim.x) {
+    hstore(pre);
+    __syncthreads();  // halo (and, first time round, the weights) visible
+    if (t + (int)gridDim.x < ntiles) hload(t + gridDim.x, pre);  // lands under this tile's MFMAs
+    f4 acc[G::RW][4];
+#pragma unroll
+    for (int f = 0; f < G::RW; ++f)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[f][n] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kh = tap / 3, kw = tap % 3;
+      h8 wf[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) wf[n] = *(const h8*)(ws + (n * 16 + j) * kC32WP + tap * 32 + g * 8);
+#pragma unroll
+      for (int f = 0; f < G::RW; ++f) {
+        const h8 xf = *(const h8*)(hs + (((wid * G::RW + f) * S + kh) * G::HW + j * S + kw) * G::PP + g * 8);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[f][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[n], xf, acc[f][n], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave is done with the halo before the next tile's store
+    int n, ty, tx;
+    tile_of(t, n, ty, tx);
+    const int ox = tx * kC32TW + j;
+#pragma unroll
+    for (int f = 0; f < G::RW; ++f) {
+      const int oy = ty * G::TH + wid * G::RW + f;
+      if (!cval || oy >= a.oh || ox >= a.ow) continue;
+      const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
+      h8v rv[2];
+      if constexpr (RES) {
+        const _Float16* rp = (const _Float16*)e.res.ptr + pix * e.res.cs + e.res.co + c0;
+        rv[0] = *(const h8v*)rp;
+        rv[1] = *(const h8v*)(rp + 8);
+      }
+      h8v hv[2];
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = 4 * nn + r;  // channel c0 + q
+          float x = acc[f][nn][r] + bias[q];
+          x = leaky ? (x > 0.f ? x : x * e.slope) : x;
+          // (opaque: x * slope rounds to fp32 before the fp16 conversion, as in the other
+          // epilogues, instead of folding into one single-rounding fp16-result mix op)
+          asm volatile("" : "+v"(x));
+          x = x * 1.f + 0.f;  // epi_vec8_lean's (absent) BN affine: -0 -> +0 as there
+          if constexpr (RES) x += (float)rv[q >> 3][q & 7];
+          hv[q >> 3][q & 7] = (_Float16)x;
+        }
+      _Float16* op = (_Float16*)e.full.ptr + pix * e.full.cs + e.full.co + c0;
+      *(h8v*)op = hv[0];
+      *(h8v*)(op + 8) = hv[1];
+    }
+  }
+}
+
+static bool view8(const View& v) { return ((v.cs | v.co) & 7) == 0; }
+
+bool c32_ok(const ConvArgs& a) {
+  if (!tune().conv_c32 || a.in_kind != IN_NHWC || a.w_f32 || a.cin != 32 || a.ks != 3 || a.pad != 1) return false;
+  if ((a.stride != 1 && a.stride != 2) || a.quad || a.cout_pad != 64 || a.cout % 16 || a.kpad < 288) return false;
+  if ((a.in_cs | a.in_co) & 7 || a.in_cs < a.in_co + 32) return false;
+  if (a.oh != (a.ih + 2 - 3) / a.stride + 1 || a.ow != (a.iw + 2 - 3) / a.stride + 1) return false;
+  const Epilogue& e = a.e;
+  if (!e.full.ptr || e.pool.ptr || e.up.ptr || e.io || e.scale || e.act == ACT_SWISH) return false;
+  if (!view8(e.full) || (e.res.ptr && !view8(e.res))) return false;
+  return (int64_t)a.n * a.ih * a.iw * a.in_cs < (1ll << 31) && (int64_t)a.n * a.oh * a.ow * e.full.cs < (1ll << 31);
+}
+
+static int c32_tiles(const ConvArgs& a) {
+  const int th = a.stride == 1 ? C32Geom<1>::TH : C32Geom<2>::TH;
+  return a.n * ((a.oh + th - 1) / th) * ((a.ow + kC32TW - 1) / kC32TW);
+}
+
+const char* c32_name(const ConvArgs& a) {
+  static const char* names[2][2] = {{"conv3_c32<1,false>", "conv3_c32<1,true>"}, {"conv3_c32<2,false>", "conv3_c32<2,true>"}};
+  return names[a.stride == 2][a.e.res.ptr != nullptr];
+}
+
+template <int S, bool RES>
+static void launch_c32_t(const ConvArgs& a, int ntiles, hipStream_t s) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  // workgroups per CU the LDS allows (160 KB per CU)
+  const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / C32Geom<S>::LDS);
+  const int grid = std::min(ntiles, cus * per_cu);
+  hipLaunchKernelGGL((conv3_c32<S, RES>), dim3(grid), dim3(256), C32Geom<S>::LDS, s, a, ntiles);
+}
+
+void launch_c32(const ConvArgs& a, hipStream_t s) {
+  const int nt = c32_tiles(a);
+  if (nt <= 0) return;
+  const bool res = a.e.res.ptr != nullptr;
+  if (a.stride == 1)
+    res ? launch_c32_t<1, true>(a, nt, s) : launch_c32_t<1, false>(a, nt, s);
+  else
+    res ? launch_c32_t<2, true>(a, nt, s) : launch_c32_t<2, false>(a, nt, s);
+}
+
+}  // namespace rtdm

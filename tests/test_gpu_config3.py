@@ -21,11 +21,11 @@ pytestmark = pytest.mark.gpu
 CFG, IMG, B = "yolov3-aider-416", 416, 16
 
 
-def _model(half=True):
+def _model(half=True, img=IMG):
     from rtdm.darknet import Darknet
     from rtdm.synth import load_calibration, synth_darknet_weights
     text = cfg_text(CFG)
-    m = Darknet(text, (IMG, IMG))
+    m = Darknet(text, (img, img))
     m.load_weight_stream(synth_darknet_weights(text, calib=load_calibration(CFG, "cond"), preset="cond"))
     if half:
         m.half()
