@@ -149,7 +149,9 @@ const char* rtdm_build_arch(void);
  * "conv_wide_eff" its cost-model rate (x100); "stem_fuse" 1 = a pooled Cin-3 stem and the
  * 16 -> 32 pooled 3x3 conv reading its map as one conv_stem_pool2 launch (bit-identical;
  * default 0: measured slower); "conv_c32" 1 = the Cin-32 3x3 convs on
- * conv3_c32 (default; bit-identical to 0 = conv_mfma / conv3_direct).
+ * conv3_c32 (default; bit-identical to 0 = conv_mfma / conv3_direct); "pipe_regpool" 1 =
+ * conv_pipe's register epilogue also for the pool / upsample layers (bit-identical;
+ * default 0: measured slower, profiles/r04r_regpool_ab.txt).
  * Unknown keys: RTDM_E_INVALID. */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 /* The same keys on one handle's own copy (see above). */

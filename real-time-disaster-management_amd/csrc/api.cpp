@@ -54,6 +54,7 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "fuse_head") t.fuse_head = v ? 1 : 0;
   else if (k == "two_streams") t.two_streams = v ? 1 : 0;
   else if (k == "conv_c32") t.conv_c32 = v ? 1 : 0;
+  else if (k == "pipe_regpool") t.pipe_regpool = v ? 1 : 0;
   else if (k == "acff_persist") t.acff_persist = v < 0 ? 0 : v;
   else if (k == "acff_chain") t.acff_chain = v;
   else if (k == "stem_abl") t.stem_abl = v;

@@ -1212,7 +1212,9 @@ static int g_pipe_korder_get() { return tune().pipe_korder; }
 static int pipe_abl(const ConvArgs& a) {
   if (a.head_w) return 8;
   if (epi_io_ok(a)) return 1024;
-  const int reg = !a.e.pool.ptr && !a.e.up.ptr ? 512 : 0;
+  // (pool / upsample layers: the LDS C tile unless rtdm_set_tuning("pipe_regpool", 1) — the
+  // register epilogue pools the quad-ordered rows across lane quads by DPP)
+  const int reg = (!a.e.pool.ptr && !a.e.up.ptr) || tune().pipe_regpool ? 512 : 0;
   if (epi_lean_ok(a)) return 128 | reg;
   if (epi_lean_ok(a, true)) return 384 | reg;
   return 0;
