@@ -151,7 +151,9 @@ const char* rtdm_build_arch(void);
  * default 0: measured slower); "conv_c32" 1 = the Cin-32 3x3 convs on
  * conv3_c32 (default; bit-identical to 0 = conv_mfma / conv3_direct); "pipe_regpool" 1 =
  * conv_pipe's register epilogue also for the pool / upsample layers (bit-identical;
- * default 0: measured slower, profiles/r04r_regpool_ab.txt).
+ * default 0: measured slower, profiles/r04r_regpool_ab.txt); "pool_small_pf" 0 = halo
+ * tiles in flight per conv3_pool_small block by Cin (default: 2 for Cin 16, 1 for Cin 32)
+ * | 1 | 2 (bit-identical).
  * Unknown keys: RTDM_E_INVALID. */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 /* The same keys on one handle's own copy (see above). */

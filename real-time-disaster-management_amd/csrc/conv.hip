@@ -1065,8 +1065,8 @@ __global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
 // groups x (COUT / 16 / WCH) channel groups = 4.  LDS: the 18 x 18 input halo,
 // pixel stride CIN + 8 halfs (16 consecutive pixels hit distinct banks).
 // --------------------------------------------------------------------------
-template <int CIN, int COUT, int TH, int WROWS, int WCH>
-__global__ __launch_bounds__(256, CIN == 16 || WCH == 1 ? 3 : 2) void conv3_pool_small(ConvArgs a) {  // 3 blocks per CU (<= 168 registers): CIN 16, and CIN 32 with one 16-channel tile per wave (WCH 1: half the weight registers; with WCH 2 it would spill)
+template <int CIN, int COUT, int TH, int WROWS, int WCH, int PF = 1>
+__global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF > 1) ? 3 : 2) void conv3_pool_small(ConvArgs a) {  // 3 blocks per CU (<= 168 registers): CIN 16, and CIN 32 with one 16-channel tile per wave (WCH 1: half the weight registers; with WCH 2 it would spill)
   // PS: halo pixel stride (halfs).  Cin 32: 48, so the B-fragment reads of a 16-lane group
   // (16 pixels x 2 channel groups) fall in 16 distinct 4-bank slots (at 40: 2-way conflicts,
   // half the kernel's LDS cycles, PMC r04f)
@@ -1125,8 +1125,10 @@ __global__ __launch_bounds__(256, CIN == 16 || WCH == 1 ? 3 : 2) void conv3_pool
     soff[k] = pix * PS + v * 8;
   }
   const int img = a.ih * a.iw * a.in_cs;  // halfs per image (< 2^31: planner limits)
-  u32x4 pre[PV];
-  auto prefetch = [&](int tile) {
+  // PF halo register sets: tiles t + tstep .. t + PF*tstep in flight while tile t computes
+  // (PF 2: twice the bytes in flight per CU; these layers are HBM-latency bound)
+  u32x4 pre[PV], pre2[PF > 1 ? PV : 1];
+  auto prefetch_to = [&](int tile, u32x4 (&dst)[PV]) {
     const int tx = tile % tiles_x, t1 = tile / tiles_x;
     const int ty = t1 % tiles_y, n = t1 / tiles_y;
     const _Float16* base = in + (size_t)n * img;
@@ -1137,7 +1139,7 @@ __global__ __launch_bounds__(256, CIN == 16 || WCH == 1 ? 3 : 2) void conv3_pool
       u32x4 d = {0u, 0u, 0u, 0u};
       if ((unsigned)y < (unsigned)a.ih && (unsigned)x < (unsigned)a.iw)
         d = *(const u32x4*)(base + (y * a.iw + x) * a.in_cs + hoff[k]);
-      pre[k] = d;
+      dst[k] = d;
     }
   };
   const Epilogue& e = a.e;
@@ -1147,58 +1149,122 @@ __global__ __launch_bounds__(256, CIN == 16 || WCH == 1 ? 3 : 2) void conv3_pool
   int buf = 0;
   int tile, tend, tstep;  // XCD-contiguous tile walk (horizontal neighbours share the halo columns)
   xcd_span(blockIdx.x, gridDim.x, ntiles, tile, tend, tstep);
-  if (tile < tend) prefetch(tile);
-  for (; tile < tend; tile += tstep) {
-    _Float16* xb_w = xs + buf * XS;
+  if constexpr (PF == 1) {
+    if (tile < tend) prefetch_to(tile, pre);
+    for (; tile < tend; tile += tstep) {
+      _Float16* xb_w = xs + buf * XS;
 #pragma unroll
-    for (int k = 0; k < PV; ++k)
-      if (tid + 256 * k < HALO) *(u32x4*)(xb_w + soff[k]) = pre[k];
-    __syncthreads();
-    const int tx = tile % tiles_x, t1 = tile / tiles_x;
-    const int ty = t1 % tiles_y, n = t1 / tiles_y;
-    if (tile + tstep < tend) prefetch(tile + tstep);  // in flight during the MFMAs
-    const _Float16* xb = xb_w + (wr * WROWS * HW + p) * PS;
-    f4 acc[WROWS][WCH];
+      for (int k = 0; k < PV; ++k)
+        if (tid + 256 * k < HALO) *(u32x4*)(xb_w + soff[k]) = pre[k];
+      __syncthreads();
+      const int tx = tile % tiles_x, t1 = tile / tiles_x;
+      const int ty = t1 % tiles_y, n = t1 / tiles_y;
+      if (tile + tstep < tend) prefetch_to(tile + tstep, pre);  // in flight during the MFMAs
+      const _Float16* xb = xb_w + (wr * WROWS * HW + p) * PS;
+      f4 acc[WROWS][WCH];
 #pragma unroll
-    for (int j = 0; j < WROWS; ++j)
+      for (int j = 0; j < WROWS; ++j)
 #pragma unroll
-      for (int t = 0; t < WCH; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < WCH; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-      const _Float16* bp = xb + kofs[s];
+      for (int s = 0; s < NKS; ++s) {
+        const _Float16* bp = xb + kofs[s];
 #pragma unroll
-      for (int j = 0; j < WROWS; ++j) {
-        const h8 b = *(const h8*)(bp + j * HW * PS);
+        for (int j = 0; j < WROWS; ++j) {
+          const h8 b = *(const h8*)(bp + j * HW * PS);
 #pragma unroll
-        for (int t = 0; t < WCH; ++t)
-          acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][t], b, acc[j][t], 0, 0, 0);
-      }
-    }
-    // pooled epilogue: lane = pixel column ox0 + p, rows j; channels co0 + 16t + 4g + r.
-    // One pooled-row pointer per tile; rows j step by qw pixels.
-    const int px = (tx * TW + p) >> 1;
-    const int py0 = (ty * TH + wr * WROWS) >> 1;
-    _Float16* const prow = (_Float16*)e.pool.ptr + e.pool.co + co0 + 4 * g +
-                           ((size_t)(n * qh + py0) * qw + px) * e.pool.cs;
-    const bool lane_st = (p & 1) == 0 && px < qw;
-#pragma unroll
-    for (int j = 0; j < WROWS; j += 2) {
-      const bool st = lane_st && py0 + j / 2 < qh;
-#pragma unroll
-      for (int t = 0; t < WCH; ++t) {
-        float m[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float t2 = fmaxf(acc[j][t][r], acc[j + 1][t][r]);
-          const float x = fmaxf(t2, dpp_xor1(t2)) + bias[t][r];
-          m[r] = fmaxf(x, x * slope);
+          for (int t = 0; t < WCH; ++t)
+            acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][t], b, acc[j][t], 0, 0, 0);
         }
-        if (st)
-          *(uint2*)(prow + (size_t)(j / 2) * qw * e.pool.cs + 16 * t) =
-              make_uint2(pack_h2(m[0], m[1]), pack_h2(m[2], m[3]));
       }
+      // pooled epilogue: lane = pixel column ox0 + p, rows j; channels co0 + 16t + 4g + r.
+      // One pooled-row pointer per tile; rows j step by qw pixels.
+      const int px = (tx * TW + p) >> 1;
+      const int py0 = (ty * TH + wr * WROWS) >> 1;
+      _Float16* const prow = (_Float16*)e.pool.ptr + e.pool.co + co0 + 4 * g +
+                            ((size_t)(n * qh + py0) * qw + px) * e.pool.cs;
+      const bool lane_st = (p & 1) == 0 && px < qw;
+#pragma unroll
+      for (int j = 0; j < WROWS; j += 2) {
+        const bool st = lane_st && py0 + j / 2 < qh;
+#pragma unroll
+        for (int t = 0; t < WCH; ++t) {
+          float m[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float t2 = fmaxf(acc[j][t][r], acc[j + 1][t][r]);
+            const float x = fmaxf(t2, dpp_xor1(t2)) + bias[t][r];
+            m[r] = fmaxf(x, x * slope);
+          }
+          if (st)
+            *(uint2*)(prow + (size_t)(j / 2) * qw * e.pool.cs + 16 * t) =
+                make_uint2(pack_h2(m[0], m[1]), pack_h2(m[2], m[3]));
+        }
+      }
+      buf ^= 1;
     }
-    buf ^= 1;
+  } else {
+    if (tile < tend) prefetch_to(tile, pre);
+    if (tile + tstep < tend) prefetch_to(tile + tstep, pre2);
+    auto body = [&](u32x4 (&cur)[PV]) {
+      _Float16* xb_w = xs + buf * XS;
+#pragma unroll
+      for (int k = 0; k < PV; ++k)
+        if (tid + 256 * k < HALO) *(u32x4*)(xb_w + soff[k]) = cur[k];
+      __syncthreads();
+      const int tx = tile % tiles_x, t1 = tile / tiles_x;
+      const int ty = t1 % tiles_y, n = t1 / tiles_y;
+      if (tile + 2 * tstep < tend) prefetch_to(tile + 2 * tstep, cur);  // two tiles in flight
+      // (the tile's MFMAs + pooled epilogue as in the PF 1 loop, written out: as a shared lambda
+      // the compiler allocated ~27 more VGPRs, 135 -> 162)
+      const _Float16* xb = xb_w + (wr * WROWS * HW + p) * PS;
+      f4 acc[WROWS][WCH];
+#pragma unroll
+      for (int j = 0; j < WROWS; ++j)
+#pragma unroll
+        for (int t = 0; t < WCH; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        const _Float16* bp = xb + kofs[s];
+#pragma unroll
+        for (int j = 0; j < WROWS; ++j) {
+          const h8 b = *(const h8*)(bp + j * HW * PS);
+#pragma unroll
+          for (int t = 0; t < WCH; ++t)
+            acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][t], b, acc[j][t], 0, 0, 0);
+        }
+      }
+      // pooled epilogue: lane = pixel column ox0 + p, rows j; channels co0 + 16t + 4g + r.
+      // One pooled-row pointer per tile; rows j step by qw pixels.
+      const int px = (tx * TW + p) >> 1;
+      const int py0 = (ty * TH + wr * WROWS) >> 1;
+      _Float16* const prow = (_Float16*)e.pool.ptr + e.pool.co + co0 + 4 * g +
+                            ((size_t)(n * qh + py0) * qw + px) * e.pool.cs;
+      const bool lane_st = (p & 1) == 0 && px < qw;
+#pragma unroll
+      for (int j = 0; j < WROWS; j += 2) {
+        const bool st = lane_st && py0 + j / 2 < qh;
+#pragma unroll
+        for (int t = 0; t < WCH; ++t) {
+          float m[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float t2 = fmaxf(acc[j][t][r], acc[j + 1][t][r]);
+            const float x = fmaxf(t2, dpp_xor1(t2)) + bias[t][r];
+            m[r] = fmaxf(x, x * slope);
+          }
+          if (st)
+            *(uint2*)(prow + (size_t)(j / 2) * qw * e.pool.cs + 16 * t) =
+                make_uint2(pack_h2(m[0], m[1]), pack_h2(m[2], m[3]));
+        }
+      }
+      buf ^= 1;
+      tile += tstep;
+    };
+    while (tile < tend) {
+      body(pre);
+      if (tile < tend) body(pre2);
+    }
   }
 }
 
@@ -1237,14 +1303,26 @@ static void launch_pool_small(const ConvArgs& a, hipStream_t s) {
   const int64_t tiles = (int64_t)a.n * ((a.oh + th - 1) / th) * ((a.ow + 15) / 16);
   RTDM_REQUIRE(tiles < (1ll << 31), RTDM_E_CAPACITY, "conv: too many tiles");
   // persistent blocks: exactly the resident count, each streaming tiles with its weights in registers
+  // halo tiles in flight per block: 2 for Cin 16 (b64 L2 0.082 -> 0.077 ms), 1 for Cin 32 (at 2
+  // it needs 210 VGPRs, 2 blocks per CU: 0.056 -> 0.058 ms; profiles/r04s_pool_small_pf.txt);
+  // rtdm_set_tuning("pool_small_pf", 1 | 2) forces one (0 = this choice)
+  const bool pf2 = tune().pool_small_pf ? tune().pool_small_pf >= 2 : a.cin == 16;
   if (a.cin == 16) {
     static const int per_cu = resident_blocks(conv3_pool_small<16, 32, 16, 4, 2>, 256, 0);
-    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cu_count());
-    hipLaunchKernelGGL((conv3_pool_small<16, 32, 16, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    static const int per_cu2 = resident_blocks(conv3_pool_small<16, 32, 16, 4, 2, 2>, 256, 0);
+    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)(pf2 ? per_cu2 : per_cu) * cu_count());
+    if (pf2)
+      hipLaunchKernelGGL((conv3_pool_small<16, 32, 16, 4, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv3_pool_small<16, 32, 16, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   } else {
     static const int per_cu = resident_blocks(conv3_pool_small<32, 64, 8, 8, 1>, 256, 0);
-    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cu_count());
-    hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 8, 1>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    static const int per_cu2 = resident_blocks(conv3_pool_small<32, 64, 8, 8, 1, 2>, 256, 0);
+    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)(pf2 ? per_cu2 : per_cu) * cu_count());
+    if (pf2)
+      hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 8, 1, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 8, 1>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   }
 }
 
