@@ -204,6 +204,7 @@ struct Tuning {
   int two_streams = 1;      // detector head branches on a second stream (plan time)
   int pipe_regpool = 0;     // conv_pipe register epilogue for pool / upsample layers too
   int pool_small_pf = 0;    // conv3_pool_small halo tiles in flight per block (0 auto | 1 | 2)
+  int stem_persist = 0;     // conv_stem3p for the pooled uint8 stem (measured slower r04u)
   int conv_c32 = 1;         // conv3_c32 for the Cin-32 3x3 convs (conv_c32.hip)
 };
 Tuning& default_tuning();

@@ -252,7 +252,7 @@ def test_stem_pair_fusion_planned():
         assert n[0] == "conv_stem_pool2" and n[1] == "conv_stem_pool2:fused", n[:3]
         L.check(lib.rtdm_detector_set_tuning(h, b"stem_fuse", 0))
         n0 = _step_names(h)
-        assert n0[0].startswith("conv_stem3<true") and n0[1].startswith("conv3_pool_small<16,32"), n0[:3]
+        assert n0[0].startswith("conv_stem3") and n0[1].startswith("conv3_pool_small<16,32"), n0[:3]
     finally:
         lib.rtdm_detector_destroy(h)
     h, _, _ = _plan("yolov4-tiny-swish", 416)  # swish stem: not the lean epilogue, no fusion

@@ -51,7 +51,7 @@ def test_stem_pair_fused_bit_identical(case):
     if fused:
         i = names[1].index("conv_stem_pool2")
         assert names[1][i + 1] == "conv_stem_pool2:fused", names[1]
-        assert names[0][i].startswith("conv_stem3<true") and names[0][i + 1].startswith("conv3_pool_small<16,32"), names[0]
+        assert names[0][i].startswith("conv_stem3") and names[0][i + 1].startswith("conv3_pool_small<16,32"), names[0]
     assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
 
 
@@ -76,3 +76,33 @@ def test_stem_pair_fused_layer_output_and_nchw():
     m.layer_output(1, 2)  # unfused this time: the map exists
     d = (ctypes_io - io_u8).abs()  # the float frames round to fp16 in the stem: the fp16 bar
     assert float(d[..., :4].max()) <= 0.5 and float(d[..., 4:].max()) <= 2e-2, float(d.max())
+
+
+
+@pytest.mark.parametrize("knob", [("stem_persist", 0, 1, "conv_stem3p<1>")])
+@pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608:3", "yolov4-tiny-aider-416@416:5",
+                                  "yolov3-tiny-aider-416@416:2", "yolov4-tiny-aider-416@256:7"])
+def test_stem_variants_bit_identical(case, knob):
+    """Pooled uint8 stem variants against conv_stem3<true> with its defaults: conv_stem3p
+    (persistent: the next band's frame bytes in flight while the current band computes;
+    rtdm_set_tuning("stem_persist", 1); measured slower, off by default).  Per tile the same
+    staging, MFMAs and epilogue: BIT-IDENTICAL io."""
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    key, base, alt, name = knob
+    cfg, rest = case.split("@")
+    size, b = (int(v) for v in rest.split(":"))
+    x = torch.from_numpy(synth_frames(b, size, size, seed=79)).cuda()
+    outs, names = {}, {}
+    try:
+        for v in (base, alt):
+            L.check(L.lib().rtdm_set_tuning(key.encode(), v))
+            m, _, _, _ = _detector(cfg, size, preset="cond")
+            outs[v] = m(x)[0].cpu()
+            names[v] = _names(m, b)
+    finally:
+        L.check(L.lib().rtdm_set_tuning(key.encode(), base))
+    assert names[base][0].startswith("conv_stem3<true"), names[base][:2]
+    if name:
+        assert names[alt][0] == name, names[alt][:2]
+    assert torch.equal(outs[base], outs[alt]), float((outs[base] - outs[alt]).abs().max())
