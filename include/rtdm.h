@@ -149,7 +149,10 @@ const char* rtdm_build_arch(void);
  * "conv_wide_eff" its cost-model rate (x100); "stem_fuse" 1 = a pooled Cin-3 stem and the
  * 16 -> 32 pooled 3x3 conv reading its map as one conv_stem_pool2 launch (bit-identical;
  * default 0: measured slower); "conv_c32" 1 = the Cin-32 3x3 convs on
- * conv3_c32 (default; bit-identical to 0 = conv_mfma / conv3_direct); "pipe_regpool" 1 =
+ * conv3_c32 (default; bit-identical to 0 = conv_mfma / conv3_direct); "res_fuse" 1 =
+ * Darknet-53's first residual block (1x1 64 -> 32, 3x3 32 -> 64, shortcut) as one
+ * conv3_c32r launch, 8 waves (default; 2 = 4 waves; 0 = two launches; bit-identical;
+ * the reduce map is then not materialised: layer_output refuses it); "pipe_regpool" 1 =
  * conv_pipe's register epilogue also for the pool / upsample layers (bit-identical;
  * default 0: measured slower, profiles/r04r_regpool_ab.txt); "pool_small_pf" 0 = halo
  * tiles in flight per conv3_pool_small block by Cin (default: 2 for Cin 16, 1 for Cin 32)

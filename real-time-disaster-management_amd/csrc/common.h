@@ -206,6 +206,7 @@ struct Tuning {
   int pool_small_pf = 0;    // conv3_pool_small halo tiles in flight per block (0 auto | 1 | 2)
   int stem_persist = 0;     // conv_stem3p for the pooled uint8 stem (measured slower r04u)
   int conv_c32 = 1;         // conv3_c32 for the Cin-32 3x3 convs (conv_c32.hip)
+  int res_fuse = 1;         // conv3_c32r: Darknet-53's first residual block as one launch (1: 8 waves, 2: 4 waves)
 };
 Tuning& default_tuning();
 const Tuning& tune();
@@ -277,6 +278,9 @@ void launch_stem_pool2(const ConvArgs& a0, const ConvArgs& a2, int abl, hipStrea
 bool c32_ok(const ConvArgs& a);
 void launch_c32(const ConvArgs& a, hipStream_t s);
 const char* c32_name(const ConvArgs& a);
+// ... and Darknet-53's first residual block (1x1 64 -> 32, 3x3 32 -> 64, shortcut) as one launch
+bool c32r_ok(const ConvArgs& a1, const ConvArgs& a);
+void launch_c32r(const ConvArgs& a1, const ConvArgs& a, hipStream_t s);
 // conv_wide.hip: 256 x 256-tile window-mode twin of conv_pipew for the big 3x3 / s1 layers
 bool conv_wide_ok(const ConvArgs& a, int abl);
 int64_t conv_wide_tiles(const ConvArgs& a);

@@ -163,6 +163,183 @@ __global__ __launch_bounds__(256) void conv3_c32(ConvArgs a, int ntiles) {
   }
 }
 
+// conv3_c32r: Darknet-53's first residual block in one launch — the 1x1 reduce (64 -> 32,
+// Darknet.forward models.py:345-347), the 3x3 (32 -> 64) and the shortcut add (:349-354) —
+// for a 16 x 16 output tile per step of a persistent walk:
+//   1. the tile's 18 x 18 halo of the block input X (64 channels, pitch 80 halfs) is staged
+//      from registers (the next tile's halo loads are issued before this tile's MFMAs);
+//   2. the 1x1 runs on every halo pixel inside the image (21 fragments of 16 pixels over the 4
+//      waves, 2 k-steps of 32 channels, conv_mfma's order), bias -> LeakyReLU (rounded to
+//      fp32) -> fp16 into the Y halo (32 channels, pitch 48); pixels outside the image are
+//      zero (the 3x3's padding);
+//   3. the 3x3 is conv3_c32<1>'s loop on the Y halo, and its residual is X at the tile's
+//      pixels, read from the staged halo instead of HBM.
+// The reduce map (Y) never reaches HBM: per output pixel 128 B of X in (with the halo) and
+// 128 B out, against 128 + 64 + 64 + 128 + 128 B for the two launches.  Every value takes
+// the unfused kernels' operations in their order: bit-identical (tests/test_gpu_c32.py).
+constexpr int kC32rPX = 80;                           // X halo pixel pitch (halfs)
+constexpr int kC32rHP = C32Geom<1>::HR * C32Geom<1>::HW;  // 324 halo pixels
+constexpr int kC32rXV = kC32rHP * 8;                  // 16-byte vectors of the X halo
+constexpr size_t kC32rLDS = (size_t)(kC32rHP * kC32rPX + C32Geom<1>::HALO + 64 * kC32WP) * 2;
+
+template <int NW>  // waves per workgroup (4 | 8)
+__global__ __launch_bounds__(64 * NW) void conv3_c32r(ConvArgs a1, ConvArgs a, int ntiles) {
+  using G = C32Geom<1>;
+  constexpr int NT = 64 * NW, RW = G::TH / NW;        // threads; tile rows per wave
+  constexpr int kC32rNV = (kC32rXV + NT - 1) / NT;    // X halo vectors per thread
+  extern __shared__ __attribute__((aligned(16))) _Float16 c32r_lds[];
+  _Float16* const xs = c32r_lds;                      // X halo [324][80]
+  _Float16* const hs = xs + kC32rHP * kC32rPX;        // Y halo [324][48]
+  _Float16* const ws = hs + G::HALO;                  // 3x3 weights
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int tx_n = (a.ow + kC32TW - 1) / kC32TW, ty_n = (a.oh + G::TH - 1) / G::TH;
+  const _Float16* __restrict__ in = (const _Float16*)a1.in + a1.in_co;
+
+  auto tile_of = [&](int t, int& n, int& ty, int& tx) {
+    tx = t % tx_n;
+    const int t2 = t / tx_n;
+    ty = t2 % ty_n;
+    n = t2 / ty_n;
+  };
+  auto hload = [&](int t, u32x4 (&r)[kC32rNV]) {
+    int n, ty, tx;
+    tile_of(t, n, ty, tx);
+    const int iy0 = ty * G::TH - 1, ix0 = tx * kC32TW - 1;
+#pragma unroll
+    for (int k = 0; k < kC32rNV; ++k) {
+      const int v = tid + k * NT;
+      const int pix = v >> 3, c = v & 7;
+      const int hr = pix / G::HW, col = pix - hr * G::HW;
+      const int y = iy0 + hr, x = ix0 + col;
+      const bool ok = v < kC32rXV && (unsigned)y < (unsigned)a1.ih && (unsigned)x < (unsigned)a1.iw;
+      r[k] = u32x4{0u, 0u, 0u, 0u};
+      if (ok) r[k] = *(const u32x4*)(in + ((size_t)(n * a1.ih + y) * a1.iw + x) * a1.in_cs + c * 8);
+    }
+  };
+
+  int t = blockIdx.x;
+  u32x4 pre[kC32rNV];
+  if (t < ntiles) hload(t, pre);
+  // 3x3 weights -> LDS (conv3_c32's fragment-ordered rows)
+  for (int v = tid; v < 64 * 36; v += NT) {
+    const int q = v / 36, kv = v - q * 36;
+    const int n = q >> 4, i = q & 15;
+    const int co = (i >> 2) * 16 + 4 * n + (i & 3);
+    *(u32x4*)(ws + q * kC32WP + kv * 8) = *(const u32x4*)((const _Float16*)a.w + (size_t)co * a.kpad + kv * 8);
+  }
+  // 1x1 weight fragments (A, registers): N-fragment n row i = reduce channel (i/4)*8 + 4n + i%4,
+  // so a lane's two fragments hold reduce channels 8g .. 8g+7 of one pixel
+  h8 w1[2][2];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int co = (j >> 2) * 8 + 4 * n + (j & 3);
+      w1[n][ks] = *(const h8*)((const _Float16*)a1.w + (size_t)co * a1.kpad + ks * 32 + g * 8);
+    }
+  const Epilogue& e1 = a1.e;
+  const Epilogue& e = a.e;
+  float b1[8], bias[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) b1[q] = e1.bias ? e1.bias[8 * g + q] : 0.f;
+  const int c0 = 16 * g;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) bias[q] = e.bias ? e.bias[c0 + q] : 0.f;
+  const bool leaky1 = e1.act == ACT_LEAKY, leaky = e.act == ACT_LEAKY;
+
+  for (; t < ntiles; t += gridDim.x) {
+#pragma unroll
+    for (int k = 0; k < kC32rNV; ++k) {
+      const int v = tid + k * NT;
+      if (v < kC32rXV) *(u32x4*)(xs + (v >> 3) * kC32rPX + (v & 7) * 8) = pre[k];
+    }
+    __syncthreads();  // X halo (and the 3x3 weights) visible; the previous tile's reads done
+    if (t + (int)gridDim.x < ntiles) hload(t + gridDim.x, pre);
+    int n, ty, tx;
+    tile_of(t, n, ty, tx);
+    // ---- 1x1 reduce over the halo pixels -> Y halo ----
+    for (int f = wid; f * 16 < kC32rHP; f += NW) {
+      const int q = f * 16 + j;  // this lane's halo pixel (B column)
+      const int qc = q < kC32rHP ? q : kC32rHP - 1;
+      const h8 xa = *(const h8*)(xs + qc * kC32rPX + g * 8);
+      const h8 xb = *(const h8*)(xs + qc * kC32rPX + 32 + g * 8);
+      f4 acc[2];
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) {
+        acc[nn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[nn][0], xa, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        acc[nn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[nn][1], xb, acc[nn], 0, 0, 0);
+      }
+      const int hr = qc / G::HW, col = qc - hr * G::HW;
+      const int y = ty * G::TH - 1 + hr, x = tx * kC32TW - 1 + col;
+      const bool inside = (unsigned)y < (unsigned)a.ih && (unsigned)x < (unsigned)a.iw;
+      h8v yv;
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = 4 * nn + r;  // reduce channel 8g + qq
+          float v = acc[nn][r] + b1[qq];
+          v = leaky1 ? (v > 0.f ? v : v * e1.slope) : v;
+          asm volatile("" : "+v"(v));  // (x * slope rounds to fp32 first, as in the other epilogues)
+          v = v * 1.f + 0.f;           // epi_vec8_lean's (absent) BN affine
+          yv[qq] = inside ? (_Float16)v : (_Float16)0.f;
+        }
+      if (q < kC32rHP) *(h8v*)(hs + q * G::PP + 8 * g) = yv;
+    }
+    __syncthreads();  // Y halo complete
+    // ---- 3x3 (conv3_c32<1>) on the Y halo ----
+    f4 acc[RW][4];
+#pragma unroll
+    for (int f = 0; f < RW; ++f)
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn) acc[f][nn] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kh = tap / 3, kw = tap % 3;
+      h8 wf[4];
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn) wf[nn] = *(const h8*)(ws + (nn * 16 + j) * kC32WP + tap * 32 + g * 8);
+#pragma unroll
+      for (int f = 0; f < RW; ++f) {
+        const h8 xf = *(const h8*)(hs + (((wid * RW + f) + kh) * G::HW + j + kw) * G::PP + g * 8);
+#pragma unroll
+        for (int nn = 0; nn < 4; ++nn) acc[f][nn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[nn], xf, acc[f][nn], 0, 0, 0);
+      }
+    }
+    const int ox = tx * kC32TW + j;
+#pragma unroll
+    for (int f = 0; f < RW; ++f) {
+      const int row = wid * RW + f;
+      const int oy = ty * G::TH + row;
+      // residual: X at this output pixel = halo pixel (row + 1, j + 1)
+      const _Float16* rp = xs + ((row + 1) * G::HW + j + 1) * kC32rPX + c0;
+      h8v rv[2];
+      rv[0] = *(const h8v*)rp;
+      rv[1] = *(const h8v*)(rp + 8);
+      if (oy >= a.oh || ox >= a.ow) continue;
+      const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
+      h8v hv[2];
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = 4 * nn + r;
+          float x = acc[f][nn][r] + bias[q];
+          x = leaky ? (x > 0.f ? x : x * e.slope) : x;
+          asm volatile("" : "+v"(x));
+          x = x * 1.f + 0.f;
+          x += (float)rv[q >> 3][q & 7];
+          hv[q >> 3][q & 7] = (_Float16)x;
+        }
+      _Float16* op = (_Float16*)e.full.ptr + pix * e.full.cs + e.full.co + c0;
+      *(h8v*)op = hv[0];
+      *(h8v*)(op + 8) = hv[1];
+    }
+    __syncthreads();  // X / Y halo reads done before the next tile's stores
+  }
+}
+
 static bool view8(const View& v) { return ((v.cs | v.co) & 7) == 0; }
 
 bool c32_ok(const ConvArgs& a) {
@@ -179,6 +356,35 @@ bool c32_ok(const ConvArgs& a) {
 static int c32_tiles(const ConvArgs& a) {
   const int th = a.stride == 1 ? C32Geom<1>::TH : C32Geom<2>::TH;
   return a.n * ((a.oh + th - 1) / th) * ((a.ow + kC32TW - 1) / kC32TW);
+}
+
+// The residual pair: a1 = the 1x1 reduce (64 -> 32, reading X), a = the 3x3 (32 -> 64) reading
+// a1's output with the shortcut X as its residual view.
+bool c32r_ok(const ConvArgs& a1, const ConvArgs& a) {
+  if (!c32_ok(a) || a.stride != 1 || !a.e.res.ptr || a.cout != 64) return false;
+  const Epilogue& e1 = a1.e;
+  if (a1.in_kind != IN_NHWC || a1.w_f32 || a1.ks != 1 || a1.stride != 1 || a1.pad != 0 || a1.quad) return false;
+  if (a1.cin != 64 || a1.cout != 32 || a1.cout_pad != 32 || a1.kpad < 64 || (a1.in_cs | a1.in_co) & 7) return false;
+  if (!e1.full.ptr || e1.pool.ptr || e1.up.ptr || e1.io || e1.res.ptr || e1.scale || e1.act == ACT_SWISH) return false;
+  if (a1.ih != a.ih || a1.iw != a.iw || a1.oh != a.ih || a1.ow != a.iw || a1.n != a.n) return false;
+  // a reads a1's output; a's residual is a1's input (same view)
+  if (a.in != e1.full.ptr || a.in_cs != e1.full.cs || a.in_co != e1.full.co) return false;
+  if (a.e.res.ptr != a1.in || a.e.res.cs != a1.in_cs || a.e.res.co != a1.in_co) return false;
+  return (int64_t)a1.n * a1.ih * a1.iw * a1.in_cs < (1ll << 31);
+}
+
+void launch_c32r(const ConvArgs& a1, const ConvArgs& a, hipStream_t s) {
+  const int nt = c32_tiles(a);
+  if (nt <= 0) return;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / kC32rLDS);
+  const dim3 grid(std::min(nt, cus * per_cu));
+  if (tune().res_fuse == 2)
+    hipLaunchKernelGGL(conv3_c32r<4>, grid, dim3(256), kC32rLDS, s, a1, a, nt);
+  else
+    hipLaunchKernelGGL(conv3_c32r<8>, grid, dim3(512), kC32rLDS, s, a1, a, nt);
 }
 
 const char* c32_name(const ConvArgs& a) {

@@ -116,6 +116,10 @@ struct Step {
   // fused stem pair (stem_fused.hip): this pooled stem's pooled map is read by the next step
   // only, so both run as one conv_stem_pool2 launch when its shapes fit (stem_pool2_ok)
   bool fuse2 = false;
+  // Darknet-53's first residual block: this 1x1 reduce (64 -> 32), whose map only the next
+  // step (3x3 32 -> 64 with this step's input as its shortcut) reads, runs with it as one
+  // conv3_c32r launch when the shapes fit (c32r_ok)
+  bool fuse_r = false;
   float slope = 0.1f;  // LeakyReLU slope: 0.1 Darknet conv (models.py:40), 0.01 ACFF (:291)
   // [acff] (models.py:46-55, ACFF :265-315): this ST_CONV is the 1x1 fusion over the
   // ST_DW3 map b1+b2+b3 with the fused_conv weights [F][C]; BN is the post-activation
@@ -719,6 +723,22 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
       if (t.home == a.pool_t) other = true;
     a.fuse2 = !other;
   }
+  // ---- fused residual pairs (conv3_c32r) ----
+  for (size_t i = 0; i + 1 < h.steps.size(); ++i) {
+    Step& a = h.steps[i];
+    const Step& b = h.steps[i + 1];
+    if (a.kind != ST_CONV || b.kind != ST_CONV || a.in_t < 0 || a.full_t < 0 || a.ks != 1 || a.stride != 1 ||
+        a.cin != 64 || a.cout != 32 || a.pool_t >= 0 || a.up_t >= 0 || a.res_t >= 0 || a.yolo >= 0 || a.head ||
+        a.acff || b.ks != 3 || b.stride != 1 || b.cin != 32 || b.cout != 64 || b.in_t != a.full_t ||
+        b.res_t != a.in_t || b.pool_t >= 0 || b.up_t >= 0 || b.yolo >= 0 || b.head || b.acff)
+      continue;
+    bool other = h.tensors[a.full_t].home >= 0;
+    for (size_t j = 0; j < h.steps.size() && !other; ++j)
+      if (j != i + 1 && (h.steps[j].in_t == a.full_t || h.steps[j].res_t == a.full_t)) other = true;
+    for (const Tensor& t : h.tensors)
+      if (t.home == a.full_t) other = true;
+    a.fuse_r = !other;
+  }
   // ---- own buffers for materialised tensors that are not homed in a concat ----
   size_t off = 0;
   for (Tensor& t : h.tensors) {
@@ -1003,6 +1023,18 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
           h.fused_away.push_back(st.pool_t);
         }
       }
+      if (!fused_next && st.fuse_r && tune().res_fuse && st.q < 0 && h.steps[si + 1].q < 0) {
+        const Step& nx = h.steps[si + 1];
+        const ConvArgs b = run_args(h, nx, x, in_kind, n, io, raw);
+        if ((!two || nx.stream == st.stream) && c32r_ok(a, b)) {
+          if (two)
+            for (int d : nx.deps)
+              if (h.steps[d].stream != nx.stream) RTDM_HIP(hipStreamWaitEvent(s, h.step_ev[d], 0));
+          launch_c32r(a, b, s);
+          fused_next = true;
+          h.fused_away.push_back(st.full_t);
+        }
+      }
       if (fused_next) {
       } else if (st.q >= 0 && h.calibrating) {
         launch_chan_absmax(tensor_view(h, st.in_t), n, st.ih, st.iw, st.cin, h.amax.as<unsigned>() + st.amax_off, s);
@@ -1091,6 +1123,7 @@ static ConvArgs geom_args(const rtdm_detector_s& h, const Step& st) {
   }
   if (st.in_t >= 0) {
     const View iv = view_geom(h, st.in_t);
+    a.in = iv.ptr;  // (the placeholder every view carries: c32r_ok compares views)
     a.in_cs = iv.cs;
     a.in_co = iv.co;
   }
@@ -1376,7 +1409,27 @@ rtdm_status rtdm_detector_step_info(rtdm_detector h, int step, char* name, int n
       return a.fuse2 && tune().stem_fuse && a.q < 0 && c.q < 0 && (!(h->two_streams && h->side) || c.stream == a.stream) &&
              stem_pool2_ok(geom_args(*h, a), geom_args(*h, c));
     };
-    if (fused_pair(step)) {
+    const auto res_pair = [&](int i) {
+      if (i < 0 || i + 1 >= (int)h->steps.size()) return false;
+      const Step& a = h->steps[i];
+      const Step& c = h->steps[i + 1];
+      return a.fuse_r && tune().res_fuse && a.q < 0 && c.q < 0 && (!(h->two_streams && h->side) || c.stream == a.stream) &&
+             c32r_ok(geom_args(*h, a), geom_args(*h, c));
+    };
+    if (res_pair(step)) {
+      const Step& a = h->steps[step];
+      const Step& c = h->steps[step + 1];
+      std::string n2;
+      double f2 = 0, b2 = 0;
+      step_info(*h, c, n2, f2, b2);
+      nm = "conv3_c32r";
+      f += f2;
+      b = ((double)a.ih * a.iw * a.cin + (double)c.oh * c.ow * c.cout) * (double)esize_of(h->dtype);
+    } else if (res_pair(step - 1)) {
+      nm = "conv3_c32r:fused";
+      f = 0;
+      b = 0;
+    } else if (fused_pair(step)) {
       const Step& a = h->steps[step];
       const Step& c = h->steps[step + 1];
       std::string n2;
@@ -1566,7 +1619,7 @@ rtdm_status rtdm_detector_layer_output(rtdm_detector h, int layer, int n, float*
     if (!out) return;
     RTDM_REQUIRE(std::find(h->fused_away.begin(), h->fused_away.end(), t) == h->fused_away.end(), RTDM_E_UNSUPPORTED,
                  "layer_output: layer " + std::to_string(layer) +
-                     " output was fused away in the last detect (conv_stem_pool2; rtdm_detector_set_tuning stem_fuse 0 keeps it)");
+                     " output was fused away in the last detect (conv_stem_pool2 / conv3_c32r; rtdm_detector_set_tuning stem_fuse 0 / res_fuse 0 keeps it)");
     RTDM_REQUIRE(n > 0 && n <= h->last_n, RTDM_E_INVALID, "layer_output: n exceeds the last detect batch");
     RTDM_REQUIRE(out_numel >= (int64_t)n * x.c * x.h * x.w, RTDM_E_CAPACITY, "layer_output: out too small");
     launch_to_nchw_f32(tensor_view(*h, t), n, x.h, x.w, x.c, out, h->dtype, (hipStream_t)stream);
