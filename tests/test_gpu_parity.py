@@ -324,10 +324,13 @@ COND_CASES = ["yolov4-tiny-aider-416@608", "yolov3-aider-416@416", "yolov3-spp-a
 
 @pytest.mark.parametrize("case", COND_CASES)
 def test_detector_cond_weights_survey_bars(dev, case):
-    """SURVEY §8d's detector bars, as written, on the well-conditioned synthetic weights
-    (rtdm.synth COND; the reference ships no detector weights):
-      fp32: io x,y <= 1e-3 px, w,h <= 1e-3 px + 1e-5 relative, probabilities <= 1e-4 (deep
-            nets: 2e-3 px / 1e-4 relative / 1e-4), NMS survivors identical;
+    """SURVEY §8d's detector bars on the well-conditioned synthetic weights (rtdm.synth
+    COND; the reference ships no detector weights; its per-cfg knobs, CFG_COND, were chosen
+    so that the fp16-storage floor meets the 0.5 px bar):
+      fp32: io x,y <= 1e-3 px, w,h <= 1e-3 px + 1e-5 relative, probabilities <= 1e-4, as
+            written for the tiny nets; RELAXED for the deep nets (yolov3 / -spp / ACFF: 2e-3
+            px / 1e-4 relative / 1e-4: their 75+ layers' fp32 sums run in another order than
+            the oracle's); NMS survivors identical;
       fp16: every io box coordinate within 0.5 px of the fp32 oracle (x, y, w and h), and
             the NMS survivor sets (conf 0.3 / IoU 0.4) equal after excluding the candidates
             within 1e-3 of the thresholds (oracle.nms.survivors_equal_outside_band).
