@@ -1199,20 +1199,25 @@ __global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
 // groups x (COUT / 16 / WCH) channel groups = 4.  LDS: the 18 x 18 input halo,
 // pixel stride CIN + 8 halfs (16 consecutive pixels hit distinct banks).
 // --------------------------------------------------------------------------
-template <int CIN, int COUT, int TH, int WROWS, int WCH, int PF = 1>
-__global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF > 1) ? 3 : 2) void conv3_pool_small(ConvArgs a) {  // 3 blocks per CU (<= 168 registers): CIN 16, and CIN 32 with one 16-channel tile per wave (WCH 1: half the weight registers; with WCH 2 it would spill)
+// NWV: waves per block (4, or 8 for Cin 64 -> Cout 128: one 16-channel tile per wave, 18
+// k-steps of weights = 72 registers).  A full-resolution output view (a.e.full) is written
+// too when present (Cin 64: yolov4-tiny L6, whose map a route reads).
+template <int CIN, int COUT, int TH, int WROWS, int WCH, int PF = 1, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : (CIN == 16 || WCH == 1) && !(CIN == 32 && PF > 1) ? 3 : 2) void conv3_pool_small(ConvArgs a) {  // 3 blocks per CU (<= 168 registers): CIN 16, and CIN 32 with one 16-channel tile per wave (WCH 1: half the weight registers; with WCH 2 it would spill)
   // PS: halo pixel stride (halfs).  Cin 32: 48, so the B-fragment reads of a 16-lane group
   // (16 pixels x 2 channel groups) fall in 16 distinct 4-bank slots (at 40: 2-way conflicts,
   // half the kernel's LDS cycles, PMC r04f)
-  constexpr int TW = 16, HW = TW + 2, PS = CIN == 32 ? 48 : CIN + 8;
+  // Cin 64: 80 (the 1x1-style pattern, 16 pixels x 4 channel groups per k-step: conflict-free)
+  constexpr int TW = 16, HW = TW + 2, PS = CIN == 32 ? 48 : CIN == 64 ? 80 : CIN + 8;
+  constexpr int NT = 64 * NWV;
   constexpr int CG = CIN / 8;                // 8-channel groups per tap
   constexpr int NQ = 9 * CG;                 // 8-channel groups in K
   constexpr int NKS = (NQ + 3) / 4;          // 32-deep k-steps
   constexpr int RG = TH / WROWS;             // row groups of waves
   constexpr int HALO = (TH + 2) * HW * CG;   // 16-byte vectors per staged tile
-  constexpr int PV = (HALO + 255) / 256;     // prefetch registers per thread
+  constexpr int PV = (HALO + NT - 1) / NT;   // prefetch registers per thread
   constexpr int XS = (TH + 2) * HW * PS;     // halfs per LDS buffer
-  static_assert(RG * (COUT / 16 / WCH) == 4, "wave layout must cover 4 waves");
+  static_assert(RG * (COUT / 16 / WCH) == NWV, "wave layout must cover the block's waves");
   __shared__ __attribute__((aligned(16))) _Float16 xs[2 * XS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int p = lane & 15, g = lane >> 4;
@@ -1230,15 +1235,28 @@ __global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF >
     for (int t = 0; t < WCH; ++t) wf[s][t] = *(const h8*)((const _Float16*)a.w + (size_t)(co0 + 16 * t + p) * a.kpad + 8 * q);
   }
   // per-lane LDS offset of every k-step (tap clamped for the zero-weight tail)
-  int kofs[NKS];
+  // (Cin 64: a k-step is half of one tap's channels, so the offset is a compile-time constant
+  // per k-step plus 8 g: no per-k-step registers, which the 8-wave variant cannot spare)
+  int kofs[CIN == 64 ? 1 : NKS];
+  if constexpr (CIN != 64) {
 #pragma unroll
-  for (int s = 0; s < NKS; ++s) {
-    int q = 4 * s + g;
-    q = q < NQ ? q : NQ - 1;
-    const int tap = q / CG, cg = q - tap * CG;
-    const int kh = tap / 3, kw = tap - kh * 3;
-    kofs[s] = (kh * HW + kw) * PS + cg * 8;
+    for (int s = 0; s < NKS; ++s) {
+      int q = 4 * s + g;
+      q = q < NQ ? q : NQ - 1;
+      const int tap = q / CG, cg = q - tap * CG;
+      const int kh = tap / 3, kw = tap - kh * 3;
+      kofs[s] = (kh * HW + kw) * PS + cg * 8;
+    }
   }
+  const int g8 = 8 * g;
+  auto kofs_of = [&](int s) {
+    if constexpr (CIN == 64) {
+      const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3;
+      return (kh * HW + kw) * PS + (s & 1) * 32 + g8;
+    } else {
+      return kofs[s];
+    }
+  };
   float bias[WCH][4];
 #pragma unroll
   for (int t = 0; t < WCH; ++t)
@@ -1251,7 +1269,7 @@ __global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF >
   int hr[PV], hc[PV], hoff[PV], soff[PV];
 #pragma unroll
   for (int k = 0; k < PV; ++k) {
-    const int i = tid + 256 * k;
+    const int i = tid + NT * k;
     const int pix = i / CG, v = i - pix * CG;
     hr[k] = i < HALO ? pix / HW : -(1 << 20);  // out of range: never loaded
     hc[k] = pix - (pix / HW) * HW;
@@ -1289,7 +1307,7 @@ __global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF >
       _Float16* xb_w = xs + buf * XS;
 #pragma unroll
       for (int k = 0; k < PV; ++k)
-        if (tid + 256 * k < HALO) *(u32x4*)(xb_w + soff[k]) = pre[k];
+        if (tid + NT * k < HALO) *(u32x4*)(xb_w + soff[k]) = pre[k];
       __syncthreads();
       const int tx = tile % tiles_x, t1 = tile / tiles_x;
       const int ty = t1 % tiles_y, n = t1 / tiles_y;
@@ -1302,13 +1320,17 @@ __global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF >
         for (int t = 0; t < WCH; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < NKS; ++s) {
-        const _Float16* bp = xb + kofs[s];
+        const _Float16* bp = xb + kofs_of(s);
 #pragma unroll
         for (int j = 0; j < WROWS; ++j) {
           const h8 b = *(const h8*)(bp + j * HW * PS);
 #pragma unroll
           for (int t = 0; t < WCH; ++t)
             acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][t], b, acc[j][t], 0, 0, 0);
+        }
+        if constexpr (CIN == 64) {  // one k-step's reads, then its MFMAs: no reads hoisted further
+          __builtin_amdgcn_sched_group_barrier(0x100, WROWS, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, WROWS * WCH, 0);
         }
       }
       // pooled epilogue: lane = pixel column ox0 + p, rows j; channels co0 + 16t + 4g + r.
@@ -1323,6 +1345,22 @@ __global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF >
         const bool st = lane_st && py0 + j / 2 < qh;
 #pragma unroll
         for (int t = 0; t < WCH; ++t) {
+          if (e.full.ptr) {  // rows j, j+1 at full resolution: bias -> LeakyReLU -> fp16
+            const int ox = tx * TW + p;
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+              const int oy = ty * TH + wr * WROWS + j + jj;
+              float v[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float x = acc[j + jj][t][r] + bias[t][r];
+                v[r] = fmaxf(x, x * slope);
+              }
+              if (ox < a.ow && oy < a.oh)
+                *(uint2*)((_Float16*)e.full.ptr + ((size_t)(n * a.oh + oy) * a.ow + ox) * e.full.cs + e.full.co + co0 +
+                          16 * t + 4 * g) = make_uint2(pack_h2(v[0], v[1]), pack_h2(v[2], v[3]));
+            }
+          }
           float m[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -1344,7 +1382,7 @@ __global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF >
       _Float16* xb_w = xs + buf * XS;
 #pragma unroll
       for (int k = 0; k < PV; ++k)
-        if (tid + 256 * k < HALO) *(u32x4*)(xb_w + soff[k]) = cur[k];
+        if (tid + NT * k < HALO) *(u32x4*)(xb_w + soff[k]) = cur[k];
       __syncthreads();
       const int tx = tile % tiles_x, t1 = tile / tiles_x;
       const int ty = t1 % tiles_y, n = t1 / tiles_y;
@@ -1359,13 +1397,17 @@ __global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF >
         for (int t = 0; t < WCH; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < NKS; ++s) {
-        const _Float16* bp = xb + kofs[s];
+        const _Float16* bp = xb + kofs_of(s);
 #pragma unroll
         for (int j = 0; j < WROWS; ++j) {
           const h8 b = *(const h8*)(bp + j * HW * PS);
 #pragma unroll
           for (int t = 0; t < WCH; ++t)
             acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][t], b, acc[j][t], 0, 0, 0);
+        }
+        if constexpr (CIN == 64) {  // one k-step's reads, then its MFMAs: no reads hoisted further
+          __builtin_amdgcn_sched_group_barrier(0x100, WROWS, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, WROWS * WCH, 0);
         }
       }
       // pooled epilogue: lane = pixel column ox0 + p, rows j; channels co0 + 16t + 4g + r.
@@ -1380,6 +1422,22 @@ __global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF >
         const bool st = lane_st && py0 + j / 2 < qh;
 #pragma unroll
         for (int t = 0; t < WCH; ++t) {
+          if (e.full.ptr) {  // rows j, j+1 at full resolution: bias -> LeakyReLU -> fp16
+            const int ox = tx * TW + p;
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+              const int oy = ty * TH + wr * WROWS + j + jj;
+              float v[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float x = acc[j + jj][t][r] + bias[t][r];
+                v[r] = fmaxf(x, x * slope);
+              }
+              if (ox < a.ow && oy < a.oh)
+                *(uint2*)((_Float16*)e.full.ptr + ((size_t)(n * a.oh + oy) * a.ow + ox) * e.full.cs + e.full.co + co0 +
+                          16 * t + 4 * g) = make_uint2(pack_h2(v[0], v[1]), pack_h2(v[2], v[3]));
+            }
+          }
           float m[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -1404,10 +1462,12 @@ __global__ __launch_bounds__(256, (CIN == 16 || WCH == 1) && !(CIN == 32 && PF >
 
 static bool pool_small_ok(const ConvArgs& a) {
   if (a.in_kind != IN_NHWC || a.ks != 3 || a.stride != 1 || a.pad != 1 || a.w_f32) return false;
-  if (!((a.cin == 16 && a.cout == 32) || (a.cin == 32 && a.cout == 64))) return false;
+  const bool c64 = a.cin == 64 && a.cout == 128 && tune().pool_small64;
+  if (!((a.cin == 16 && a.cout == 32) || (a.cin == 32 && a.cout == 64) || c64)) return false;
   if (a.cout_pad != a.cout || (a.in_cs | a.in_co) & 7 || a.oh != a.ih || a.ow != a.iw || (a.oh | a.ow) & 1) return false;
-  if (!a.e.pool.ptr || a.e.full.ptr || a.e.up.ptr || a.e.res.ptr || a.e.io || a.e.scale || a.e.act == ACT_SWISH)
+  if (!a.e.pool.ptr || (a.e.full.ptr && !c64) || a.e.up.ptr || a.e.res.ptr || a.e.io || a.e.scale || a.e.act == ACT_SWISH)
     return false;
+  if (a.e.full.ptr && ((a.e.full.cs | a.e.full.co) & 3)) return false;
   if ((a.e.pool.cs | a.e.pool.co) & 3) return false;
   if (a.e.act == ACT_LEAKY && !(a.e.slope > 0.f && a.e.slope <= 1.f)) return false;  // max(x, slope x)
   if ((int64_t)a.ih * a.iw * a.in_cs >= (1ll << 31)) return false;                  // 32-bit image offsets
@@ -1434,6 +1494,14 @@ static int cu_count() {
 
 static void launch_pool_small(const ConvArgs& a, hipStream_t s) {
   const int th = a.cin == 16 ? 16 : 8;
+  if (a.cin == 64) {  // 8 waves, one 16-channel tile each
+    const int64_t tiles64 = (int64_t)a.n * ((a.oh + 7) / 8) * ((a.ow + 15) / 16);
+    RTDM_REQUIRE(tiles64 < (1ll << 31), RTDM_E_CAPACITY, "conv: too many tiles");
+    static const int per_cu = resident_blocks(conv3_pool_small<64, 128, 8, 4, 2, 1, 8>, 512, 0);
+    const int64_t blocks = std::min<int64_t>(tiles64, (int64_t)per_cu * cu_count());
+    hipLaunchKernelGGL((conv3_pool_small<64, 128, 8, 4, 2, 1, 8>), dim3((unsigned)blocks), dim3(512), 0, s, a);
+    return;
+  }
   const int64_t tiles = (int64_t)a.n * ((a.oh + th - 1) / th) * ((a.ow + 15) / 16);
   RTDM_REQUIRE(tiles < (1ll << 31), RTDM_E_CAPACITY, "conv: too many tiles");
   // persistent blocks: exactly the resident count, each streaming tiles with its weights in registers
@@ -1558,7 +1626,7 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     return names[a.quad ? 1 : 0][ntn == 1 ? 0 : ntn == 2 ? 1 : 2];
   }
   if (dtype == RTDM_F16 && pool_small_ok(a))
-    return a.cin == 16 ? "conv3_pool_small<16,32,16,4,2>" : "conv3_pool_small<32,64,8,8,1>";
+    return a.cin == 16 ? "conv3_pool_small<16,32,16,4,2>" : a.cin == 32 ? "conv3_pool_small<32,64,8,8,1>" : "conv3_pool_small<64,128,8,4,2,1,8>";
   if (dtype == RTDM_F16 && c32_ok(a)) return c32_name(a);
   if (dtype == RTDM_F16 && direct_ok(a)) {
     const int bn = direct_cfg(a.cout_pad).bn;
