@@ -1517,6 +1517,14 @@ static void launch_pool_small(const ConvArgs& a, hipStream_t s) {
       hipLaunchKernelGGL((conv3_pool_small<16, 32, 16, 4, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((conv3_pool_small<16, 32, 16, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  } else if (tune().pool_small32 == 1) {  // two channel tiles per wave, 4 waves (half the B reads)
+    static const int per_cu = resident_blocks(conv3_pool_small<32, 64, 8, 4, 2>, 256, 0);
+    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cu_count());
+    hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  } else if (tune().pool_small32 == 2) {  // two channel tiles per wave, 8 waves
+    static const int per_cu = resident_blocks(conv3_pool_small<32, 64, 8, 2, 2, 1, 8>, 512, 0);
+    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cu_count());
+    hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 2, 2, 1, 8>), dim3((unsigned)blocks), dim3(512), 0, s, a);
   } else {
     static const int per_cu = resident_blocks(conv3_pool_small<32, 64, 8, 8, 1>, 256, 0);
     static const int per_cu2 = resident_blocks(conv3_pool_small<32, 64, 8, 8, 1, 2>, 256, 0);
@@ -1626,7 +1634,11 @@ const char* conv_kernel_name(const ConvArgs& a, int dtype) {
     return names[a.quad ? 1 : 0][ntn == 1 ? 0 : ntn == 2 ? 1 : 2];
   }
   if (dtype == RTDM_F16 && pool_small_ok(a))
-    return a.cin == 16 ? "conv3_pool_small<16,32,16,4,2>" : a.cin == 32 ? "conv3_pool_small<32,64,8,8,1>" : "conv3_pool_small<64,128,8,4,2,1,8>";
+    return a.cin == 16   ? "conv3_pool_small<16,32,16,4,2>"
+           : a.cin == 64 ? "conv3_pool_small<64,128,8,4,2,1,8>"
+           : tune().pool_small32 == 1 ? "conv3_pool_small<32,64,8,4,2>"
+           : tune().pool_small32 == 2 ? "conv3_pool_small<32,64,8,2,2,1,8>"
+                                      : "conv3_pool_small<32,64,8,8,1>";
   if (dtype == RTDM_F16 && c32_ok(a)) return c32_name(a);
   if (dtype == RTDM_F16 && direct_ok(a)) {
     const int bn = direct_cfg(a.cout_pad).bn;
