@@ -159,7 +159,8 @@ const char* rtdm_build_arch(void);
  * | 1 | 2 (bit-identical); "pool_small64" 1 = 3x3 Cin 64 -> Cout 128 + 2x2 pool (+ full
  * map) on conv3_pool_small (default; bit-identical to 0 = conv_pipe); "pool_small32" 0 =
  * the Cin-32 pooled layer with one 16-channel tile per wave (default) | 1 | 2 = two tiles
- * per wave on 4 | 8 waves (bit-identical, measured slower); "stem_persist" 1 = the pooled uint8 stem as a persistent
+ * per wave on 4 | 8 waves (bit-identical, measured slower); "pool_sep" 1 = stride-1 5 / 9 /
+ * 13 max pools (SPP) as separable band kernels (default; bit-identical to 0); "stem_persist" 1 = the pooled uint8 stem as a persistent
  * kernel with the next row band's frame bytes in flight (conv_stem3p, bit-identical;
  * default 0: measured slower, profiles/r04u_stem_ab.txt).
  * Unknown keys: RTDM_E_INVALID. */

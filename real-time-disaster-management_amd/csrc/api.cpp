@@ -57,6 +57,7 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "res_fuse") t.res_fuse = v < 0 ? 0 : v > 2 ? 2 : v;
   else if (k == "stem_persist") t.stem_persist = v ? 1 : 0;
   else if (k == "pipe_regpool") t.pipe_regpool = v ? 1 : 0;
+  else if (k == "pool_sep") t.pool_sep = v ? 1 : 0;
   else if (k == "pool_small32") t.pool_small32 = v < 0 ? 0 : v > 2 ? 2 : v;
   else if (k == "pool_small64") t.pool_small64 = v ? 1 : 0;
   else if (k == "pool_small_pf") t.pool_small_pf = v <= 0 ? 0 : v >= 2 ? 2 : 1;

@@ -203,6 +203,7 @@ struct Tuning {
   int fuse_head = 0;        // fused YOLO head convs (plan time; 0: the 3x3 on the unrolled window kernel + head1x1_f16, measured faster r04h)
   int two_streams = 1;      // detector head branches on a second stream (plan time)
   int pipe_regpool = 0;     // conv_pipe register epilogue for pool / upsample layers too
+  int pool_sep = 1;         // separable stride-1 max pools (K 5 / 9 / 13: the SPP block)
   int pool_small32 = 0;     // Cin-32 conv3_pool_small layout: 0 one channel tile per wave, 1 two (4 waves), 2 two (8 waves)
   int pool_small64 = 1;     // conv3_pool_small for 3x3 Cin 64 -> 128 + pool (+ full map)
   int pool_small_pf = 0;    // conv3_pool_small halo tiles in flight per block (0 auto | 1 | 2)

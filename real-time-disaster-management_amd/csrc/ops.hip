@@ -443,11 +443,84 @@ __global__ __launch_bounds__(256) void maxpool_vec_kernel(const T* __restrict__ 
   }
 }
 
+// Stride-1 "same" max pools with K >= 5 (the SPP block of yolov3-spp: 5 / 9 / 13,
+// models.py:57-64 with padding (K-1)/2, i.e. -inf outside the map): one thread per (image,
+// column, 8-channel group, band of R output rows) computes the R + K - 1 horizontal K-maxima
+// its band needs once (K loads each) and takes each output as the max of K of them: ~(R + K
+// - 1) K / R loads per output instead of K^2 (13: 32.5 instead of 169).  max is exact and
+// takes the same window, so the values are the generic kernel's (in fp16, as stored).
+template <int K, int R>
+__global__ __launch_bounds__(256) void maxpool_s1_sep_kernel(const _Float16* __restrict__ in, int in_cs, int in_co, int n,
+                                                             int h, int w, int c, _Float16* __restrict__ out, int out_cs,
+                                                             int out_co) {
+  typedef _Float16 h8v_ __attribute__((ext_vector_type(8)));
+  constexpr int P = K / 2, NR = R + K - 1;
+  const int cg = c >> 3, bands = (h + R - 1) / R;
+  const int total = n * bands * w * cg;
+  for (unsigned uidx = blockIdx.x * blockDim.x + threadIdx.x; uidx < (unsigned)total; uidx += gridDim.x * blockDim.x) {
+    int idx = (int)uidx;
+    const int g = idx % cg;
+    idx /= cg;
+    const int x = idx % w;
+    idx /= w;
+    const int band = idx % bands, b = idx / bands;
+    const int y0 = band * R;
+    const _Float16* base = in + (size_t)b * h * w * in_cs + in_co + g * 8;
+    h8v_ hm[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int iy = y0 - P + r;
+      h8v_ m;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = (_Float16)-INFINITY;
+      if ((unsigned)iy < (unsigned)h) {
+#pragma unroll
+        for (int dx = 0; dx < K; ++dx) {
+          const int ix = x - P + dx;
+          if ((unsigned)ix < (unsigned)w) {
+            const h8v_ v = *(const h8v_*)(base + ((size_t)iy * w + ix) * in_cs);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m[j] = m[j] > v[j] ? m[j] : v[j];
+          }
+        }
+      }
+      hm[r] = m;
+    }
+#pragma unroll
+    for (int o = 0; o < R; ++o) {
+      const int oy = y0 + o;
+      if (oy >= h) break;
+      h8v_ m = hm[o];
+#pragma unroll
+      for (int r = 1; r < K; ++r)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = m[j] > hm[o + r][j] ? m[j] : hm[o + r][j];
+      *(h8v_*)(out + (((size_t)b * h + oy) * w + x) * out_cs + out_co + g * 8) = m;
+    }
+  }
+}
+
 void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, int stride, int pad, int zero_rb,
                     View ov, int oh, int ow, int dtype, hipStream_t s) {
   (void)in;
   const int64_t total = (int64_t)n * oh * ow * c;
   if (total <= 0) return;
+  if (dtype == RTDM_F16 && tune().pool_sep && stride == 1 && !zero_rb && (k == 5 || k == 9 || k == 13) &&
+      pad == k / 2 && oh == h && ow == w && c % 8 == 0 && ((iv.cs | iv.co | ov.cs | ov.co) % 8) == 0 &&
+      (int64_t)n * ((h + 7) / 8) * w * (c / 8) < (1ll << 31)) {
+    constexpr int R = 8;
+    const int gv = grid_for((int64_t)n * ((h + R - 1) / R) * w * (c / 8), 256);
+    const _Float16* ip = (const _Float16*)iv.ptr;
+    _Float16* op = (_Float16*)ov.ptr;
+    if (k == 5)
+      hipLaunchKernelGGL((maxpool_s1_sep_kernel<5, R>), dim3(gv), dim3(256), 0, s, ip, iv.cs, iv.co, n, h, w, c, op, ov.cs, ov.co);
+    else if (k == 9)
+      hipLaunchKernelGGL((maxpool_s1_sep_kernel<9, R>), dim3(gv), dim3(256), 0, s, ip, iv.cs, iv.co, n, h, w, c, op, ov.cs, ov.co);
+    else
+      hipLaunchKernelGGL((maxpool_s1_sep_kernel<13, R>), dim3(gv), dim3(256), 0, s, ip, iv.cs, iv.co, n, h, w, c, op, ov.cs, ov.co);
+    RTDM_HIP(hipGetLastError());
+    return;
+  }
   const int vec = dtype == RTDM_F16 ? 8 : 4;
   if (c % vec == 0 && ((iv.cs | iv.co | ov.cs | ov.co) % vec) == 0 && total / vec < (1ll << 31)) {
     const int gv = grid_for(total / vec, 256);

@@ -51,3 +51,24 @@ def test_pool_small_variants_bit_identical(case, knob):
         assert "conv3_pool_small<64,128,8,4,2,1,8>" in names[1], names[1][:8]
         assert "conv3_pool_small<64,128,8,4,2,1,8>" not in names[0]
     assert torch.equal(outs[v0], outs[v1]), float((outs[v0] - outs[v1]).abs().max())
+
+
+@pytest.mark.parametrize("case", ["yolov3-spp-aider@320:3", "yolov3-spp-aider@608:1"])
+def test_spp_separable_maxpool_bit_identical(case):
+    """The SPP block's stride-1 5 / 9 / 13 max pools as separable band kernels (pool_sep 1,
+    default: horizontal K-maxima per row once, then K of them per output) against the
+    direct K x K kernel (0): max is exact over the same window, so the io is BIT-IDENTICAL."""
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    cfg, rest = case.split("@")
+    size, b = (int(v) for v in rest.split(":"))
+    x = torch.from_numpy(synth_frames(b, size, size, seed=89)).cuda()
+    outs = {}
+    try:
+        for v in (0, 1):
+            L.check(L.lib().rtdm_set_tuning(b"pool_sep", v))
+            m, _, _, _ = _detector(cfg, size, preset="cond")
+            outs[v] = m(x)[0].cpu()
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"pool_sep", 1))
+    assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
