@@ -160,7 +160,8 @@ const char* rtdm_build_arch(void);
  * map) on conv3_pool_small (default; bit-identical to 0 = conv_pipe); "pool_small32" 0 =
  * the Cin-32 pooled layer with one 16-channel tile per wave (default) | 1 | 2 = two tiles
  * per wave on 4 | 8 waves (bit-identical, measured slower); "pool_sep" 1 = stride-1 5 / 9 /
- * 13 max pools (SPP) as separable band kernels (default; bit-identical to 0); "stem_persist" 1 = the pooled uint8 stem as a persistent
+ * 13 max pools (SPP) and the zero-padded 2 x 2 stride-1 pool as separable band kernels
+ * (default; bit-identical to 0); "stem_persist" 1 = the pooled uint8 stem as a persistent
  * kernel with the next row band's frame bytes in flight (conv_stem3p, bit-identical;
  * default 0: measured slower, profiles/r04u_stem_ab.txt).
  * Unknown keys: RTDM_E_INVALID. */

@@ -449,12 +449,15 @@ __global__ __launch_bounds__(256) void maxpool_vec_kernel(const T* __restrict__ 
 // its band needs once (K loads each) and takes each output as the max of K of them: ~(R + K
 // - 1) K / R loads per output instead of K^2 (13: 32.5 instead of 169).  max is exact and
 // takes the same window, so the values are the generic kernel's (in fp16, as stored).
-template <int K, int R>
+// ZRB: Darknet's size-2 stride-1 pool (ZeroPad2d((0,1,0,1)) + MaxPool2d(2,1), models.py:57-64):
+// the window starts at the output pixel and taps past the right / bottom edge are zeros.
+template <int K, int R, bool ZRB = false>
 __global__ __launch_bounds__(256) void maxpool_s1_sep_kernel(const _Float16* __restrict__ in, int in_cs, int in_co, int n,
                                                              int h, int w, int c, _Float16* __restrict__ out, int out_cs,
                                                              int out_co) {
   typedef _Float16 h8v_ __attribute__((ext_vector_type(8)));
-  constexpr int P = K / 2, NR = R + K - 1;
+  constexpr int P = ZRB ? 0 : K / 2, NR = R + K - 1;
+  const _Float16 pad_v = ZRB ? (_Float16)0.f : (_Float16)-INFINITY;  // value of a tap off the map
   const int cg = c >> 3, bands = (h + R - 1) / R;
   const int total = n * bands * w * cg;
   for (unsigned uidx = blockIdx.x * blockDim.x + threadIdx.x; uidx < (unsigned)total; uidx += gridDim.x * blockDim.x) {
@@ -472,8 +475,10 @@ __global__ __launch_bounds__(256) void maxpool_s1_sep_kernel(const _Float16* __r
       const int iy = y0 - P + r;
       h8v_ m;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = (_Float16)-INFINITY;
-      if ((unsigned)iy < (unsigned)h) {
+      for (int j = 0; j < 8; ++j) m[j] = pad_v;
+      if ((unsigned)iy < (unsigned)h) {  // (a row off the map is pad_v throughout)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = (_Float16)-INFINITY;
 #pragma unroll
         for (int dx = 0; dx < K; ++dx) {
           const int ix = x - P + dx;
@@ -481,6 +486,9 @@ __global__ __launch_bounds__(256) void maxpool_s1_sep_kernel(const _Float16* __r
             const h8v_ v = *(const h8v_*)(base + ((size_t)iy * w + ix) * in_cs);
 #pragma unroll
             for (int j = 0; j < 8; ++j) m[j] = m[j] > v[j] ? m[j] : v[j];
+          } else if (ZRB) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m[j] = m[j] > pad_v ? m[j] : pad_v;
           }
         }
       }
@@ -505,14 +513,17 @@ void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, 
   (void)in;
   const int64_t total = (int64_t)n * oh * ow * c;
   if (total <= 0) return;
-  if (dtype == RTDM_F16 && tune().pool_sep && stride == 1 && !zero_rb && (k == 5 || k == 9 || k == 13) &&
-      pad == k / 2 && oh == h && ow == w && c % 8 == 0 && ((iv.cs | iv.co | ov.cs | ov.co) % 8) == 0 &&
-      (int64_t)n * ((h + 7) / 8) * w * (c / 8) < (1ll << 31)) {
+  const bool spp = !zero_rb && (k == 5 || k == 9 || k == 13) && pad == k / 2;
+  const bool zrb2 = zero_rb && k == 2 && pad == 0;
+  if (dtype == RTDM_F16 && tune().pool_sep && stride == 1 && (spp || zrb2) && oh == h && ow == w && c % 8 == 0 &&
+      ((iv.cs | iv.co | ov.cs | ov.co) % 8) == 0 && (int64_t)n * ((h + 7) / 8) * w * (c / 8) < (1ll << 31)) {
     constexpr int R = 8;
     const int gv = grid_for((int64_t)n * ((h + R - 1) / R) * w * (c / 8), 256);
     const _Float16* ip = (const _Float16*)iv.ptr;
     _Float16* op = (_Float16*)ov.ptr;
-    if (k == 5)
+    if (zrb2)
+      hipLaunchKernelGGL((maxpool_s1_sep_kernel<2, R, true>), dim3(gv), dim3(256), 0, s, ip, iv.cs, iv.co, n, h, w, c, op, ov.cs, ov.co);
+    else if (k == 5)
       hipLaunchKernelGGL((maxpool_s1_sep_kernel<5, R>), dim3(gv), dim3(256), 0, s, ip, iv.cs, iv.co, n, h, w, c, op, ov.cs, ov.co);
     else if (k == 9)
       hipLaunchKernelGGL((maxpool_s1_sep_kernel<9, R>), dim3(gv), dim3(256), 0, s, ip, iv.cs, iv.co, n, h, w, c, op, ov.cs, ov.co);

@@ -53,11 +53,13 @@ def test_pool_small_variants_bit_identical(case, knob):
     assert torch.equal(outs[v0], outs[v1]), float((outs[v0] - outs[v1]).abs().max())
 
 
-@pytest.mark.parametrize("case", ["yolov3-spp-aider@320:3", "yolov3-spp-aider@608:1"])
+@pytest.mark.parametrize("case", ["yolov3-spp-aider@320:3", "yolov3-spp-aider@608:1", "yolov4-tiny-aider-416@608:3",
+                                  "yolov3-tiny-aider-416@416:2"])
 def test_spp_separable_maxpool_bit_identical(case):
-    """The SPP block's stride-1 5 / 9 / 13 max pools as separable band kernels (pool_sep 1,
-    default: horizontal K-maxima per row once, then K of them per output) against the
-    direct K x K kernel (0): max is exact over the same window, so the io is BIT-IDENTICAL."""
+    """Stride-1 max pools as separable band kernels (pool_sep 1, default: horizontal K-maxima
+    per row once, then K of them per output) against the direct K x K kernel (0): the SPP
+    block's 5 / 9 / 13 (-inf padding) and the tiny nets' 2 x 2 with Darknet's zero pad on the
+    right / bottom.  max is exact over the same window, so the io is BIT-IDENTICAL."""
     from rtdm import _lib as L
     from rtdm.synth import synth_frames
     cfg, rest = case.split("@")
