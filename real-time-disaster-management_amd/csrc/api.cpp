@@ -55,6 +55,7 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "two_streams") t.two_streams = v ? 1 : 0;
   else if (k == "conv_c32") t.conv_c32 = v ? 1 : 0;
   else if (k == "res_fuse") t.res_fuse = v < 0 ? 0 : v > 2 ? 2 : v;
+  else if (k == "stem_k16") t.stem_k16 = v ? 1 : 0;
   else if (k == "stem_persist") t.stem_persist = v ? 1 : 0;
   else if (k == "pipe_regpool") t.pipe_regpool = v ? 1 : 0;
   else if (k == "pool_sep") t.pool_sep = v ? 1 : 0;

@@ -207,6 +207,7 @@ struct Tuning {
   int pool_small32 = 0;     // Cin-32 conv3_pool_small layout: 0 one channel tile per wave, 1 two (4 waves), 2 two (8 waves)
   int pool_small64 = 1;     // conv3_pool_small for 3x3 Cin 64 -> 128 + pool (+ full map)
   int pool_small_pf = 0;    // conv3_pool_small halo tiles in flight per block (0 auto | 1 | 2)
+  int stem_k16 = 1;         // pooled MFMA stem: the kh = 2 third of K as a 16-deep MFMA (0: 32-deep)
   int stem_persist = 0;     // conv_stem3p for the pooled uint8 stem (measured slower r04u)
   int conv_c32 = 1;         // conv3_c32 for the Cin-32 3x3 convs (conv_c32.hip)
   int res_fuse = 1;         // conv3_c32r: Darknet-53's first residual block as one launch (1: 8 waves, 2: 4 waves)

@@ -366,6 +366,17 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
     return x * sc[t][j] + sh[t][j];
   };
   const int kh0 = g >> 1, pr0 = g & 1;
+  // ABL bit 8 (stem_k16, default; pooled stems only): the kh = 2 third of K as one 16-deep
+  // MFMA (lane group g = pixel kw = g, 4 channels; kw = 3 has zero weights) instead of a
+  // 32-deep one whose lanes g >= 2 re-read kh = 2 pixels against zero weights: the same
+  // nonzero products, bit-identical (tests/test_gpu_stem.py).  Launched for the lean pooled
+  // epilogue only: the channel-major plain stem and the swish pooled epilogue gave wrong
+  // results (NaN) with the same change, not yet understood, and keep the 32-deep MFMA.
+  constexpr bool K16 = (ABL & 8) != 0;
+  typedef _Float16 h4s __attribute__((ext_vector_type(4)));
+  h4s w16[NTN];
+#pragma unroll
+  for (int t = 0; t < NTN; ++t) w16[t] = *(const h4s*)((const _Float16*)a.w_stem + (size_t)(16 * t + p) * 64 + 32 + 4 * g);
   if (POOL) {
     // waves 0,1 -> quad row 0, waves 2,3 -> quad row 1 (ROWS == 4); a wave's
     // tiles are 4 consecutive quads, striding by 2 tiles.
@@ -383,6 +394,7 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
     const int lx0 = (2 * ((wid & 1) * 4 + (p >> 2)) + (d & 1)) * s - pad + 1;
     const uint2* rk0 = stem_lds + (ly * s + kh0) * ls + lx0 + 2 * pr0;
     const uint2* rk2 = stem_lds + (ly * s + 2) * ls + lx0 + 2 * (g & 1);
+    const uint2* rk2s = stem_lds + (ly * s + 2) * ls + lx0 + g;
     _Float16* pool_row = (_Float16*)e.pool.ptr + ((size_t)n * qh + py) * qw * e.pool.cs + e.pool.co;
     // Darknet stem (no BN affine after the fold, LeakyReLU / linear): LeakyReLU as
     // max(x, slope x) (0 < slope < 1; 1 = linear), no per-value branches
@@ -394,14 +406,19 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
     constexpr bool LEAN = decltype(lean_c)::value;
     for (int tx0 = wid & 1, off = 0; tx0 * 4 < qw; tx0 += 4, off += 32 * s) {
       h8 bf0[2], bf1[2];
+      h4s bk[2];
       int oq[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int tx = tx0 + 2 * u, o = off + u * 16 * s;
         const uint2 b00 = rk0[o], b01 = rk0[o + 1];
-        const uint2 b10 = rk2[o], b11 = rk2[o + 1];
         bf0[u] = __builtin_bit_cast(h8, (u32x4{b00.x, b00.y, b01.x, b01.y}));
-        bf1[u] = __builtin_bit_cast(h8, (u32x4{b10.x, b10.y, b11.x, b11.y}));
+        if constexpr (K16) {
+          bk[u] = __builtin_bit_cast(h4s, rk2s[o]);
+        } else {
+          const uint2 b10 = rk2[o], b11 = rk2[o + 1];
+          bf1[u] = __builtin_bit_cast(h8, (u32x4{b10.x, b10.y, b11.x, b11.y}));
+        }
         oq[u] = tx * 4 + g;  // pooled x of this lane's output quad
       }
 #pragma unroll
@@ -410,10 +427,16 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           if constexpr ((ABL & 4) != 0) {
-            acc[u] = f4{(float)bf0[u][0], (float)bf0[u][1], (float)bf1[u][2], (float)bf1[u][3]};
+            if constexpr (K16)
+              acc[u] = f4{(float)bf0[u][0], (float)bf0[u][1], (float)bk[u][2], (float)bk[u][3]};
+            else
+              acc[u] = f4{(float)bf0[u][0], (float)bf0[u][1], (float)bf1[u][2], (float)bf1[u][3]};
           } else {
             acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf0[u], wa[t][0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1[u], wa[t][1], acc[u], 0, 0, 0);
+            if constexpr (K16)
+              acc[u] = __builtin_amdgcn_mfma_f32_16x16x16f16(bk[u], w16[t], acc[u], 0, 0, 0);
+            else
+              acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1[u], wa[t][1], acc[u], 0, 0, 0);
           }
         }
         const int c = 16 * t + p;
@@ -1681,6 +1704,9 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
       else if (ntn == 1 && abl == 2) hipLaunchKernelGGL((conv_stem3<true, 1, 2>), dim3(blocks), dim3(256), lds, s, a);
       else if (ntn == 1 && abl == 4) hipLaunchKernelGGL((conv_stem3<true, 1, 4>), dim3(blocks), dim3(256), lds, s, a);
       else if (ntn == 1 && abl == 7) hipLaunchKernelGGL((conv_stem3<true, 1, 7>), dim3(blocks), dim3(256), lds, s, a);
+      else if (ntn == 1 && tune().stem_k16 && !a.e.scale && a.e.act != ACT_SWISH &&
+               (a.e.act != ACT_LEAKY || (a.e.slope > 0.f && a.e.slope <= 1.f)))  // the lean epilogue only
+        hipLaunchKernelGGL((conv_stem3<true, 1, 8>), dim3(blocks), dim3(256), lds, s, a);
       else if (ntn == 1) hipLaunchKernelGGL((conv_stem3<true, 1>), dim3(blocks), dim3(256), lds, s, a);
       else if (ntn == 2) hipLaunchKernelGGL((conv_stem3<true, 2>), dim3(blocks), dim3(256), lds, s, a);
       else hipLaunchKernelGGL((conv_stem3<true, 4>), dim3(blocks), dim3(256), lds, s, a);

@@ -79,14 +79,15 @@ def test_stem_pair_fused_layer_output_and_nchw():
 
 
 
-@pytest.mark.parametrize("knob", [("stem_persist", 0, 1, "conv_stem3p<1>")])
+@pytest.mark.parametrize("knob", [("stem_persist", 0, 1, "conv_stem3p<1>"), ("stem_k16", 0, 1, None)])
 @pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608:3", "yolov4-tiny-aider-416@416:5",
                                   "yolov3-tiny-aider-416@416:2", "yolov4-tiny-aider-416@256:7"])
 def test_stem_variants_bit_identical(case, knob):
     """Pooled uint8 stem variants against conv_stem3<true> with its defaults: conv_stem3p
     (persistent: the next band's frame bytes in flight while the current band computes;
-    rtdm_set_tuning("stem_persist", 1); measured slower, off by default).  Per tile the same
-    staging, MFMAs and epilogue: BIT-IDENTICAL io."""
+    rtdm_set_tuning("stem_persist", 1); measured slower, off by default), and the kh = 2 third
+    of K as a 32-deep MFMA (stem_k16 0) instead of the default 16-deep one (the same nonzero
+    products).  BIT-IDENTICAL io."""
     from rtdm import _lib as L
     from rtdm.synth import synth_frames
     key, base, alt, name = knob
@@ -101,7 +102,7 @@ def test_stem_variants_bit_identical(case, knob):
             outs[v] = m(x)[0].cpu()
             names[v] = _names(m, b)
     finally:
-        L.check(L.lib().rtdm_set_tuning(key.encode(), base))
+        L.check(L.lib().rtdm_set_tuning(key.encode(), {"stem_persist": 0, "stem_k16": 1}[key]))
     assert names[base][0].startswith("conv_stem3<true"), names[base][:2]
     if name:
         assert names[alt][0] == name, names[alt][:2]
