@@ -125,7 +125,8 @@ const char* rtdm_build_arch(void);
  * copy can be changed afterwards with rtdm_detector_set_tuning /
  * rtdm_classifier_set_tuning (every call on a handle runs with its own copy, so two
  * handles in one process can differ, e.g. a latency and a throughput pipeline).
- * Plan-time keys ("fuse_head", "two_streams") only act at handle creation.
+ * Plan-time keys ("fuse_head", "two_streams") only act at handle creation:
+ * rtdm_detector_set_tuning refuses them on a created handle (RTDM_E_INVALID).
  * key "conv_pipe": 1 = pipelined 256x128 implicit GEMM for Cin%64==0 convs
  * (default), 0 = conv_glds_f16 128x128; key "fuse_head": 1 = conv -> 1x1 head conv
  * -> [yolo] planned as one launch, 0 = separate head conv (default: the conv then runs
@@ -138,32 +139,23 @@ const char* rtdm_build_arch(void);
  * launch's rounds of tiles (latency, default) | 1 = CU-time (throughput, for several
  * batches in flight); "conv_pipe_win" 1 = window mode for 3x3/s1 layers (default);
  * "conv_pipe_korder" 1 = channel-block-outer K order (default; 0 changes the fp32
- * summation order); "conv_pipe_pf" 1 = cross-tile prologue prefetch (default; not
- * with ping-pong); "conv_pipe_pp" 1 = ping-pong K-loop (two wave groups
- * alternating MFMA and memory phases; default 0: measured 4-18 % slower per layer,
- * DESIGN.md §3.4); "conv_pipe_wloop" 1 = tap-unrolled 3x3 K-loop for the
- * register-epilogue layers (default), 0 = the cursor loop; "conv_pipe_walk" g =
- * tile walk in N-groups of g panels (default 2, 0 = M-major); "conv_wide" 0 = off
- * (default: the 256x256-tile kernel measured slower) | 1 = where the
- * cost model picks it | 2 always | 3 one round of wide tiles + a 256x128 tail;
- * "conv_wide_eff" its cost-model rate (x100); "stem_fuse" 1 = a pooled Cin-3 stem and the
- * 16 -> 32 pooled 3x3 conv reading its map as one conv_stem_pool2 launch (bit-identical;
- * default 0: measured slower); "conv_c32" 1 = the Cin-32 3x3 convs on
- * conv3_c32 (default; bit-identical to 0 = conv_mfma / conv3_direct); "res_fuse" 1 =
+ * summation order); "conv_pipe_pf" 1 = cross-tile prologue prefetch (default);
+ * "conv_pipe_wloop" 1 = tap-unrolled 3x3 K-loop for the register-epilogue layers
+ * (default), 0 = the cursor loop; "conv_pipe_walk" g = tile walk in N-groups of g
+ * panels (default 2, 0 = M-major); "conv_c32" 1 = the Cin-32 3x3 convs on conv3_c32
+ * (default; bit-identical to 0 = conv_mfma / conv3_direct); "res_fuse" 1 =
  * Darknet-53's first residual block (1x1 64 -> 32, 3x3 32 -> 64, shortcut) as one
  * conv3_c32r launch, 8 waves (default; 2 = 4 waves; 0 = two launches; bit-identical;
- * the reduce map is then not materialised: layer_output refuses it); "pipe_regpool" 1 =
- * conv_pipe's register epilogue also for the pool / upsample layers (bit-identical;
- * default 0: measured slower, profiles/r04r_regpool_ab.txt); "pool_small_pf" 0 = halo
- * tiles in flight per conv3_pool_small block by Cin (default: 2 for Cin 16, 1 for Cin 32)
- * | 1 | 2 (bit-identical); "pool_small64" 1 = 3x3 Cin 64 -> Cout 128 + 2x2 pool (+ full
- * map) on conv3_pool_small (default; bit-identical to 0 = conv_pipe); "pool_small32" 0 =
- * the Cin-32 pooled layer with one 16-channel tile per wave (default) | 1 | 2 = two tiles
- * per wave on 4 | 8 waves (bit-identical, measured slower); "pool_sep" 1 = stride-1 5 / 9 /
- * 13 max pools (SPP) and the zero-padded 2 x 2 stride-1 pool as separable band kernels
- * (default; bit-identical to 0); "stem_persist" 1 = the pooled uint8 stem as a persistent
- * kernel with the next row band's frame bytes in flight (conv_stem3p, bit-identical;
- * default 0: measured slower, profiles/r04u_stem_ab.txt).
+ * the reduce map is then not materialised: layer_output refuses it); "stem_k16" 1 = the
+ * Cin-3 MFMA stems with the kh = 2 third of K on a 16-deep MFMA (default; bit-identical
+ * to 0 = a 32-deep one); "pool_small_pf" 0 = halo tiles in flight per conv3_pool_small
+ * block by Cin (default: 2 for Cin 16, 1 for Cin 32) | 1 | 2 (bit-identical);
+ * "pool_small64" 1 = 3x3 Cin 64 -> Cout 128 + 2x2 pool (+ full map) on conv3_pool_small
+ * (default; bit-identical to 0 = conv_pipe); "pool_sep" 1 = stride-1 5 / 9 / 13 max pools
+ * (SPP) and the zero-padded 2 x 2 stride-1 pool as separable band kernels (default;
+ * bit-identical to 0).  Variants measured slower in earlier rounds (256 x 256 conv tiles,
+ * the ping-pong K-loop, the fused stem pair, the persistent stem, register-epilogue pools)
+ * were removed (DESIGN.md §3.4 keeps their numbers).
  * Unknown keys: RTDM_E_INVALID. */
 rtdm_status rtdm_set_tuning(const char* key, int value);
 /* The same keys on one handle's own copy (see above). */

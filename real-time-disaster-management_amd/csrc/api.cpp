@@ -43,12 +43,9 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "conv_pipe_bm") t.pipe_bm = (v == 256 || v == 128 || v == 64) ? v : 0;
   else if (k == "conv_pipe_win") t.pipe_win = v ? 1 : 0;
   else if (k == "conv_pipe_pf") t.pipe_pf = v ? 1 : 0;
-  else if (k == "conv_pipe_pp") t.pipe_pp = v ? 1 : 0;
   else if (k == "conv_pipe_walk") t.pipe_walk = v > 0 ? v : 0;
   else if (k == "conv_pipe_cost") t.pipe_cost = v ? 1 : 0;
   else if (k == "conv_pipe_wloop") t.pipe_wloop = v ? 1 : 0;
-  else if (k == "conv_wide") t.pipe_wide = v < 0 ? 0 : v;
-  else if (k == "conv_wide_eff") t.pipe_wide_eff = v > 0 ? v : 115;
   else if (k == "head1x1") t.head1x1 = v ? 1 : 0;
   else if (k == "dw3_tile") t.dw3_tile = v ? 1 : 0;
   else if (k == "fuse_head") t.fuse_head = v ? 1 : 0;
@@ -56,19 +53,20 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "conv_c32") t.conv_c32 = v ? 1 : 0;
   else if (k == "res_fuse") t.res_fuse = v < 0 ? 0 : v > 2 ? 2 : v;
   else if (k == "stem_k16") t.stem_k16 = v ? 1 : 0;
-  else if (k == "stem_persist") t.stem_persist = v ? 1 : 0;
-  else if (k == "pipe_regpool") t.pipe_regpool = v ? 1 : 0;
   else if (k == "pool_sep") t.pool_sep = v ? 1 : 0;
-  else if (k == "pool_small32") t.pool_small32 = v < 0 ? 0 : v > 2 ? 2 : v;
   else if (k == "pool_small64") t.pool_small64 = v ? 1 : 0;
   else if (k == "pool_small_pf") t.pool_small_pf = v <= 0 ? 0 : v >= 2 ? 2 : 1;
   else if (k == "acff_persist") t.acff_persist = v < 0 ? 0 : v;
   else if (k == "acff_chain") t.acff_chain = v;
   else if (k == "stem_abl") t.stem_abl = v;
-  else if (k == "stem_fuse") t.stem_fuse = v < 0 ? 0 : v;
   else if (k == "nms_variant") t.nms_variant = v;
   else if (k == "resize_stream") t.resize_stream = v;
   else throw Error{RTDM_E_INVALID, "set_tuning: unknown key " + k};
+}
+
+bool tuning_is_plan_time(const char* key) {
+  const std::string k = key ? key : "";
+  return k == "fuse_head" || k == "two_streams";
 }
 
 }  // namespace rtdm

@@ -700,7 +700,6 @@ rtdm_status rtdm_classifier_set_tuning(rtdm_classifier h, const char* key, int v
 
 rtdm_status rtdm_classifier_destroy(rtdm_classifier h) {
   return guard([&] { delete h; });
-    TuningScope ts_(h ? &h->tuning : nullptr);
 }
 
 rtdm_status rtdm_classifier_enable_timing(rtdm_classifier h, int max_calls) {
@@ -761,6 +760,27 @@ int64_t rtdm_classifier_describe(rtdm_classifier h, char* buf, int64_t buf_len) 
   std::string s = "classifier S " + std::to_string(h->S) + " dtype " +
                   (h->int8 ? "i8" : h->dtype == RTDM_F16 ? "f16" : "f32") + " max_batch " +
                   std::to_string(h->max_batch) + "\n";
+  {  // conv1 as classify() launches it on the transformed (NHWC) frames
+    ConvArgs a;
+    a.in_kind = IN_NHWC;
+    a.in_cs = 3;
+    a.n = 1;
+    a.ih = a.iw = h->S;
+    a.cin = 3;
+    a.ks = 3;
+    a.stride = 2;
+    a.pad = 0;
+    a.oh = a.ow = h->stem_oh;
+    a.cout = h->stem_cout;
+    conv_set_rows(a);
+    a.w = h->blob.at<void>(h->stem.w_off);
+    a.kpad = h->stem.kpad;
+    a.cout_pad = h->stem.cout_pad;
+    a.w_f32 = h->stem.mfma ? 0 : 1;
+    a.w_stem = h->blob.at<void>(h->stem.stem_off);
+    a.e.full = View{h->blob.at<void>(0), h->stem_cout, 0};  // (any non-null view: only its presence is read)
+    s += std::string("conv1 kernel ") + conv_kernel_name(a, h->dtype) + "\n";
+  }
   const bool chain = h->chain_start >= 0 && acff_chain_mode();
   for (int i = 0; i < (int)h->stages.size(); ++i) {
     const AcffStage& st = h->stages[i];

@@ -174,6 +174,19 @@ __device__ __forceinline__ void xcd_span(int bid, int nb, int ntiles, int& first
   step = (nb - x + 7) >> 3;
 }
 
+// Between an accumulation chain's MFMA of one opcode and its next link of ANOTHER opcode that
+// reads the first one's accumulator as SrcC (the stem's 16x16x32 -> 16x16x16 chain).  The
+// compiler's hazard model inserts no wait states for a full-register SrcC overlap whatever the
+// opcodes, and back to back the 16-deep link read a stale accumulator: NaN / wrong values in
+// round 4 (the swish stem, the channel-major stem).  sched_barrier keeps every chain's first
+// link before the fence and every second link after it (>= 1 independent MFMA in between),
+// and the s_nops add 16 wait states on top; this costs a few issue cycles per tile.
+__device__ __forceinline__ void mfma_opcode_switch() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7" ::);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // Tuning knobs (rtdm_set_tuning keys in api.cpp): kernel-choice / A/B switches and the
 // cost-model objectives.  default_tuning() holds the process defaults; a detector / classifier
 // handle copies them when it is created (rtdm_*_set_tuning changes its own copy), and every
@@ -182,19 +195,15 @@ __device__ __forceinline__ void xcd_span(int bid, int nb, int ntiles, int& first
 // (the calling thread's scope, else the defaults).
 struct Tuning {
   int conv_pipe = 1;        // conv_pipe mode (1 the kernels; 0 off; > 1 diagnostics, conv_pipe.hip)
-  int stem_abl = 0;         // conv_stem3 / conv_stem_pool2 ablations (diagnostics)
-  int stem_fuse = 0;        // pooled stem + the next 16 -> 32 pooled conv as one conv_stem_pool2 launch (1; off: measured slower, r04e)
+  int stem_abl = 0;         // conv_stem3 ablations (diagnostics)
   int head1x1 = 1;          // stand-alone YOLO head convs on head1x1_f16
   int pipe_bm = 0;          // conv_pipe tile rows: 0 cost model, else forced 256 / 128 / 64
-  int pipe_cost = 0;        // conv_pipe / conv_wide tile objective: 0 latency (rounds), 1 throughput (CU-time)
+  int pipe_cost = 0;        // conv_pipe tile objective: 0 latency (rounds), 1 throughput (CU-time)
   int pipe_korder = 1;      // conv_pipe K order: 0 tap outer, 1 channel-block outer
   int pipe_win = 1;         // conv_pipe window mode
   int pipe_pf = 1;          // conv_pipe cross-tile prologue prefetch
-  int pipe_pp = 0;          // conv_pipe ping-pong K-loop schedule
   int pipe_walk = 2;        // conv_pipe tile walk: N-panels per group (0 = M-major)
   int pipe_wloop = 1;       // conv_pipe tap-unrolled 3x3 K-loops
-  int pipe_wide = 0;        // conv_wide: 0 off (default: measured slower, r04b), 1 cost model, 2 all 256 x 256 tiles, 3 one round + 256 x 128 tail
-  int pipe_wide_eff = 115;  // conv_wide cost model: its K-loop rate per FLOP over conv_pipew's, x100
   int dw3_tile = 1;         // YOLO-ACFF depthwise on the LDS-tiled kernel (1) or the vector one (0)
   int resize_stream = 1;    // classifier preprocessing kernel
   int nms_variant = 0;      // NMS diagnostics
@@ -202,13 +211,10 @@ struct Tuning {
   int acff_chain = 1;       // acff_chain for the small-map suffix
   int fuse_head = 0;        // fused YOLO head convs (plan time; 0: the 3x3 on the unrolled window kernel + head1x1_f16, measured faster r04h)
   int two_streams = 1;      // detector head branches on a second stream (plan time)
-  int pipe_regpool = 0;     // conv_pipe register epilogue for pool / upsample layers too
   int pool_sep = 1;         // separable stride-1 max pools (K 5 / 9 / 13: the SPP block)
-  int pool_small32 = 0;     // Cin-32 conv3_pool_small layout: 0 one channel tile per wave, 1 two (4 waves), 2 two (8 waves)
   int pool_small64 = 1;     // conv3_pool_small for 3x3 Cin 64 -> 128 + pool (+ full map)
   int pool_small_pf = 0;    // conv3_pool_small halo tiles in flight per block (0 auto | 1 | 2)
   int stem_k16 = 1;         // pooled MFMA stem: the kh = 2 third of K as a 16-deep MFMA (0: 32-deep)
-  int stem_persist = 0;     // conv_stem3p for the pooled uint8 stem (measured slower r04u)
   int conv_c32 = 1;         // conv3_c32 for the Cin-32 3x3 convs (conv_c32.hip)
   int res_fuse = 1;         // conv3_c32r: Darknet-53's first residual block as one launch (1: 8 waves, 2: 4 waves)
 };
@@ -223,6 +229,9 @@ struct TuningScope {
 };
 // key -> knob (RTDM_E_INVALID on an unknown key)
 void tuning_set(Tuning& t, const char* key, int value);
+// keys read only when a detector handle is planned (fuse_head, two_streams): a created
+// handle refuses them (rtdm_detector_set_tuning), they apply through rtdm_set_tuning
+bool tuning_is_plan_time(const char* key);
 
 struct ConvArgs {
   const void* in = nullptr;
@@ -244,7 +253,7 @@ struct ConvArgs {
   int pipe_corder = 0;           // conv_pipe_f16: channel-block-outer K order (set by launch_conv_pipe)
   int pipe_g = 0;                // conv_pipe: N-panels per tile-walk group (0: M-major walk; set at launch)
   int pipe_u = 1;                // conv_pipe: tap-unrolled loop for the per-tap-load 3x3 layers (set at launch)
-  int pipe_t0 = 0;               // conv_pipe: first tile of the launch (the tail of a conv_wide split)
+  int pipe_t0 = 0;               // conv_pipe: first tile of the launch
   Epilogue e;
   // Fused YOLO head (conv_pipe_f16 only): a 1x1 conv over this conv's activated
   // output (cout <= 128 = one N tile), head_w fp16 [head_cout_pad][cout_pad] (k = c),
@@ -275,9 +284,6 @@ const char* head1x1_name(const ConvArgs& a);
 int conv_pipe_mode();
 int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 / 128 / 64)
 const char* conv_pipe_name(const ConvArgs& a);  // kernel symbol of that launch
-// stem_fused.hip: pooled stem (Cin 3 -> 16) + the 16 -> 32 3x3 pooled conv reading its map, one launch
-bool stem_pool2_ok(const ConvArgs& a0, const ConvArgs& a2);
-void launch_stem_pool2(const ConvArgs& a0, const ConvArgs& a2, int abl, hipStream_t s);
 // conv_c32.hip: persistent Cin-32 3x3 kernel (stride 1 / 2, Cout 64, optional residual)
 bool c32_ok(const ConvArgs& a);
 void launch_c32(const ConvArgs& a, hipStream_t s);
@@ -285,10 +291,6 @@ const char* c32_name(const ConvArgs& a);
 // ... and Darknet-53's first residual block (1x1 64 -> 32, 3x3 32 -> 64, shortcut) as one launch
 bool c32r_ok(const ConvArgs& a1, const ConvArgs& a);
 void launch_c32r(const ConvArgs& a1, const ConvArgs& a, hipStream_t s);
-// conv_wide.hip: 256 x 256-tile window-mode twin of conv_pipew for the big 3x3 / s1 layers
-bool conv_wide_ok(const ConvArgs& a, int abl);
-int64_t conv_wide_tiles(const ConvArgs& a);
-void launch_conv_wide(const ConvArgs& a, int abl, int ntiles, int cus, hipStream_t s);
 // int8 twin (RTDM_I8): a.in = quantised contiguous int8 copy of the input, a.w8 int8
 // weights (per-channel activation scales folded in), a.deq per-output-channel scales
 bool conv_pipe_i8_ok(const ConvArgs& a);

@@ -241,9 +241,14 @@ __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
 }
 
+// The kh = 2 third of K on one 16-deep MFMA (K16, the default): lane group g supplies the
+// pixel at kw = g (4 channels; kw = 3 meets zero weights), so K = 32 + 16 instead of 32 + 32
+// with lane groups 2, 3 re-reading kh = 2 pixels against zero weights — the same nonzero
+// products, bit-identical (tests/test_gpu_stem.py).  The 16-deep link reads the 32-deep
+// link's accumulator as SrcC; mfma_opcode_switch() keeps the two opcodes apart (see there).
 // ABL (diagnostic builds only, outputs wrong when non-zero): 1 = no frame loads,
 // 2 = no output stores, 4 = no MFMA.
-template <bool POOL, int NTN, int ABL = 0>
+template <bool POOL, int NTN, bool K16, int ABL = 0>
 __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LDS bound (<= 31 KB per block at 608); lets the compiler keep the fragment reads in flight
   extern __shared__ __attribute__((aligned(16))) uint2 stem_lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -366,13 +371,6 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
     return x * sc[t][j] + sh[t][j];
   };
   const int kh0 = g >> 1, pr0 = g & 1;
-  // ABL bit 8 (stem_k16, default; pooled stems only): the kh = 2 third of K as one 16-deep
-  // MFMA (lane group g = pixel kw = g, 4 channels; kw = 3 has zero weights) instead of a
-  // 32-deep one whose lanes g >= 2 re-read kh = 2 pixels against zero weights: the same
-  // nonzero products, bit-identical (tests/test_gpu_stem.py).  Launched for the lean pooled
-  // epilogue only: the channel-major plain stem and the swish pooled epilogue gave wrong
-  // results (NaN) with the same change, not yet understood, and keep the 32-deep MFMA.
-  constexpr bool K16 = (ABL & 8) != 0;
   typedef _Float16 h4s __attribute__((ext_vector_type(4)));
   h4s w16[NTN];
 #pragma unroll
@@ -421,24 +419,35 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
         }
         oq[u] = tx * 4 + g;  // pooled x of this lane's output quad
       }
+      f4 accs[NTN][2];
+      if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+        for (int t = 0; t < NTN; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            accs[t][u] = K16 ? f4{(float)bf0[u][0], (float)bf0[u][1], (float)bk[u][2], (float)bk[u][3]}
+                             : f4{(float)bf0[u][0], (float)bf0[u][1], (float)bf1[u][2], (float)bf1[u][3]};
+      } else {
+        // every chain's 32-deep link, then (K16) the fence, then every 16-deep link
+#pragma unroll
+        for (int t = 0; t < NTN; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            accs[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf0[u], wa[t][0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        if constexpr (K16) mfma_opcode_switch();
+#pragma unroll
+        for (int t = 0; t < NTN; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            if constexpr (K16)
+              accs[t][u] = __builtin_amdgcn_mfma_f32_16x16x16f16(bk[u], w16[t], accs[t][u], 0, 0, 0);
+            else
+              accs[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1[u], wa[t][1], accs[t][u], 0, 0, 0);
+          }
+      }
 #pragma unroll
       for (int t = 0; t < NTN; ++t) {
-        f4 acc[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if constexpr ((ABL & 4) != 0) {
-            if constexpr (K16)
-              acc[u] = f4{(float)bf0[u][0], (float)bf0[u][1], (float)bk[u][2], (float)bk[u][3]};
-            else
-              acc[u] = f4{(float)bf0[u][0], (float)bf0[u][1], (float)bf1[u][2], (float)bf1[u][3]};
-          } else {
-            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf0[u], wa[t][0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            if constexpr (K16)
-              acc[u] = __builtin_amdgcn_mfma_f32_16x16x16f16(bk[u], w16[t], acc[u], 0, 0, 0);
-            else
-              acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1[u], wa[t][1], acc[u], 0, 0, 0);
-          }
-        }
+        const f4* acc = accs[t];
         const int c = 16 * t + p;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -475,15 +484,32 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
       const uint2* rowk0 = stem_lds + (tr * s + kh0) * ls;
       const uint2* rowk2 = stem_lds + (tr * s + 2) * ls;
       const uint2 b00 = rowk0[lx + 2 * pr0], b01 = rowk0[lx + 2 * pr0 + 1];
-      uint2 b10 = rowk2[lx + 2 * (g & 1)], b11 = rowk2[lx + 2 * (g & 1) + 1];
-      if (g >= 2) b10 = b11 = make_uint2(0u, 0u);
       const h8 bf0 = __builtin_bit_cast(h8, (u32x4{b00.x, b00.y, b01.x, b01.y}));
-      const h8 bf1 = __builtin_bit_cast(h8, (u32x4{b10.x, b10.y, b11.x, b11.y}));
+      h8 bf1;
+      h4s bk;
+      if constexpr (K16) {
+        bk = __builtin_bit_cast(h4s, rowk2[lx + g]);  // kw = g (kw = 3: zero weights, staged pixel)
+      } else {
+        uint2 b10 = rowk2[lx + 2 * (g & 1)], b11 = rowk2[lx + 2 * (g & 1) + 1];
+        if (g >= 2) b10 = b11 = make_uint2(0u, 0u);
+        bf1 = __builtin_bit_cast(h8, (u32x4{b10.x, b10.y, b11.x, b11.y}));
+      }
       const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
+      f4 accs[NTN];
+#pragma unroll
+      for (int tt = 0; tt < NTN; ++tt)
+        accs[tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[tt][0], bf0, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      if constexpr (K16) mfma_opcode_switch();
 #pragma unroll
       for (int tt = 0; tt < NTN; ++tt) {
-        f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[tt][0], bf0, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[tt][1], bf1, acc, 0, 0, 0);
+        if constexpr (K16)
+          accs[tt] = __builtin_amdgcn_mfma_f32_16x16x16f16(w16[tt], bk, accs[tt], 0, 0, 0);
+        else
+          accs[tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[tt][1], bf1, accs[tt], 0, 0, 0);
+      }
+#pragma unroll
+      for (int tt = 0; tt < NTN; ++tt) {
+        const f4 acc = accs[tt];
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = epi(acc[j], tt, j);
@@ -501,140 +527,6 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
       }
     }
   }
-}
-
-// Persistent twin of conv_stem3<true> for uint8 frames with the lean epilogue (the Darknet
-// stem of the detector of record): a block walks row bands (xcd_span: the bands of one XCD
-// are contiguous, so neighbours' halo rows meet in its L2) and keeps the NEXT band's raw
-// frame bytes in flight in registers while the current band's MFMAs and stores run.
-// conv_stem3 stages a band, computes it and exits, so each block's loads wait with nothing
-// else to do and a CU had ~30 KB of frame reads in flight on average (2.5 TB/s at b64 608).
-// Per band the same staging (4 pixels = 12 bytes per item, fp16 4-channel LDS pixels),
-// the same MFMAs and the same pooled epilogue as conv_stem3<true>: bit-identical.
-// Eligible: stem_p_ok (items of a band <= 4 per thread, W % 4 == 0, cols >= W + 1, 16 channels).
-template <int NTN>
-__global__ __launch_bounds__(256, 5) void conv_stem3p(ConvArgs a, int nbands) {
-  extern __shared__ __attribute__((aligned(16))) uint2 stem_lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int s = a.stride, pad = a.pad;
-  constexpr int ROWS = kStemRowsPool;
-  const int bpi = (a.oh + ROWS - 1) / ROWS;
-  const int nrows = (ROWS - 1) * s + 3;
-  const int cols = (a.ow - 1) * s - pad + 5;
-  const int ls = cols + stem_xcols(true, s);
-  const int H = a.ih, W = a.iw;
-  const int gpr = W >> 2;  // 4-pixel groups per row
-  const int items = nrows * gpr;
-  // this thread's staging items (k = 0..3: item tid + 256 k): LDS row / group, fixed per band
-  int ir[4], ig[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i = tid + 256 * k;
-    ir[k] = i < items ? i / gpr : -1;
-    ig[k] = i < items ? i - (i / gpr) * gpr : 0;
-  }
-  uint32_t d[4][3];
-  auto fetch = [&](int band) {
-    const int n = band / bpi, iy0 = (band - n * bpi) * ROWS * s - pad;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      d[k][0] = d[k][1] = d[k][2] = 0u;
-      const int y = iy0 + ir[k];
-      if (ir[k] >= 0 && (unsigned)y < (unsigned)H) {
-        const uint32_t* src = (const uint32_t*)((const uint8_t*)a.in + ((size_t)(n * H + y) * W + 4 * ig[k]) * 3);
-        d[k][0] = src[0];
-        d[k][1] = src[1];
-        d[k][2] = src[2];
-      }
-    }
-  };
-  // padding columns (LDS column 0 and W+1 .. cols-1): zero for every band
-  {
-    const int npad = cols - W;
-    for (int idx = tid; idx < nrows * npad; idx += 256) {
-      const int r = idx / npad, k = idx - r * npad;
-      stem_lds[r * ls + (k == 0 ? 0 : W + k)] = make_uint2(0u, 0u);
-    }
-  }
-  const int p = lane & 15, g = lane >> 4;
-  const Epilogue& e = a.e;
-  h8 wa[NTN][2];
-  float bias[NTN];
-#pragma unroll
-  for (int t = 0; t < NTN; ++t) {
-    const _Float16* wp = (const _Float16*)a.w_stem + (size_t)(16 * t + p) * 64 + 8 * g;
-    wa[t][0] = *(const h8*)wp;
-    wa[t][1] = *(const h8*)(wp + 32);
-    const int c = 16 * t + p;
-    bias[t] = (e.bias && c < a.cout) ? e.bias[c] : 0.f;
-  }
-  const float slp = e.act == ACT_LEAKY ? e.slope : 1.f;
-  const int qw = a.ow >> 1, qh = a.oh >> 1;
-  const int kh0 = g >> 1, pr0 = g & 1;
-  const int tr = wid >> 1, d4 = p & 3;
-  const int ly = 2 * tr + (d4 >> 1);
-  const int lx0 = (2 * ((wid & 1) * 4 + (p >> 2)) + (d4 & 1)) * s - pad + 1;
-  const uint2* rk0 = stem_lds + (ly * s + kh0) * ls + lx0 + 2 * pr0;
-  const uint2* rk2 = stem_lds + (ly * s + 2) * ls + lx0 + 2 * (g & 1);
-
-  int band, bend, bstep;
-  xcd_span(blockIdx.x, gridDim.x, nbands, band, bend, bstep);
-  if (band < bend) fetch(band);
-  for (; band < bend; band += bstep) {
-    __syncthreads();  // every wave is done with the previous band's LDS rows
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (ir[k] < 0) continue;
-      const uint32_t d0 = d[k][0], d1 = d[k][1], d2 = d[k][2];
-      const uint32_t b[12] = {d0 & 255u, (d0 >> 8) & 255u, (d0 >> 16) & 255u, d0 >> 24,
-                              d1 & 255u, (d1 >> 8) & 255u, (d1 >> 16) & 255u, d1 >> 24,
-                              d2 & 255u, (d2 >> 8) & 255u, (d2 >> 16) & 255u, d2 >> 24};
-      uint2* dst = stem_lds + ir[k] * ls + 4 * ig[k] + 1;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        dst[q] = make_uint2(pack_h2((float)b[3 * q], (float)b[3 * q + 1]), pack_h2((float)b[3 * q + 2], 0.f));
-    }
-    __syncthreads();
-    if (band + bstep < bend) fetch(band + bstep);  // in flight during this band's MFMAs
-    const int n = band / bpi, oy0 = (band - n * bpi) * ROWS;
-    const int py = (oy0 >> 1) + tr;
-    if (py >= qh) continue;
-    _Float16* pool_row = (_Float16*)e.pool.ptr + ((size_t)n * qh + py) * qw * e.pool.cs + e.pool.co;
-    for (int tx0 = wid & 1, off = 0; tx0 * 4 < qw; tx0 += 4, off += 32 * s) {
-      h8 bf0[2], bf1[2];
-      int oq[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int tx = tx0 + 2 * u, o = off + u * 16 * s;
-        const uint2 b00 = rk0[o], b01 = rk0[o + 1];
-        const uint2 b10 = rk2[o], b11 = rk2[o + 1];
-        bf0[u] = __builtin_bit_cast(h8, (u32x4{b00.x, b00.y, b01.x, b01.y}));
-        bf1[u] = __builtin_bit_cast(h8, (u32x4{b10.x, b10.y, b11.x, b11.y}));
-        oq[u] = tx * 4 + g;
-      }
-#pragma unroll
-      for (int t = 0; t < NTN; ++t) {
-        const int c = 16 * t + p;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf0[u], wa[t][0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf1[u], wa[t][1], acc, 0, 0, 0);
-          const float x = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) * (1.f / 255.f) + bias[t];
-          const float m = fmaxf(x, x * slp) + 0.f;  // conv_stem3's lean pooled epilogue
-          if (oq[u] < qw && c < a.cout) pool_row[(size_t)oq[u] * e.pool.cs + c] = (_Float16)m;
-        }
-      }
-    }
-  }
-}
-
-static bool stem_p_ok(const ConvArgs& a) {
-  // (16 output channels: the 2- and 4-tile instantiations spill under the 5-block bound)
-  if (!tune().stem_persist || a.in_kind != IN_FRAME_U8 || !a.quad || (a.iw & 3) || a.cout_pad != 16) return false;
-  const int s = a.stride, nrows = (kStemRowsPool - 1) * s + 3, cols = (a.ow - 1) * s - a.pad + 5;
-  if (cols < a.iw + 1 || nrows * (a.iw >> 2) > 4 * 256) return false;
-  const Epilogue& e = a.e;
-  return !e.scale && e.act != ACT_SWISH && (e.act != ACT_LEAKY || (e.slope > 0.f && e.slope <= 1.f));
 }
 
 static size_t stem3_lds_bytes(const ConvArgs& a) {
@@ -1540,14 +1432,6 @@ static void launch_pool_small(const ConvArgs& a, hipStream_t s) {
       hipLaunchKernelGGL((conv3_pool_small<16, 32, 16, 4, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((conv3_pool_small<16, 32, 16, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-  } else if (tune().pool_small32 == 1) {  // two channel tiles per wave, 4 waves (half the B reads)
-    static const int per_cu = resident_blocks(conv3_pool_small<32, 64, 8, 4, 2>, 256, 0);
-    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cu_count());
-    hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-  } else if (tune().pool_small32 == 2) {  // two channel tiles per wave, 8 waves
-    static const int per_cu = resident_blocks(conv3_pool_small<32, 64, 8, 2, 2, 1, 8>, 512, 0);
-    const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cu_count());
-    hipLaunchKernelGGL((conv3_pool_small<32, 64, 8, 2, 2, 1, 8>), dim3((unsigned)blocks), dim3(512), 0, s, a);
   } else {
     static const int per_cu = resident_blocks(conv3_pool_small<32, 64, 8, 8, 1>, 256, 0);
     static const int per_cu2 = resident_blocks(conv3_pool_small<32, 64, 8, 8, 1, 2>, 256, 0);
@@ -1650,18 +1534,18 @@ static bool use_pipe(const ConvArgs& a, int dtype) {
 
 const char* conv_kernel_name(const ConvArgs& a, int dtype) {
   if (dtype == RTDM_F16 && stem_ok(a)) {
-    static const char* names[2][3] = {{"conv_stem3<false,1>", "conv_stem3<false,2>", "conv_stem3<false,4>"},
-                                      {"conv_stem3<true,1>", "conv_stem3<true,2>", "conv_stem3<true,4>"}};
+    static const char* names[2][2][3] = {
+        {{"conv_stem3<false,1>", "conv_stem3<false,2>", "conv_stem3<false,4>"},
+         {"conv_stem3<true,1>", "conv_stem3<true,2>", "conv_stem3<true,4>"}},
+        {{"conv_stem3<false,1,k16>", "conv_stem3<false,2,k16>", "conv_stem3<false,4,k16>"},
+         {"conv_stem3<true,1,k16>", "conv_stem3<true,2,k16>", "conv_stem3<true,4,k16>"}}};
     const int ntn = a.cout_pad / 16;
-    if (a.quad && stem_abl() == 0 && stem_p_ok(a)) return "conv_stem3p<1>";
-    return names[a.quad ? 1 : 0][ntn == 1 ? 0 : ntn == 2 ? 1 : 2];
+    return names[tune().stem_k16 ? 1 : 0][a.quad ? 1 : 0][ntn == 1 ? 0 : ntn == 2 ? 1 : 2];
   }
   if (dtype == RTDM_F16 && pool_small_ok(a))
     return a.cin == 16   ? "conv3_pool_small<16,32,16,4,2>"
            : a.cin == 64 ? "conv3_pool_small<64,128,8,4,2,1,8>"
-           : tune().pool_small32 == 1 ? "conv3_pool_small<32,64,8,4,2>"
-           : tune().pool_small32 == 2 ? "conv3_pool_small<32,64,8,2,2,1,8>"
-                                      : "conv3_pool_small<32,64,8,8,1>";
+                         : "conv3_pool_small<32,64,8,8,1>";
   if (dtype == RTDM_F16 && c32_ok(a)) return c32_name(a);
   if (dtype == RTDM_F16 && direct_ok(a)) {
     const int bn = direct_cfg(a.cout_pad).bn;
@@ -1694,26 +1578,26 @@ void launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
     const int blocks = a.n * ((a.oh + rows - 1) / rows);
     const size_t lds = stem3_lds_bytes(a);
     const int ntn = a.cout_pad / 16;
-    if (a.quad && stem_abl() == 0 && stem_p_ok(a)) {
-      const int nbands = a.n * ((a.oh + kStemRowsPool - 1) / kStemRowsPool);
-      const int grid = std::min(nbands, resident_blocks(conv_stem3p<1>, 256, lds) * cu_count());
-      hipLaunchKernelGGL((conv_stem3p<1>), dim3(grid), dim3(256), lds, s, a, nbands);
-    } else if (a.quad) {
-      const int abl = stem_abl();
-      if (ntn == 1 && abl == 1) hipLaunchKernelGGL((conv_stem3<true, 1, 1>), dim3(blocks), dim3(256), lds, s, a);
-      else if (ntn == 1 && abl == 2) hipLaunchKernelGGL((conv_stem3<true, 1, 2>), dim3(blocks), dim3(256), lds, s, a);
-      else if (ntn == 1 && abl == 4) hipLaunchKernelGGL((conv_stem3<true, 1, 4>), dim3(blocks), dim3(256), lds, s, a);
-      else if (ntn == 1 && abl == 7) hipLaunchKernelGGL((conv_stem3<true, 1, 7>), dim3(blocks), dim3(256), lds, s, a);
-      else if (ntn == 1 && tune().stem_k16 && !a.e.scale && a.e.act != ACT_SWISH &&
-               (a.e.act != ACT_LEAKY || (a.e.slope > 0.f && a.e.slope <= 1.f)))  // the lean epilogue only
-        hipLaunchKernelGGL((conv_stem3<true, 1, 8>), dim3(blocks), dim3(256), lds, s, a);
-      else if (ntn == 1) hipLaunchKernelGGL((conv_stem3<true, 1>), dim3(blocks), dim3(256), lds, s, a);
-      else if (ntn == 2) hipLaunchKernelGGL((conv_stem3<true, 2>), dim3(blocks), dim3(256), lds, s, a);
-      else hipLaunchKernelGGL((conv_stem3<true, 4>), dim3(blocks), dim3(256), lds, s, a);
+    const int abl = stem_abl();
+    const bool k16 = tune().stem_k16 != 0;
+    if (a.quad && abl) {  // diagnostic ablation builds (tools/ab_conv.py --key stem_abl)
+      RTDM_REQUIRE(ntn == 1 && k16 && (abl == 1 || abl == 2 || abl == 4 || abl == 7), RTDM_E_INVALID,
+                   "stem_abl: 1 | 2 | 4 | 7 on the 16-channel K16 pooled stem");
+      if (abl == 1) hipLaunchKernelGGL((conv_stem3<true, 1, true, 1>), dim3(blocks), dim3(256), lds, s, a);
+      else if (abl == 2) hipLaunchKernelGGL((conv_stem3<true, 1, true, 2>), dim3(blocks), dim3(256), lds, s, a);
+      else if (abl == 4) hipLaunchKernelGGL((conv_stem3<true, 1, true, 4>), dim3(blocks), dim3(256), lds, s, a);
+      else hipLaunchKernelGGL((conv_stem3<true, 1, true, 7>), dim3(blocks), dim3(256), lds, s, a);
     } else {
-      if (ntn == 1) hipLaunchKernelGGL((conv_stem3<false, 1>), dim3(blocks), dim3(256), lds, s, a);
-      else if (ntn == 2) hipLaunchKernelGGL((conv_stem3<false, 2>), dim3(blocks), dim3(256), lds, s, a);
-      else hipLaunchKernelGGL((conv_stem3<false, 4>), dim3(blocks), dim3(256), lds, s, a);
+      auto go = [&](auto pool_c, auto k16_c) {
+        constexpr bool P = decltype(pool_c)::value, K = decltype(k16_c)::value;
+        if (ntn == 1) hipLaunchKernelGGL((conv_stem3<P, 1, K>), dim3(blocks), dim3(256), lds, s, a);
+        else if (ntn == 2) hipLaunchKernelGGL((conv_stem3<P, 2, K>), dim3(blocks), dim3(256), lds, s, a);
+        else hipLaunchKernelGGL((conv_stem3<P, 4, K>), dim3(blocks), dim3(256), lds, s, a);
+      };
+      if (a.quad && k16) go(std::true_type{}, std::true_type{});
+      else if (a.quad) go(std::true_type{}, std::false_type{});
+      else if (k16) go(std::false_type{}, std::true_type{});
+      else go(std::false_type{}, std::false_type{});
     }
   } else if (dtype == RTDM_F16 && pool_small_ok(a)) {
     launch_pool_small(a, s);

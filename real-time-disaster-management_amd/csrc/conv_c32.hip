@@ -385,6 +385,7 @@ void launch_c32r(const ConvArgs& a1, const ConvArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(conv3_c32r<4>, grid, dim3(256), kC32rLDS, s, a1, a, nt);
   else
     hipLaunchKernelGGL(conv3_c32r<8>, grid, dim3(512), kC32rLDS, s, a1, a, nt);
+  RTDM_HIP(hipGetLastError());
 }
 
 const char* c32_name(const ConvArgs& a) {
@@ -401,6 +402,7 @@ static void launch_c32_t(const ConvArgs& a, int ntiles, hipStream_t s) {
   const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / C32Geom<S>::LDS);
   const int grid = std::min(ntiles, cus * per_cu);
   hipLaunchKernelGGL((conv3_c32<S, RES>), dim3(grid), dim3(256), C32Geom<S>::LDS, s, a, ntiles);
+  RTDM_HIP(hipGetLastError());
 }
 
 void launch_c32(const ConvArgs& a, hipStream_t s) {

@@ -171,14 +171,12 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // per 16x16 block, with the 2x2 pool as two DPP max steps over quad-order rows: no
   // fp32 C tile through LDS and no barrier between the K-loop and the stores.
   constexpr bool REG = (ABL & 512) != 0;
-  // ABL bit 2048: ping-pong schedule (see the PP loop below)
-  constexpr bool PP = (ABL & 2048) != 0;
   // window mode with the taps unrolled (see the WLOOP loop below); ABL bit 4096 selects the
   // generic cursor loop instead (A/B diagnostics)
-  constexpr bool WLOOP = WIN && !PP && !(ABL & 4096);
+  constexpr bool WLOOP = WIN && !(ABL & 4096);
   // the same tap-unrolled loop for the per-tap-load (non-window) 3x3 layers (channel-block-outer
   // K order), chosen at run time; 1x1 layers keep the generic cursor loop
-  constexpr bool ULOOP = !PP && !(ABL & 4096) && !(ABL & 32);
+  constexpr bool ULOOP = !(ABL & 4096) && !(ABL & 32);
   const bool uloop = ULOOP && (WIN || (a.ks == 3 && a.pipe_corder != 0 && a.pipe_u != 0));
   constexpr bool RES_ = (ABL & 256) != 0;
   // cross-tile prefetch (pf, register epilogue only: the LDS ring is free during it)
@@ -537,7 +535,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // epilogue, whose exactly EPI vector-memory ops are younger than K-block NSt-2)
   if constexpr (WLOOP)
     waddr(std::integral_constant<int, 0>{}, 0);
-  else if constexpr (WIN && !PP)
+  else if constexpr (WIN)
     win_addr();
   // the tile cursor past the prologue's NSt-1 K-blocks (issued here or by the previous tile)
   auto skip_prologue = [&]() {
@@ -550,9 +548,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
       st_buf = st_buf == NSt - 1 ? 0 : st_buf + 1;
     }
   };
-  if (PP) {
-    // (the ping-pong loop below issues its own prologue)
-  } else if (PF && pre) {
+  if (PF && pre) {
     skip_prologue();
     // (fused head: its io stores are per-lane conditional, so younger than K-block NSt-2
     // only a lower bound of them: none — the wait also covers them)
@@ -568,14 +564,12 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     for (int i = 0; i < nk; ++i) stage();
     wait_vm_lgkm0<0>();
   }
-  if constexpr (!PP) {
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (WLOOP)
-      wread0(std::integral_constant<int, 0>{});
-    else
-      read0(0);
-  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (WLOOP)
+    wread0(std::integral_constant<int, 0>{});
+  else
+    read0(0);
 
   // Cluster A (half 0 of kb): MFMAs on fa0/fb0, interleaved with the reads of half 1
   // (fa1/fb1) and the buffer->LDS loads of kb+NSt-1.  Cluster B (half 1): MFMAs on
@@ -772,91 +766,11 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
           wbody(t_, std::bool_constant<(T <= 6)>{}, F_{}, std::bool_constant<(T <= 7)>{}, cb);
         },
         std::make_integer_sequence<int, 9>{});
-  } else if constexpr (!(ABL & 32) && !PP && !WLOOP) {
+  } else if constexpr (!(ABL & 32) && !WLOOP) {
     int kb = 0;
     for (; kb + NSt - 1 < nk; ++kb) body(T_{}, T_{});  // stages kb + NSt - 1
     for (; kb + 1 < nk; ++kb) body(F_{}, T_{});        // tail: nothing left to stage (waits vmcnt(0))
     body(F_{}, F_{});
-  }
-  // ---- ping-pong schedule (PP): the 8 waves are two groups of 4 -- group 0 = waves 0-3
-  //      (output rows 0 .. BM/2-1), group 1 = waves 4-7 (rows BM/2 ..), one wave of each
-  //      on every SIMD.  Every wave runs the same sequence -- a memory phase (its share of a
-  //      ring stage's LDS-DMA loads, the next K-block's fragment reads and addresses), then
-  //      an MFMA phase (all 32 MFMAs of that K-block, operands already in registers),
-  //      phases separated by workgroup barriers -- but group 1 runs one phase behind group
-  //      0, so in every phase each SIMD's matrix pipe has one wave issuing MFMAs back to
-  //      back while its partner feeds the next K-block (instead of both waves of a SIMD
-  //      meeting the same barrier, DMA wait and read latency together).  The memory phase
-  //      after K-block k's MFMAs issues stage k+3 (into k's ring slot: both groups have
-  //      read k by then) and reads K-block k+1; before each barrier a wave retires its ops
-  //      of the stage the next phase may read (the one after that stays in flight).
-  //      The loop body has no group-dependent branch, so the accumulators stay in one
-  //      register set.  Per accumulator the MFMA order is unchanged (K-blocks in order,
-  //      half 0 then half 1): bit-identical to the other schedule.
-  if constexpr (PP && !(ABL & 32)) {
-    const bool grp1 = wid >= WAVES / 2;
-    auto mfma_all = [&]() {
-#pragma unroll
-      for (int tm = 0; tm < FM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < FN; ++tn) acc[tm][tn] = mfma(fa0[tm], fb0[tn], acc[tm][tn]);
-#pragma unroll
-      for (int tm = 0; tm < FM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < FN; ++tn) acc[tm][tn] = mfma(fa1[tm], fb1[tn], acc[tm][tn]);
-    };
-    auto read_kb = [&](int buf) {  // both halves of one K-block's fragments
-      if constexpr (WIN) win_addr();
-      if constexpr (!(ABL & 2)) {
-        read0(buf);
-        read1(buf);
-      }
-    };
-    int ns = 0;  // ring stages issued by this wave
-    auto issue = [&]() {
-      if constexpr (!(ABL & 1)) stage();
-      ++ns;
-    };
-    // retire this wave's ops of stage `need` (and older); a younger issued stage stays in flight
-    auto wait_need = [&](int need) {
-      need = need < nk - 1 ? need : nk - 1;
-      if (ns - 1 > need)
-        wait_vmn_lgkm0<VM>();
-      else
-        wait_vmn_lgkm0<0>();
-    };
-    auto phase_end = [&]() {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    // prologue: (window mode: channel block 0's window,) stages 0 and 1
-    if constexpr (WIN) {
-      for (int j = 0; 64 * j < wr; ++j) win_op(G0, j, 0, true);
-    }
-    if (nk > 0) issue();
-    if (nk > 1) issue();
-    wait_need(0);
-    phase_end();
-    if (grp1) phase_end();  // group 1: one phase behind
-    // memory phase before K-block 0: stage 2, K-block 0's fragments
-    if (ns < nk) issue();
-    read_kb(0);
-    wait_need(1);
-    phase_end();
-    int cur = 0;
-    for (int m = 0; m < nk; ++m) {
-      const int nxt = cur == NSt - 1 ? 0 : cur + 1;
-      mfma_all();
-      wait_need(m + 1);
-      phase_end();
-      if (ns < nk) issue();  // stage m + 3
-      if (m + 1 < nk) read_kb(nxt);
-      wait_need(m + 2);
-      phase_end();
-      cur = nxt;
-    }
-    if (!grp1) phase_end();  // the barrier count of group 1
   }
   if constexpr (REG) {
     if (pf) {
@@ -1080,7 +994,7 @@ __device__ __forceinline__ int pipe_tile_map(const ConvArgs& a, int t, int ntile
 
 template <int ABL, int BM, bool I8, bool WIN>
 __device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem_raw, int ntiles, bool pf) {
-  // tiles [a.pipe_t0, ntiles) (pipe_t0 > 0: the 256 x 128 tail of a conv_wide split)
+  // tiles [a.pipe_t0, ntiles)
   const int nb = gridDim.x, xcd = blockIdx.x & 7, l = blockIdx.x >> 3;
   const int cnt = ntiles - a.pipe_t0;
   const int q = cnt >> 3, r = cnt & 7;
@@ -1097,7 +1011,7 @@ __device__ __forceinline__ void pipe_walk(const ConvArgs& a, unsigned char* smem
   bool pre = false;
   for (int t = lo + l; t < hi; t += bx) {
     const int nx = pf && t + bx < hi ? pipe_tile_map(a, t + bx, ntiles) : -1;
-    pipe_tile<ABL, BM, I8, WIN>(a, smem_raw, pipe_tile_map(a, t, ntiles), pf && !(ABL & 2048), nx, pre);
+    pipe_tile<ABL, BM, I8, WIN>(a, smem_raw, pipe_tile_map(a, t, ntiles), pf, nx, pre);
     pre = nx >= 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1183,9 +1097,9 @@ static int pipe_bm_nk(const ConvArgs& a, int nk, double* est) {
   // 256-row tiles of window-mode layers run the tap-unrolled window loop: ~1.2x the K-loop
   // rate of the per-tap-load 256-row tiles (b64 L10 / L14 on 256-row window tiles 0.0614 /
   // 0.0682 ms against 0.0664 / 0.0710 on the 128-row tiles this model picked without it, r03ak)
-  // (only when that launch will run the unrolled window loop: register-epilogue layers, no
-  // ping-pong; the LDS-epilogue window layers run the cursor loop, launch_abl_w0)
-  const double eff[3] = {!head && pipe_win_ok(a, 256) && pipe_unroll(pipe_abl(a)) && !tune().pipe_pp ? 1.2 : 1.0, 0.85,
+  // (only when that launch will run the unrolled window loop: register-epilogue layers; the
+  // LDS-epilogue window layers run the cursor loop, launch_abl_w0)
+  const double eff[3] = {!head && pipe_win_ok(a, 256) && pipe_unroll(pipe_abl(a)) ? 1.2 : 1.0, 0.85,
                          0.65};
   const double ovh = 3.0 + (head ? 4.0 : 0.0);
   int best = 256;
@@ -1212,9 +1126,9 @@ static int g_pipe_korder_get() { return tune().pipe_korder; }
 static int pipe_abl(const ConvArgs& a) {
   if (a.head_w) return 8;
   if (epi_io_ok(a)) return 1024;
-  // (pool / upsample layers: the LDS C tile unless rtdm_set_tuning("pipe_regpool", 1) — the
-  // register epilogue pools the quad-ordered rows across lane quads by DPP)
-  const int reg = (!a.e.pool.ptr && !a.e.up.ptr) || tune().pipe_regpool ? 512 : 0;
+  // (pool / upsample layers: the LDS C tile; the register epilogue, which pools the
+  // quad-ordered rows across lane quads by DPP, measured slower there: r02cg, r04r)
+  const int reg = !a.e.pool.ptr && !a.e.up.ptr ? 512 : 0;
   if (epi_lean_ok(a)) return 128 | reg;
   if (epi_lean_ok(a, true)) return 384 | reg;
   return 0;
@@ -1237,8 +1151,6 @@ static bool pipe_win_ok(const ConvArgs& a, int bm) {
 // front of them.  Needs nk >= NSt - 1 and byte offsets of the output / residual views
 // below 2^31 - 16 (the epilogue's fixed-count buffer ops).  rtdm_set_tuning("conv_pipe_pf", 0)
 // turns it off (bit-identical either way).
-// Ping-pong schedule (ABL bit 2048, f16 only): rtdm_set_tuning("conv_pipe_pp", 1) turns it
-// on (bit-identical either way; measured slower, so off by default).
 
 // Tile walk (pipe_tile_map): N-panels per group; 0 = the M-major walk.  rtdm_set_tuning(
 // "conv_pipe_walk", g).  Bit-identical for every g (only the order tiles run in changes).
@@ -1259,7 +1171,7 @@ static int pipe_walk_g(const ConvArgs& a) {
 }
 
 static bool pipe_pf_ok(const ConvArgs& a, int abl, int nk) {
-  if (!tune().pipe_pf || nk < kPNS - 1 || (abl & 2048)) return false;
+  if (!tune().pipe_pf || nk < kPNS - 1) return false;
   if (abl == 8) return true;  // fused head: prefetch after the head GEMM, before the decode
   if (!(abl & 512) || !a.e.full.ptr || a.e.pool.ptr || a.e.up.ptr || a.e.scale) return false;
   const int64_t pix = (int64_t)a.n * a.oh * a.ow;
@@ -1267,50 +1179,6 @@ static bool pipe_pf_ok(const ConvArgs& a, int abl, int nk) {
   if ((pix * a.e.full.cs) * 2 >= lim) return false;
   if (a.e.res.ptr && (pix * a.e.res.cs) * 2 >= lim) return false;
   return true;
-}
-
-// conv_wide (conv_wide.hip): 256 x 256 tiles for the window-mode register-epilogue layers.
-// A wide tile is two 256 x 128 tiles' work; it runs them at wide_eff x the K-loop rate (64 x 128
-// per wave: 3/4 of the LDS read bytes, half the barriers and 5/6 of the LDS-DMA ops per FLOP),
-// but there are half as many, so a launch of U wide tiles over the CUs quantises twice as coarsely.
-// Options, in the units of pipe_bm_nk (latency objective: rounds of tiles over the CUs; throughput
-// objective: CU-time):
-//   * the best conv_pipe tiling alone (pipe_bm_nk);
-//   * all wide tiles;
-//   * split: whole rounds of wide tiles, then the remaining wide units as 256 x 128 conv_pipew
-//     tiles (twice as many, so they fill the last round twice as evenly) in a second launch.
-// Returns the wide tiles of the first launch (0: conv_pipe alone); *split: a tail follows.
-// rtdm_set_tuning("conv_wide", 0 off | 1 model | 2 all wide | 3 split), ("conv_wide_eff", x100).
-static int wide_plan(const ConvArgs& a, bool* split) {
-  *split = false;
-  if (!tune().pipe_wide || tune().pipe_pp || conv_pipe_mode() != 1 || a.head_w || !conv_wide_ok(a, pipe_abl(a))) return 0;
-  const int64_t U = conv_wide_tiles(a);
-  const int cus = pipe_cus();
-  const bool can_split = a.cout_pad % 256 == 0 && U > cus;  // tail tile t = 2 x its wide unit
-  if (tune().pipe_wide == 2 || tune().pipe_wide >= 10) return (int)U;  // (>= 10: all wide, diagnostic ablations)
-  if (tune().pipe_wide == 3) {
-    *split = can_split;
-    return can_split ? (int)(U / cus) * cus : (int)U;
-  }
-  const int nk = a.kpad / kPBK;
-  double small = 0.0;
-  pipe_bm_nk(a, nk, &small);  // the best conv_pipe tiling (window credit included)
-  const double ovh = 3.0;
-  const double ts = nk / 1.2 + ovh + 1.0;                                     // a 256 x 128 window tile
-  const double tw = 2.0 * nk / (1.2 * tune().pipe_wide_eff / 100.0) + 2.0 * ovh + 1.0;  // a 256 x 256 tile
-  auto rounds = [&](int64_t t) { return tune().pipe_cost ? (double)t : (double)((t + cus - 1) / cus); };
-  const double all = rounds(U) * tw;
-  double sp = 1e300;
-  if (can_split && !tune().pipe_cost) {
-    const int64_t full = U / cus, rem = U - full * cus;
-    sp = full * tw + rounds(2 * rem) * ts;
-  }
-  if (std::min(all, sp) >= small * 0.97) return 0;
-  if (sp < all) {
-    *split = true;
-    return (int)((U / cus) * cus);
-  }
-  return (int)U;
 }
 
 #define RTDM_PIPE_KERNEL(NAME)                                                                  \
@@ -1326,23 +1194,9 @@ RTDM_PIPE_KERNEL(conv_pipe_i8)
 RTDM_PIPE_KERNEL(conv_pipew_i8)
 #undef RTDM_PIPE_KERNEL
 
-template <template <int, int> class K, int BM, bool WITH_PP = false>
+template <template <int, int> class K, int BM>
 static void launch_abl(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int nt, int pf) {
-  if constexpr (WITH_PP) {
-    switch (abl) {
-      case 8 | 2048:
-        if constexpr (BM >= 128) K<8 | 2048, BM>::go(g, s, a, nt, pf);
-        return;
-      case 128 | 2048: K<128 | 2048, BM>::go(g, s, a, nt, pf); return;
-      case 384 | 2048: K<384 | 2048, BM>::go(g, s, a, nt, pf); return;
-      case 640 | 2048: K<640 | 2048, BM>::go(g, s, a, nt, pf); return;
-      case 896 | 2048: K<896 | 2048, BM>::go(g, s, a, nt, pf); return;
-      case 1024 | 2048: K<1024 | 2048, BM>::go(g, s, a, nt, pf); return;
-      case 2048: K<2048, BM>::go(g, s, a, nt, pf); return;
-      default: break;
-    }
-  }
-  switch (abl & ~2048) {
+  switch (abl) {
     case 8:
       if constexpr (BM >= 128) K<8, BM>::go(g, s, a, nt, pf);
       break;
@@ -1373,44 +1227,33 @@ static void launch_abl_w0(int abl, dim3 g, hipStream_t s, const ConvArgs& a, int
 
 template <int BM>
 static void launch_pipe_bm(const ConvArgs& a, hipStream_t s, int ntiles, dim3 grid, bool win) {
-  const int abl = pipe_abl(a) | (tune().pipe_pp ? 2048 : 0), pf = pipe_pf_ok(a, abl, a.kpad / kPBK) ? 1 : 0;
+  const int abl = pipe_abl(a), pf = pipe_pf_ok(a, abl, a.kpad / kPBK) ? 1 : 0;
   if constexpr (BM >= 128) {
-    if (win && BM == 256 && !pipe_unroll(abl) && !(abl & 2048))
-      return launch_abl_w0<conv_pipew_f16_k, BM>(abl, grid, s, a, ntiles, pf);
-    if (win) return launch_abl<conv_pipew_f16_k, BM, true>(abl, grid, s, a, ntiles, pf);
+    if (win && BM == 256 && !pipe_unroll(abl)) return launch_abl_w0<conv_pipew_f16_k, BM>(abl, grid, s, a, ntiles, pf);
+    if (win) return launch_abl<conv_pipew_f16_k, BM>(abl, grid, s, a, ntiles, pf);
   }
-  launch_abl<conv_pipe_f16_k, BM, true>(abl, grid, s, a, ntiles, pf);
+  launch_abl<conv_pipe_f16_k, BM>(abl, grid, s, a, ntiles, pf);
 }
 
-// kernel symbol of a launch, e.g. conv_pipew_f16<640,256> (the ping-pong schedule, ABL bit
-// 2048, as conv_pipewpp_f16<640,256>); the strings live in a set (stable pointers)
+// kernel symbol of a launch, e.g. conv_pipew_f16<640,256>; the strings live in a set (stable
+// pointers)
 static const char* pipe_name(bool i8, bool win, int abl, int bm) {
   static std::mutex mu;  // (handles may be planned on several threads)
   std::lock_guard<std::mutex> lk(mu);
   static std::set<std::string> names;
   char b[48];
-  snprintf(b, sizeof b, "conv_pipe%s%s_%s<%d,%d>", win ? ((abl & 4096) ? "w0" : "w") : "", (abl & 2048) ? "pp" : "",
-           i8 ? "i8" : "f16", abl & ~(2048 | 4096), bm);
+  snprintf(b, sizeof b, "conv_pipe%s_%s<%d,%d>", win ? ((abl & 4096) ? "w0" : "w") : "", i8 ? "i8" : "f16",
+           abl & ~4096, bm);
   return names.insert(b).first->c_str();
 }
 
 const char* conv_pipe_name(const ConvArgs& a_in) {
   ConvArgs a = a_in;
   a.pipe_corder = g_pipe_korder_get() && a.ks == 3 && a.cin % 64 == 0 ? 1 : 0;
-  {
-    bool split = false;
-    if (wide_plan(a, &split) > 0) {  // (the step's time covers the tail launch too)
-      static const char* names[2][2] = {{"conv_wide_f16<640>", "conv_wide_f16<640>+tail"},
-                                        {"conv_wide_f16<896>", "conv_wide_f16<896>+tail"}};
-      return names[pipe_abl(a) == 896][split ? 1 : 0];
-    }
-  }
   const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
   const bool abl_mode = a.head_w || conv_pipe_mode() <= 1 || conv_pipe_mode() == 13;
   const bool win = abl_mode && pipe_win_ok(a, bm);
-  return pipe_name(false, win,
-                   pipe_abl(a) | (abl_mode && tune().pipe_pp ? 2048 : 0) | (win && !pipe_unroll(pipe_abl(a)) && !tune().pipe_pp ? 4096 : 0),
-                   bm);
+  return pipe_name(false, win, pipe_abl(a) | (win && !pipe_unroll(pipe_abl(a)) ? 4096 : 0), bm);
 }
 
 // K order of the implicit GEMM: 0 = tap outer (each tap's whole channel run), 1 = 64-channel
@@ -1424,22 +1267,6 @@ void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
   a.pipe_corder = tune().pipe_korder && a.ks == 3 && a.cin % 64 == 0 ? 1 : 0;
   a.pipe_g = pipe_walk_g(a);
   a.pipe_u = pipe_unroll(pipe_abl(a)) ? 1 : 0;
-  {
-    bool split = false;
-    const int nw = wide_plan(a, &split);
-    if (nw > 0) {
-      launch_conv_wide(a, pipe_abl(a), nw, pipe_cus(), s);
-      if (split) {  // the remaining wide units as 256 x 128 window tiles [2 nw, 2 U) of the M-major walk
-        ConvArgs b = a;
-        b.pipe_g = 0;
-        b.pipe_t0 = 2 * nw;
-        const int nt2 = (int)(2 * conv_wide_tiles(a));
-        const int cnt = nt2 - b.pipe_t0;
-        launch_pipe_bm<256>(b, s, nt2, dim3((unsigned)(cnt < pipe_cus() ? cnt : pipe_cus())), true);
-      }
-      return;
-    }
-  }
   const int bm = conv_pipe_mode() > 1 && conv_pipe_mode() != 13 ? 256 : pipe_bm(a);
   const int64_t nt = (int64_t)((a.M + bm - 1) / bm) * (a.cout_pad / kPBN);
   RTDM_REQUIRE(nt < (1ll << 31), RTDM_E_CAPACITY, "conv: grid too large");
@@ -1458,13 +1285,6 @@ void launch_conv_pipe(const ConvArgs& a_in, hipStream_t s) {
     case 9: hipLaunchKernelGGL((conv_pipe_f16<48, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
     case 10: hipLaunchKernelGGL((conv_pipe_f16<96, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
     case 11: hipLaunchKernelGGL((conv_pipe_f16<0, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
-    // ping-pong ablations (diagnostics): 20 the PP kernel, generic epilogue; 21 no loads;
-    // 22 no fragment reads; 23 neither; 24 no epilogue
-    case 20: hipLaunchKernelGGL((conv_pipe_f16<2048, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
-    case 21: hipLaunchKernelGGL((conv_pipe_f16<2049, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
-    case 22: hipLaunchKernelGGL((conv_pipe_f16<2050, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
-    case 23: hipLaunchKernelGGL((conv_pipe_f16<2051, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
-    case 24: hipLaunchKernelGGL((conv_pipe_f16<2064, 256>), grid, dim3(512), 0, s, a, ntiles, 0); break;
     // tap-unrolled window loop ablations (diagnostics; window-mode register-epilogue layers
     // only, every other layer runs its normal kernel): 31 no LDS-DMA loads, 32 no fragment
     // reads, 33 neither, 34 no wait + barrier, 35 no window-slice loads (B loads kept), 36 no B

@@ -17,6 +17,11 @@ LIB_PATH = os.environ.get("RTDM_LIB", os.path.join(_HERE, "librtdm.so"))
 
 # rtdm_status
 RTDM_OK = 0
+RTDM_E_INVALID = 1
+RTDM_E_HIP = 2
+RTDM_E_CAPACITY = 3
+RTDM_E_UNSUPPORTED = 4
+RTDM_E_OOM = 5
 STATUS_NAMES = {0: "OK", 1: "INVALID", 2: "HIP", 3: "CAPACITY", 4: "UNSUPPORTED", 5: "OOM"}
 # rtdm_dtype
 RTDM_F32 = 0

@@ -154,12 +154,16 @@ class _ACFFClassifier(torch.nn.Module):
         return h
 
     def set_tuning(self, key: str, value: int):
-        """One knob of rtdm_set_tuning for this model's handles only."""
+        """One knob of rtdm_set_tuning for this model's handles only.  A change on a live handle
+        bumps handle_generation (rtdm.pipeline then re-captures its hipGraphs)."""
         if not hasattr(self, "tuning"):
             self.tuning = {}
+        changed = self.tuning.get(key) != int(value)
         self.tuning[key] = int(value)
         if self._handle is not None:
             L.check(L.lib().rtdm_classifier_set_tuning(self._handle, key.encode(), int(value)))
+            if changed:
+                self.handle_generation = getattr(self, "handle_generation", 0) + 1
         return self
 
     def describe(self, n: int = 1) -> str:

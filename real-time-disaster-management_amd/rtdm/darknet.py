@@ -184,13 +184,25 @@ class Darknet(torch.nn.Module):
             self._calibrate(h)
         return h
 
+    # knobs the planner reads at rtdm_detector_create only: a created handle refuses them
+    PLAN_TIME_KEYS = ("fuse_head", "two_streams")
+
     def set_tuning(self, key: str, value: int):
         """One launch-time knob of rtdm_set_tuning for this model only (its handles; the
         process defaults and other models are unchanged): e.g. ("conv_pipe_cost", 1) plans the
-        conv tiles for throughput when several batches are in flight."""
+        conv tiles for throughput when several batches are in flight.  Plan-time keys
+        (PLAN_TIME_KEYS) raise ValueError: set them with rtdm_set_tuning before the model's
+        first handle is created.  A change on a live handle bumps handle_generation, so
+        rtdm.pipeline re-captures its hipGraphs instead of replaying kernels chosen under the
+        old value."""
+        if key in self.PLAN_TIME_KEYS:
+            raise ValueError(f"{key} is a plan-time key: set it with rtdm_set_tuning before the handle is created")
+        changed = self.tuning.get(key) != int(value)
         self.tuning[key] = int(value)
         if self._handle is not None:
             L.check(L.lib().rtdm_detector_set_tuning(self._handle, key.encode(), int(value)))
+            if changed:
+                self.handle_generation = getattr(self, "handle_generation", 0) + 1
         return self
 
     # ---------------------------------------------------------------- forward --

@@ -207,57 +207,52 @@ def test_tuning_is_per_handle():
     """the knobs a plan reads are per handle.  rtdm_set_tuning sets the process
     defaults a handle copies at creation; rtdm_detector_set_tuning changes one handle only.
     Checked through the kernel each step would launch (step_info names, host-side planning):
-    yolov4-tiny@608 at b64 plans L12 on conv_pipew by default (conv_wide off), and on conv_wide
-    (latency objective: one round of 256 x 256 tiles + a 256 x 128 tail) with conv_wide 1."""
+    the pooled stem of yolov4-tiny@608 is conv_stem3<true,1,k16> by default (the kh = 2 third of
+    K on a 16-deep MFMA) and conv_stem3<true,1> with stem_k16 0."""
     from rtdm import _lib as L
     lib = L.lib()
     h1, _, _ = _plan("yolov4-tiny-aider-416", 608)
     h2, _, _ = _plan("yolov4-tiny-aider-416", 608)
     try:
         n1 = _step_names(h1)
-        assert not any(n.startswith("conv_wide") for n in n1) and "conv_pipew_f16<640,256>" in n1, n1
-        L.check(lib.rtdm_detector_set_tuning(h2, b"conv_wide", 1))
+        assert n1[0] == "conv_stem3<true,1,k16>" and "conv_pipew_f16<640,256>" in n1, n1
+        L.check(lib.rtdm_detector_set_tuning(h2, b"stem_k16", 0))
         n2 = _step_names(h2)
-        assert "conv_wide_f16<640>+tail" in n2 and "conv_wide_f16<640>" in n2, n2
+        assert n2[0] == "conv_stem3<true,1>" and n2[1:] == n1[1:], n2
         assert _step_names(h1) == n1  # the other handle is unchanged
-        L.check(lib.rtdm_detector_set_tuning(h2, b"conv_wide", 2))  # all wide, no tail
-        n3 = _step_names(h2)
-        assert "conv_wide_f16<640>" in n3 and "conv_wide_f16<640>+tail" not in n3, n3
         assert lib.rtdm_detector_set_tuning(h2, b"no_such_key", 1) != 0
         # process defaults: a handle created after rtdm_set_tuning copies them; older ones keep theirs
-        L.check(lib.rtdm_set_tuning(b"conv_wide", 1))
+        L.check(lib.rtdm_set_tuning(b"stem_k16", 0))
         try:
             h3, _, _ = _plan("yolov4-tiny-aider-416", 608)
             try:
-                assert any(n.startswith("conv_wide") for n in _step_names(h3))
+                assert _step_names(h3)[0] == "conv_stem3<true,1>"
             finally:
                 lib.rtdm_detector_destroy(h3)
             assert _step_names(h1) == n1
         finally:
-            L.check(lib.rtdm_set_tuning(b"conv_wide", 0))
+            L.check(lib.rtdm_set_tuning(b"stem_k16", 1))
     finally:
         lib.rtdm_detector_destroy(h1)
         lib.rtdm_detector_destroy(h2)
 
 
-def test_stem_pair_fusion_planned():
-    """yolov4-tiny@608: layers 0-3 (pooled stem + pooled 16 -> 32 conv) plan as one
-    conv_stem_pool2 launch (the second step reports as fused), per handle switchable."""
+def test_plan_time_keys_refused_on_live_handle():
+    """fuse_head / two_streams are read when a handle is planned: rtdm_detector_set_tuning
+    refuses them on a created handle (RTDM_E_INVALID) instead of accepting a silent no-op, and
+    Darknet.set_tuning raises for them; rtdm_set_tuning (process defaults) still takes them."""
     from rtdm import _lib as L
+    from rtdm.darknet import Darknet
     lib = L.lib()
     h, _, _ = _plan("yolov4-tiny-aider-416", 608)
     try:
-        L.check(lib.rtdm_detector_set_tuning(h, b"stem_fuse", 1))  # opt-in (default off)
-        n = _step_names(h)
-        assert n[0] == "conv_stem_pool2" and n[1] == "conv_stem_pool2:fused", n[:3]
-        L.check(lib.rtdm_detector_set_tuning(h, b"stem_fuse", 0))
-        n0 = _step_names(h)
-        assert n0[0].startswith("conv_stem3") and n0[1].startswith("conv3_pool_small<16,32"), n0[:3]
+        for key in (b"fuse_head", b"two_streams"):
+            assert lib.rtdm_detector_set_tuning(h, key, 1) == 1
+            assert b"plan-time" in lib.rtdm_last_error()
+        L.check(lib.rtdm_detector_set_tuning(h, b"conv_pipe_cost", 1))  # launch-time keys still apply
     finally:
         lib.rtdm_detector_destroy(h)
-    h, _, _ = _plan("yolov4-tiny-swish", 416)  # swish stem: not the lean epilogue, no fusion
-    try:
-        L.check(lib.rtdm_detector_set_tuning(h, b"stem_fuse", 1))
-        assert "conv_stem_pool2" not in _step_names(h)
-    finally:
-        lib.rtdm_detector_destroy(h)
+    L.check(lib.rtdm_set_tuning(b"fuse_head", 0))
+    m = Darknet(cfg_text("yolov4-tiny-aider-416"), (608, 608))
+    with pytest.raises(ValueError, match="plan-time"):
+        m.set_tuning("two_streams", 0)

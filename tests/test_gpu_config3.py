@@ -1,6 +1,6 @@
 """GPU: BASELINE config 3 (yolov3-aider-416 at 416x416, fp16, batch 16, detection only) at
-the batch it is benchmarked on.  At b16 the tile cost model picks its own tiles (and the
-256 x 256 conv_wide tiles for the residual 3x3s where they pay), so this is the plan
+the batch it is benchmarked on.  At b16 the tile cost model picks its own tiles, so this is
+the plan
 bench.py --classifier none --cfg yolov3-aider-416 --img 416 --batch 16 times:
   * every frame's io rows at b16 are BIT-IDENTICAL to the same frame run at b1 (no kernel's
     K order depends on the batch or the tiling);

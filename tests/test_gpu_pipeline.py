@@ -354,40 +354,37 @@ def test_lean_window_epilogues_bit_identical(dev, case):
                 want = ("<896,",) if cfg.startswith("yolov3") else ("<640,", "_f16<128,")
                 for w in want:
                     assert any(w in n for n in names), (w, names)
-                assert any(n.startswith(("conv_pipew_f16<", "conv_pipewpp_f16<")) for n in names), names
+                assert any(n.startswith("conv_pipew_f16<") for n in names), names
     finally:
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe", 1))
         L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
     assert torch.equal(outs[11], outs[1])
 
 
-@pytest.mark.parametrize("case", ["yolov4-tiny-aider-416@608:3", "yolov3-aider-416@416:3", "yolov4-tiny-aider-416@608:9"])
-@pytest.mark.parametrize("pp", [0, 1])
-def test_pingpong_bit_identical(dev, case, pp):
-    """conv_pipe's ping-pong K-loop (rtdm_set_tuning("conv_pipe_pp"): two wave groups
-    alternating MFMA and memory phases) against the per-K-block-barrier schedule, window
-    mode off (pp=0 row) and on: same io bits; 256-row tiles and the cost model's tiles."""
-    from rtdm import _lib as L
+def test_set_tuning_recaptures_graphs(dev, cls_weights):
+    """A knob changed on a live handle (Darknet / classifier set_tuning) bumps the model's
+    handle_generation, so TwoStagePipeline drops the hipGraph it captured under the old knob and
+    captures a new one, instead of replaying the old kernels.  stem_k16 changes
+    the stem kernel of both stages and not a bit of the outputs."""
     from rtdm.synth import synth_frames
-    cfg, rest = case.split("@")
-    size, b = (int(v) for v in rest.split(":"))
-    x = torch.from_numpy(synth_frames(b, size, size, seed=37)).to(dev)
-    outs = {}
-    try:
-        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_win", pp))
-        for bm in (256, 0):
-            L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", bm))
-            for v in (0, 1):
-                L.check(L.lib().rtdm_set_tuning(b"conv_pipe_pp", v))
-                m, _, _, _ = _detector(cfg, size)
-                outs[(bm, v)] = m(x)[0].cpu()
-                assert any("pp_f16<" in n for n in _names(m, b)) == bool(v)
-    finally:
-        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_pp", 0))
-        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_win", 1))
-        L.check(L.lib().rtdm_set_tuning(b"conv_pipe_bm", 0))
-    for bm in (256, 0):
-        assert torch.equal(outs[(bm, 0)], outs[(bm, 1)]), bm
+    x = torch.from_numpy(synth_frames(8, IMG, IMG, seed=91)).to(dev)
+    pg, _, _, _ = _pipeline(cls_weights, graphs=True)
+    for _ in range(2):  # capture, then replay
+        ref = _host(pg(x))
+    k0 = set(pg._graphs)
+    gd, gc = pg.detector.handle_generation, pg.classifier.handle_generation
+    pg.detector.set_tuning("stem_k16", 0)
+    pg.classifier.set_tuning("stem_k16", 0)
+    assert (pg.detector.handle_generation, pg.classifier.handle_generation) == (gd + 1, gc + 1)
+    for _ in range(2):
+        got = _host(pg(x))
+    k1 = set(pg._graphs)
+    assert k0.isdisjoint(k1) and len(k1) == 1, (k0, k1)
+    _same(got, ref, "re-captured graph, stem_k16 0")
+    pg.detector.set_tuning("stem_k16", 0)  # the same value again: nothing to re-capture
+    assert pg.detector.handle_generation == gd + 1
+    _same(_host(pg(x)), ref, "replay")
+    assert set(pg._graphs) == k1
 
 
 def _names(m, n):
