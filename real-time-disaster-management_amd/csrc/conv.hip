@@ -400,6 +400,11 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
     const float slp = act == ACT_LEAKY ? slope : 1.f;
     // two 4-quad tiles per iteration (tx, tx + 2): two independent LDS -> MFMA -> epilogue
     // chains per wave instead of one latency-bound chain; the loop is unswitched on `lean`
+    // the pixel pair as two ds_read_b64 (2 LDS cycles each, 64 banks) rather than the one
+    // ds_read2_b64 the compiler would merge them into (8 cycles, 32 banks: 55 % of the LDS
+    // cycles were conflicts): an offset it cannot see keeps them apart
+    int one = 1;
+    asm volatile("" : "+v"(one));
     auto run = [&](auto lean_c) {
     constexpr bool LEAN = decltype(lean_c)::value;
     for (int tx0 = wid & 1, off = 0; tx0 * 4 < qw; tx0 += 4, off += 32 * s) {
@@ -409,7 +414,7 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int tx = tx0 + 2 * u, o = off + u * 16 * s;
-        const uint2 b00 = rk0[o], b01 = rk0[o + 1];
+        const uint2 b00 = rk0[o], b01 = rk0[o + one];
         bf0[u] = __builtin_bit_cast(h8, (u32x4{b00.x, b00.y, b01.x, b01.y}));
         if constexpr (K16) {
           bk[u] = __builtin_bit_cast(h4s, rk2s[o]);
@@ -483,7 +488,9 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
       const int lx = (valid ? ox : a.ow - 1) * s - pad + 1;
       const uint2* rowk0 = stem_lds + (tr * s + kh0) * ls;
       const uint2* rowk2 = stem_lds + (tr * s + 2) * ls;
-      const uint2 b00 = rowk0[lx + 2 * pr0], b01 = rowk0[lx + 2 * pr0 + 1];
+      int one = 1;  // (two ds_read_b64, not a ds_read2_b64: see the pooled path)
+      asm volatile("" : "+v"(one));
+      const uint2 b00 = rowk0[lx + 2 * pr0], b01 = rowk0[lx + 2 * pr0 + one];
       const h8 bf0 = __builtin_bit_cast(h8, (u32x4{b00.x, b00.y, b01.x, b01.y}));
       h8 bf1;
       h4s bk;
@@ -1112,7 +1119,7 @@ __global__ __launch_bounds__(256) void conv3_direct(ConvArgs a, int cc_log2) {
 //     (p, p^1) by DPP, then one bias/activation/store per pooled pixel.
 // Block: TH x 16 output pixels x COUT channels; waves = (TH / WROWS) row
 // groups x (COUT / 16 / WCH) channel groups = 4.  LDS: the 18 x 18 input halo,
-// pixel stride CIN + 8 halfs (16 consecutive pixels hit distinct banks).
+// pixel stride PS halfs (below: chosen so the B-fragment reads are conflict-free).
 // --------------------------------------------------------------------------
 // NWV: waves per block (4, or 8 for Cin 64 -> Cout 128: one 16-channel tile per wave, 18
 // k-steps of weights = 72 registers).  A full-resolution output view (a.e.full) is written
@@ -1123,7 +1130,9 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : (CIN == 16 || WCH == 1) &&
   // (16 pixels x 2 channel groups) fall in 16 distinct 4-bank slots (at 40: 2-way conflicts,
   // half the kernel's LDS cycles, PMC r04f)
   // Cin 64: 80 (the 1x1-style pattern, 16 pixels x 4 channel groups per k-step: conflict-free)
-  constexpr int TW = 16, HW = TW + 2, PS = CIN == 32 ? 48 : CIN == 64 ? 80 : CIN + 8;
+  // Cin 16: 16, unpadded -- a k-step's lane groups pair the two channel halves of one tap
+  // (+16 B), which at 32-B pixels fill all 16 slots (at 24: 18 extra cycles per 5 k-steps)
+  constexpr int TW = 16, HW = TW + 2, PS = CIN == 32 ? 48 : CIN == 64 ? 80 : CIN == 16 ? 16 : CIN + 8;
   constexpr int NT = 64 * NWV;
   constexpr int CG = CIN / 8;                // 8-channel groups per tap
   constexpr int NQ = 9 * CG;                 // 8-channel groups in K
