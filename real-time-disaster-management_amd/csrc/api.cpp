@@ -53,7 +53,6 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "conv_c32") t.conv_c32 = v ? 1 : 0;
   else if (k == "res_fuse") t.res_fuse = v < 0 ? 0 : v > 2 ? 2 : v;
   else if (k == "stem_k16") t.stem_k16 = v ? 1 : 0;
-  else if (k == "stem_fuse") t.stem_fuse = v < 0 ? 0 : v > 3 ? 3 : v;
   else if (k == "pool_sep") t.pool_sep = v ? 1 : 0;
   else if (k == "pool_small64") t.pool_small64 = v ? 1 : 0;
   else if (k == "pool_small_pf") t.pool_small_pf = v <= 0 ? 0 : v >= 2 ? 2 : 1;

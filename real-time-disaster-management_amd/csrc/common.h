@@ -196,7 +196,6 @@ __device__ __forceinline__ void mfma_opcode_switch() {
 struct Tuning {
   int conv_pipe = 1;        // conv_pipe mode (1 the kernels; 0 off; > 1 diagnostics, conv_pipe.hip)
   int stem_abl = 0;         // conv_stem3 ablations (diagnostics)
-  int stem_fuse = 1;        // pooled u8 stem + the 16 -> 32 pooled conv reading its map as one conv_stem_band launch
   int head1x1 = 1;          // stand-alone YOLO head convs on head1x1_f16
   int pipe_bm = 0;          // conv_pipe tile rows: 0 cost model, else forced 256 / 128 / 64
   int pipe_cost = 0;        // conv_pipe tile objective: 0 latency (rounds), 1 throughput (CU-time)
@@ -285,10 +284,6 @@ const char* head1x1_name(const ConvArgs& a);
 int conv_pipe_mode();
 int pipe_bm(const ConvArgs& a);           // tile rows the launch will use (256 / 128 / 64)
 const char* conv_pipe_name(const ConvArgs& a);  // kernel symbol of that launch
-// stem_band.hip: the pooled uint8 stem (Cin 3 -> 16) + the 16 -> 32 3x3 pooled conv reading its
-// map as one persistent row-band launch (the pooled stem map stays in LDS)
-bool stem_band_ok(const ConvArgs& a0, const ConvArgs& a2);
-void launch_stem_band(const ConvArgs& a0, const ConvArgs& a2, hipStream_t s);
 // conv_c32.hip: persistent Cin-32 3x3 kernel (stride 1 / 2, Cout 64, optional residual)
 bool c32_ok(const ConvArgs& a);
 void launch_c32(const ConvArgs& a, hipStream_t s);

@@ -113,9 +113,6 @@ struct Step {
   int full_t = -1, pool_t = -1, up_t = -1, res_t = -1;
   int yolo = -1;  // index into yolo heads
   bool quad = false;
-  // fused stem pair (stem_band.hip): this pooled stem's pooled map is read by the next step
-  // only, so both run as one conv_stem_band launch when its shapes fit (stem_band_ok)
-  bool fuse2 = false;
   // Darknet-53's first residual block: this 1x1 reduce (64 -> 32), whose map only the next
   // step (3x3 32 -> 64 with this step's input as its shortcut) reads, runs with it as one
   // conv3_c32r launch when the shapes fit (c32r_ok)
@@ -708,21 +705,6 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     RTDM_REQUIRE(wptr == n_floats, RTDM_E_INVALID,
                  "darknet weights: stream has " + std::to_string(n_floats) + " floats, cfg needs " +
                      std::to_string(wptr));
-  // ---- fused stem pairs: a pooled stem whose pooled map (own buffer, not a concat slice)
-  //      only the next step reads ----
-  for (size_t i = 0; i + 1 < h.steps.size(); ++i) {
-    Step& a = h.steps[i];
-    const Step& b = h.steps[i + 1];
-    if (a.kind != ST_CONV || b.kind != ST_CONV || a.in_t >= 0 || a.pool_t < 0 || a.full_t >= 0 || a.up_t >= 0 ||
-        a.yolo >= 0 || a.head || b.in_t != a.pool_t || b.res_t == a.pool_t)
-      continue;
-    bool other = h.tensors[a.pool_t].home >= 0;
-    for (size_t j = 0; j < h.steps.size() && !other; ++j)
-      if (j != i + 1 && (h.steps[j].in_t == a.pool_t || h.steps[j].res_t == a.pool_t)) other = true;
-    for (const Tensor& t : h.tensors)
-      if (t.home == a.pool_t) other = true;
-    a.fuse2 = !other;
-  }
   // ---- fused residual pairs (conv3_c32r) ----
   for (size_t i = 0; i + 1 < h.steps.size(); ++i) {
     Step& a = h.steps[i];
@@ -1007,23 +989,11 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       for (int d : st.deps)
         if (h.steps[d].stream != st.stream) RTDM_HIP(hipStreamWaitEvent(s, h.step_ev[d], 0));
     if (ev) RTDM_HIP(hipEventRecord(ev[2 * si], s));
-    if (fused_next) {  // this step ran inside the previous step's launch (conv_stem_band / conv3_c32r)
+    if (fused_next) {  // this step ran inside the previous step's launch (conv3_c32r)
       fused_next = false;
     } else if (st.kind == ST_CONV) {
       ConvArgs a = run_args(h, st, x, in_kind, n, io, raw);
-      if (st.fuse2 && tune().stem_fuse && st.q < 0 && h.steps[si + 1].q < 0) {
-        const Step& nx = h.steps[si + 1];
-        const ConvArgs b = run_args(h, nx, x, in_kind, n, io, raw);
-        if ((!two || nx.stream == st.stream) && stem_band_ok(a, b)) {
-          if (two)
-            for (int d : nx.deps)
-              if (h.steps[d].stream != nx.stream) RTDM_HIP(hipStreamWaitEvent(s, h.step_ev[d], 0));
-          launch_stem_band(a, b, s);
-          fused_next = true;
-          h.fused_away.push_back(st.pool_t);
-        }
-      }
-      if (!fused_next && st.fuse_r && tune().res_fuse && st.q < 0 && h.steps[si + 1].q < 0) {
+      if (st.fuse_r && tune().res_fuse && st.q < 0 && h.steps[si + 1].q < 0) {
         const Step& nx = h.steps[si + 1];
         const ConvArgs b = run_args(h, nx, x, in_kind, n, io, raw);
         if ((!two || nx.stream == st.stream) && c32r_ok(a, b)) {
@@ -1403,13 +1373,6 @@ rtdm_status rtdm_detector_step_info(rtdm_detector h, int step, char* name, int n
     step_info(*h, h->steps[step], nm, f, b);
     // a fused residual pair (run_detector's conv3_c32r choice): the first step reports the
     // launch (both layers' FLOPs), the second an empty step
-    const auto stem_pair = [&](int i) {
-      if (i < 0 || i + 1 >= (int)h->steps.size()) return false;
-      const Step& a = h->steps[i];
-      const Step& c = h->steps[i + 1];
-      return a.fuse2 && tune().stem_fuse && a.q < 0 && c.q < 0 && (!(h->two_streams && h->side) || c.stream == a.stream) &&
-             stem_band_ok(geom_args(*h, a), geom_args(*h, c));
-    };
     const auto res_pair = [&](int i) {
       if (i < 0 || i + 1 >= (int)h->steps.size()) return false;
       const Step& a = h->steps[i];
@@ -1417,20 +1380,7 @@ rtdm_status rtdm_detector_step_info(rtdm_detector h, int step, char* name, int n
       return a.fuse_r && tune().res_fuse && a.q < 0 && c.q < 0 && (!(h->two_streams && h->side) || c.stream == a.stream) &&
              c32r_ok(geom_args(*h, a), geom_args(*h, c));
     };
-    if (stem_pair(step)) {
-      const Step& a = h->steps[step];
-      const Step& c = h->steps[step + 1];
-      std::string n2;
-      double f2 = 0, b2 = 0;
-      step_info(*h, c, n2, f2, b2);
-      nm = "conv_stem_band";
-      f += f2;
-      b = (double)a.ih * a.iw * 3.0 + (double)(c.oh / 2) * (c.ow / 2) * c.cout * (double)esize_of(h->dtype);
-    } else if (stem_pair(step - 1)) {
-      nm = "conv_stem_band:fused";
-      f = 0;
-      b = 0;
-    } else if (res_pair(step)) {
+    if (res_pair(step)) {
       const Step& a = h->steps[step];
       const Step& c = h->steps[step + 1];
       std::string n2;
@@ -1620,7 +1570,7 @@ rtdm_status rtdm_detector_layer_output(rtdm_detector h, int layer, int n, float*
     if (!out) return;
     RTDM_REQUIRE(std::find(h->fused_away.begin(), h->fused_away.end(), t) == h->fused_away.end(), RTDM_E_UNSUPPORTED,
                  "layer_output: layer " + std::to_string(layer) +
-                     " output was fused away in the last detect (conv_stem_band / conv3_c32r; rtdm_detector_set_tuning stem_fuse 0 / res_fuse 0 keeps it)");
+                     " output was fused away in the last detect (conv3_c32r; rtdm_detector_set_tuning res_fuse 0 keeps it)");
     RTDM_REQUIRE(n > 0 && n <= h->last_n, RTDM_E_INVALID, "layer_output: n exceeds the last detect batch");
     RTDM_REQUIRE(out_numel >= (int64_t)n * x.c * x.h * x.w, RTDM_E_CAPACITY, "layer_output: out too small");
     launch_to_nchw_f32(tensor_view(*h, t), n, x.h, x.w, x.c, out, h->dtype, (hipStream_t)stream);

@@ -211,13 +211,8 @@ def test_tuning_is_per_handle():
     K on a 16-deep MFMA) and conv_stem3<true,1> with stem_k16 0."""
     from rtdm import _lib as L
     lib = L.lib()
-    L.check(lib.rtdm_set_tuning(b"stem_fuse", 0))  # (the stem as its own step)
-    try:
-        h1, _, _ = _plan("yolov4-tiny-aider-416", 608)
-        h2, _, _ = _plan("yolov4-tiny-aider-416", 608)
-    finally:
-        L.check(lib.rtdm_set_tuning(b"stem_fuse", 1))
-    L.check(lib.rtdm_detector_set_tuning(h1, b"stem_fuse", 0))
+    h1, _, _ = _plan("yolov4-tiny-aider-416", 608)
+    h2, _, _ = _plan("yolov4-tiny-aider-416", 608)
     try:
         n1 = _step_names(h1)
         assert n1[0] == "conv_stem3<true,1,k16>" and "conv_pipew_f16<640,256>" in n1, n1
@@ -231,7 +226,6 @@ def test_tuning_is_per_handle():
         try:
             h3, _, _ = _plan("yolov4-tiny-aider-416", 608)
             try:
-                L.check(lib.rtdm_detector_set_tuning(h3, b"stem_fuse", 0))
                 assert _step_names(h3)[0] == "conv_stem3<true,1>"
             finally:
                 lib.rtdm_detector_destroy(h3)
@@ -262,25 +256,3 @@ def test_plan_time_keys_refused_on_live_handle():
     m = Darknet(cfg_text("yolov4-tiny-aider-416"), (608, 608))
     with pytest.raises(ValueError, match="plan-time"):
         m.set_tuning("two_streams", 0)
-
-
-def test_stem_band_planned():
-    """yolov4-tiny@608: layers 0-3 (pooled stem + pooled 16 -> 32 conv) plan as one
-    conv_stem_band launch (the second step reports as fused), per handle switchable; the swish
-    stem (not the lean epilogue) keeps two launches."""
-    from rtdm import _lib as L
-    lib = L.lib()
-    h, _, _ = _plan("yolov4-tiny-aider-416", 608)
-    try:
-        n = _step_names(h)
-        assert n[0] == "conv_stem_band" and n[1] == "conv_stem_band:fused", n[:3]
-        L.check(lib.rtdm_detector_set_tuning(h, b"stem_fuse", 0))
-        n0 = _step_names(h)
-        assert n0[0].startswith("conv_stem3") and n0[1].startswith("conv3_pool_small<16,32"), n0[:3]
-    finally:
-        lib.rtdm_detector_destroy(h)
-    h, _, _ = _plan("yolov4-tiny-swish", 416)
-    try:
-        assert "conv_stem_band" not in _step_names(h)
-    finally:
-        lib.rtdm_detector_destroy(h)

@@ -411,8 +411,7 @@ def _layer_outputs(m, n_layers, n):
     refusals are skipped, each by its own status and message: a layer the plan never
     materialises (its map lives only inside a fused launch: rtdm_detector_layer_output refuses
     the shape query) and a map the last detect fused away at run time -- which must be exactly
-    the 1x1 reduce of each planned conv3_c32r pair (step name "conv3_c32r") and the pooled stem
-    map of a conv_stem_band pair.  Anything else
+    the 1x1 reduce of each planned conv3_c32r pair (step name "conv3_c32r").  Anything else
     (capacity, bad layer, a new refusal) fails the test."""
     import ctypes
     from rtdm import _lib as L
@@ -421,10 +420,8 @@ def _layer_outputs(m, n_layers, n):
     for i in range(L.lib().rtdm_detector_num_steps(h)):
         nm, layer = ctypes.create_string_buffer(64), ctypes.c_int()
         L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, ctypes.byref(layer), None, None))
-        if nm.value == b"conv3_c32r":  # the 1x1 reduce's own map
+        if nm.value == b"conv3_c32r":
             runtime_fused.add(layer.value)
-        elif nm.value == b"conv_stem_band":  # the pooled stem map: the [maxpool] after the stem
-            runtime_fused.add(layer.value + 1)
     out, skipped = {}, set()
     for i in range(n_layers):
         c = ctypes.c_int()

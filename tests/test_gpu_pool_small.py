@@ -41,7 +41,6 @@ def test_pool_small_variants_bit_identical(case, knob):
         for v in (v0, v1):
             L.check(L.lib().rtdm_set_tuning(key.encode(), v))
             m, _, _, _ = _detector(cfg, size, preset="cond")
-            m.set_tuning("stem_fuse", 0)  # (the Cin-16 layer as its own conv3_pool_small launch)
             outs[v] = m(x)[0].cpu()
             names[v] = _names(m, b)
     finally:

@@ -1,5 +1,4 @@
-"""GPU: the Cin-3 MFMA stems (csrc/conv.hip conv_stem3) and the fused stem pair (csrc/stem_band.hip).
-Stems: with the kh = 2 third of K on one
+"""GPU: the Cin-3 MFMA stems (csrc/conv.hip conv_stem3) with the kh = 2 third of K on one
 16-deep MFMA (stem_k16 1, the default) against the 32-deep form (stem_k16 0) whose lane groups
 2, 3 re-read kh = 2 pixels against zero weights.  The two compute the same nonzero products in
 the same order, so every output must be BIT-IDENTICAL -- for every instantiation: the pooled
@@ -59,7 +58,6 @@ def test_stem_k16_bit_identical(case):
     for v in (0, 1):
         m, _, _, _ = _detector(cfg, size, preset=preset)
         m.set_tuning("stem_k16", v)  # this model's handles only
-        m.set_tuning("stem_fuse", 0)  # (the stem as its own launch)
         outs[v] = m(x)[0].cpu()
         names[v] = _names(m, b)
     assert names[1][0] == DET_CASES[case], names[1][:2]
@@ -92,62 +90,3 @@ def test_classifier_stem_k16_bit_identical(name, half, cls_weights):
     assert bool(torch.isfinite(logits[1]).all())
     assert torch.equal(logits[0], logits[1]), float((logits[0] - logits[1]).abs().max())
     assert np.array_equal(logits[0].argmax(1).numpy(), logits[1].argmax(1).numpy())
-
-
-# ---------------------------------------------------------------- the fused stem pair --
-# case -> whether conv_stem_band takes layers 0-3 (the swish stem is not the lean epilogue)
-BAND_CASES = {"yolov4-tiny-aider-416@608:3": True, "yolov4-tiny-aider-416@608:64": True,
-              "yolov4-tiny-aider-416@608:8": True, "yolov4-tiny-aider-416@416:5": True,
-              "yolov3-tiny-aider-416@416:2": True, "yolov4-tiny-aider-416@256:7": True,
-              "yolov4-tiny-3l-512x512@512:3": False, "yolov4-tiny-swish@416:2": False}
-
-
-@pytest.mark.parametrize("case", list(BAND_CASES))
-def test_stem_band_bit_identical(case):
-    """conv_stem_band (csrc/stem_band.hip: the pooled uint8 stem and the 16 -> 32 pooled conv
-    reading its map as ONE persistent row-band launch, the pooled stem map only ever in an LDS
-    ring) against the two launches (stem_fuse 0): BIT-IDENTICAL io -- batches with one and many
-    bands per image, 608 / 416 / 256 frames; the swish cfg (not the lean epilogue) and the 3l cfg
-    (a stride-2 plain stem) keep their launches."""
-    from rtdm.synth import synth_frames
-    cfg, rest = case.split("@")
-    size, b = (int(v) for v in rest.split(":"))
-    x = torch.from_numpy(synth_frames(b, size, size, seed=71)).cuda()
-    preset = "he" if "swish" in cfg else "cond"
-    outs, names = {}, {}
-    for v in (0, 1):
-        m, _, _, _ = _detector(cfg, size, preset=preset)
-        m.set_tuning("stem_fuse", v)
-        outs[v] = m(x)[0].cpu()
-        names[v] = _names(m, b)
-    assert "conv_stem_band" not in names[0], names[0][:3]
-    fused = BAND_CASES[case]
-    assert (names[1][0] == "conv_stem_band") == fused, names[1][:3]
-    if fused:
-        assert names[1][1] == "conv_stem_band:fused", names[1][:3]
-        assert names[0][0].startswith("conv_stem3<true") and names[0][1].startswith("conv3_pool_small<16,32"), names[0][:3]
-    assert bool(torch.isfinite(outs[1]).all())
-    assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
-
-
-def test_stem_band_layer_output_and_nchw():
-    """The fused-away pooled stem map is refused by layer_output (not silently stale); NCHW
-    float input runs the two launches, whose io equals the frame path's within the fp16 bar."""
-    from rtdm import _lib as L
-    from rtdm.synth import synth_frames
-    frames = synth_frames(2, 608, 608, seed=73)
-    x = torch.from_numpy(frames).cuda()
-    m, _, _, _ = _detector("yolov4-tiny-aider-416", 608, preset="cond")
-    io_u8 = m(x)[0].clone()
-    assert _names(m, 2)[0] == "conv_stem_band"
-    with pytest.raises(L.RtdmError, match="fused away"):
-        m.layer_output(1, 2)
-    m.layer_output(3, 2)  # the second conv's pooled map (layer 3) is written
-    h = m.handle(2)
-    io_f = torch.empty_like(io_u8)
-    xf = (torch.from_numpy(frames).permute(0, 3, 1, 2).float() / 255.0).contiguous().cuda()
-    L.check(L.lib().rtdm_detect(h, L.ptr(xf), L.RTDM_INPUT_NCHW_F32, 2, L.ptr(io_f), L.stream_ptr()))
-    torch.cuda.synchronize()
-    m.layer_output(1, 2)  # two launches this time: the map exists
-    d = (io_f - io_u8).abs()  # the float frames round to fp16 in the stem: the fp16 bar
-    assert float(d[..., :4].max()) <= 0.5 and float(d[..., 4:].max()) <= 2e-2, float(d.max())
