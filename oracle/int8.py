@@ -12,9 +12,9 @@ The reference has no numeric int8 path (opaque TensorRT engines 
 entropy-calibration caches, tensorrt_inference/yolo/calibrator.py:87-153), so the int8
 check compares the HIP int8 io with the fp32 oracle relative to this model of the same
 scheme on the oracle (conv_hook of oracle.darknet.DarknetRef in f16_storage mode):
-  * quantised convs: [convolutional] layers with cin % 128 == 0 and cout % 128 == 0,
-    except a conv whose output only a YOLO head conv reads (the int8-eligible convs of
-    the C++ planner, detector.cpp);
+  * quantised convs: 3x3 [convolutional] layers with cin % 128 == 0 and cout % 128 == 0,
+    except a conv whose output only a YOLO head conv reads (the int8-eligible convs of the
+    C++ planner, detector.cpp);
   * calibration: per input channel |x|max over the calibration frames' fp16-storage
     forward; s_c = HEADROOM * |x|max_c / 127 (HEADROOM 2: frames beyond the calibration
     set's extremes round instead of clamping);
@@ -47,18 +47,22 @@ def pre_head(mdefs, i):
             and mdefs[c[0] + 1]["type"] == "yolo")
 
 
-def eligible(mdefs, i, cin):
+def eligible(mdefs, i, cin, out_stride):
+    """out_stride: the conv's output grid stride in image pixels (tools/int8_scope.py
+    experiments with the pre-head rule by stride)."""
     m = mdefs[i]
     return (m["type"] == "convolutional" and cin % 128 == 0 and int(m["filters"]) % 128 == 0
-            and int(m["size"]) in (1, 3) and not pre_head(mdefs, i))
+            and int(m["size"]) == 3 and not pre_head(mdefs, i))
 
 
 def calibrate(ref, x):
     """Per-channel |x|max of every eligible conv input on frames x ([N,3,H,W] in [0,1])."""
     amax = {}
+    img_h = x.shape[2]
 
     def hook(i, xi, w, b):
-        if eligible(ref.mdefs, i, xi.shape[1]):
+        out_h = (xi.shape[2] - 1) // int(ref.mdefs[i].get("stride", 1)) + 1
+        if eligible(ref.mdefs, i, xi.shape[1], img_h // out_h):
             m = xi.abs().amax(dim=(0, 2, 3))
             amax[i] = torch.maximum(amax[i], m) if i in amax else m
         return xi, w, b

@@ -809,15 +809,20 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
         RTDM_REQUIRE(st.hpc.kpad == 128 && st.hpc.cout_pad == 32, RTDM_E_INVALID, "internal: head packing");
       }
       if (stem) st.pc.stem_off = pack_stem(blob, st.w_W, filters, st.bn ? sc.data() : nullptr);
-      // int8 convs: Cin % 128, not a head conv, and not a conv whose output only a YOLO head
-      // conv reads (its rounding reaches the logits with no layer after it to average it
-      // out: the int8 scheme model loses 4 of 226 fp32 detections to yolov4-tiny@608's
-      // L14 / L28 alone, tools/cond_eval.py)
+      // int8 convs: 3x3, Cin % 128, not a head conv, and not a conv whose output only a YOLO
+      // head conv reads.  1x1 convs stay fp16: with the quantize pass of their input they
+      // measured slower than fp16 (b16 L13 / L18 / L25: 14.2 / 12.0 / 16.4 us fp16 vs 17.0 /
+      // 15.7 / 21.5 us int8, tools/det_int8_timing.py r05q).  A pre-head conv's rounding reaches
+      // the logits with no layer after it to average it out: the scheme model
+      // (tools/int8_scope.py, 16 frames) loses 4 % of the two-sided matches with L28 int8
+      // (stride-8 head); L14 (stride 32) costs nothing there, but at b16 it is no faster in
+      // int8 (r05s: 25.9 + the quantize pass vs 25.2 us), so it stays fp16 too.
+      // oracle/int8.py eligible() mirrors this rule.
       const bool pre_head = consumers[st.layer].size() == 1 && consumers[st.layer][0] + 1 < L &&
                             defs[consumers[st.layer][0]].type == "convolutional" &&
                             defs[consumers[st.layer][0] + 1].type == "yolo";
       if (h.int8 && use_mfma && !st.acff && st.yolo < 0 && !st.head && !pre_head && st.cin % 128 == 0 &&
-          (size == 1 || size == 3) && st.pc.cout_pad % 128 == 0 && st.pc.kpad == size * size * st.cin) {
+          size == 3 && st.pc.cout_pad % 128 == 0 && st.pc.kpad == size * size * st.cin) {
         // BN-folded fp32 rows [cout][k] kept for calibration; int8 slots filled there
         const int kp = st.pc.kpad, cp = st.pc.cout_pad;
         st.wf.assign((size_t)filters * kp, 0.f);
