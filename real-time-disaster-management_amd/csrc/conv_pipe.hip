@@ -479,6 +479,7 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
   // the 1 KB zero area; 2048 tm and the window parity offset are multiples of 128, so the
   // half-1 XOR commutes with them).
   const int zb = (2 * kWinRows * BK + kPNS * BN * BK) * 2;
+  static_assert(((2 * kWinRows * kPBK + kPNS * kPBN * kPBK) * 2) % 256 == 0, "zero area 256-byte aligned");
   uint32_t wtab = 0;
   if constexpr (WLOOP) {
 #pragma unroll
@@ -498,10 +499,16 @@ __device__ __forceinline__ void pipe_tile(const ConvArgs& a, unsigned char* smem
     const int iw_o = a.iw + zo;
     const int sh = KH * iw_o + KW;
     const int off = lrow + ((par * kWinRows + sh) << 7) + (int)(((wtab >> (3 * (sh & 7))) & 7u) << 4);
+    // an out-of-image tap reads the zero area at its own offset mod 256 (zb is 256-aligned), so
+    // it takes the bank slot its in-image read would have: a 16-lane group stays conflict-free
+    // (one shared zero address collided with the group's in-image reads: 20 % of the 19^2
+    // layers' LDS cycles were bank conflicts, PMC r05g; now 0 %, the layers 0.2-0.5 % faster,
+    // bit-identical, profiles/r05w_zero_area_ab.txt)
+    const int zl = zb + (off & 255);
 #pragma unroll
     for (int tm = 0; tm < FM; ++tm) {
       const int keep = (int)(amask[tm] << (31 - TT + zo)) >> 31;  // 0 / -1: tap TT valid for this row
-      aoff[tm] = (off & keep) | ((zb - tm * 2048) & ~keep);
+      aoff[tm] = (off & keep) | ((zl - tm * 2048) & ~keep);
     }
   };
   auto wread0 = [&](auto buf_) {
