@@ -209,3 +209,77 @@ def test_read_weights_checkpoint_formats(tmp_path, cls_weights):
     for f in ("a.pt", "b.pt", "c.npz"):
         got = read_weights(str(tmp_path / f))
         assert all(np.array_equal(np.asarray(got[k]), cls_weights["ernet"][k]) for k in cls_weights["ernet"]), f
+
+
+def _map_worker(rank, world, port, q):
+    """One rank of the sharded mAP harness (rtdm.evaluation): its contiguous image shard of the
+    reference's stored detector output, NMS by the CPU oracle, DetectionStats merged over the
+    gloo group."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from conftest import load_npz
+        from oracle import nms as ON
+        from rtdm.evaluation import image_shard, merge_stats
+        from rtdm.metrics import DetectionStats
+        g = load_npz("map_golden.npz")
+        io, t, nl = g["eval/io"], g["eval/targets"], g["eval/n_labels"]
+        img = int(g["eval/img"])
+        starts = np.concatenate([[0], np.cumsum(nl)])
+        lo, hi = image_shard(io.shape[0], world, rank)
+        res = {}
+        for name in ("default", "strict"):
+            conf, iou = g[f"eval/{name}/conf_iou"]
+            st = DetectionStats(2)
+            for b0 in range(lo, hi, 3):  # batches of 3 inside the shard
+                idx = range(b0, min(b0 + 3, hi))
+                tb = np.concatenate([t[starts[i]:starts[i + 1]] for i in idx]).copy()
+                # the image column is batch-relative (datasets.py collate)
+                k = 0
+                for j, i in enumerate(idx):
+                    tb[k:k + nl[i], 0] = j
+                    k += nl[i]
+                out = ON.non_max_suppression(io[b0:b0 + len(idx)], float(conf), float(iou))
+                st.update(out, tb, img, img)
+            merged = merge_stats(st, dist)
+            r = merged.compute()
+            res[name] = (merged.seen, [r["mp"], r["mr"], r["map"], r["mf1"]], np.asarray(r["maps"]).tolist())
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_map_harness_shards():
+    """rtdm.evaluation's multi-GPU path (one process per GPU instead of the reference's
+    nn.DataParallel, yolov3/test.py:42-43): each rank's contiguous image shard, stats merged in
+    rank order, gives the reference test.test's (P, R, mAP@0.5, F1) and maps for the stored
+    detector output (tests/golden/map_golden.npz) on every rank."""
+    import torch.multiprocessing as mp
+    from conftest import load_npz
+    from rtdm.evaluation import image_shard
+    g = load_npz("map_golden.npz")
+    n = g["eval/io"].shape[0]
+    for world in (1, 2, 3, 5):
+        cover = []
+        for r in range(world):
+            lo, hi = image_shard(n, world, r)
+            cover += list(range(lo, hi))
+        assert cover == list(range(n))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_map_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, rr in res:
+        for name in ("default", "strict"):
+            seen, vals, maps = rr[name]
+            assert seen == n
+            assert np.allclose(vals, g[f"eval/{name}/result"], rtol=0, atol=1e-12), (name, vals)
+            assert np.allclose(maps, g[f"eval/{name}/maps"], rtol=0, atol=1e-12)
