@@ -5,6 +5,11 @@ Same flags (:201-211) and the same table: P, R, mAP@0.5 and F1 per class at
 conf_thres 0.001 / iou_thres from the command line.  Tasks: 'test' (default) and
 'benchmark' (img-size 320..608 x iou 0.5/0.7, :225-233); 'study' needs matplotlib
 plotting and is not carried over.  Evaluation logic: rtdm.evaluation.test.
+
+Several GPUs (the reference's nn.DataParallel, :42-43): one process per GPU,
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 test.py ...
+each rank evaluates a contiguous shard of the list file and every rank prints / returns
+the single-process result.
 """
 import argparse
 import os
