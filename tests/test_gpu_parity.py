@@ -327,10 +327,9 @@ def test_detector_cond_weights_survey_bars(dev, case):
     """SURVEY §8d's detector bars on the well-conditioned synthetic weights (rtdm.synth
     COND; the reference ships no detector weights; its per-cfg knobs, CFG_COND, were chosen
     so that the fp16-storage floor meets the 0.5 px bar):
-      fp32: io x,y <= 1e-3 px, w,h <= 1e-3 px + 1e-5 relative, probabilities <= 1e-4, as
-            written for the tiny nets; RELAXED for the deep nets (yolov3 / -spp / ACFF: 2e-3
-            px / 1e-4 relative / 1e-4: their 75+ layers' fp32 sums run in another order than
-            the oracle's); NMS survivors identical;
+      fp32: io x,y <= 1e-3 px, w,h <= 1e-3 px + 1e-5 relative, probabilities <= 1e-4 —
+            SURVEY's bars as written, for every cfg including the 75+-layer ones (measured
+            r05ab: xy <= 1.2e-4 px, w,h inside 1e-3 px, p <= 1e-5); NMS survivors identical;
       fp16: every io box coordinate within 0.5 px of the fp32 oracle (x, y, w and h), and
             the NMS survivor sets (conf 0.3 / IoU 0.4) equal after excluding the candidates
             within 1e-3 of the thresholds (oracle.nms.survivors_equal_outside_band).
@@ -356,12 +355,14 @@ def test_detector_cond_weights_survey_bars(dev, case):
     # another CPU's conv kernels round differently in the last bits)
     dg = np.abs(io32[:2, ::53] - g[f"{case}/io_rows"])
     assert dg[..., :4].max() <= 1e-3 + 1e-4 * np.abs(g[f"{case}/io_rows"][..., :4]).max() and dg[..., 4:].max() <= 1e-4
-    deep = not cfg.startswith(("yolov4-tiny", "yolov3-tiny"))
     x = torch.from_numpy(frames).to(dev)
     m32, _, _ = _darknet(cfg, size, False, "cond")
     io = m32(x)[0].cpu().numpy()
     d = np.abs(io - io32)
-    xy_t, wh_r, p_t = (2e-3, 1e-4, 1e-4) if deep else (1e-3, 1e-5, 1e-4)
+    whx = (d[..., 2:4] - 1e-3) / np.maximum(np.abs(io32[..., 2:4]), 1e-30)
+    print(case, "fp32 max |d|: xy", d[..., :2].max(), "wh", d[..., 2:4].max(), "wh rel excess", whx.max(),
+          "p", d[..., 4:].max())
+    xy_t, wh_r, p_t = 1e-3, 1e-5, 1e-4
     assert d[..., :2].max() <= xy_t, d[..., :2].max()
     assert (d[..., 2:4] <= 1e-3 + wh_r * np.abs(io32[..., 2:4])).all(), d[..., 2:4].max()
     assert d[..., 4:].max() <= p_t, d[..., 4:].max()
