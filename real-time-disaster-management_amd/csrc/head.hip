@@ -108,13 +108,21 @@ __global__ __launch_bounds__(256) void head1x1_f16(ConvArgs a) {
   constexpr int PX = 16 * FM, PXS = PX + 1;
   __shared__ float hs_tile[4][32 * PXS];
   float* T = hs_tile[wid];
+  // The decode branch is per lane (the head channel k = lane's column) and so divergent
+  // across the wave: every path's operations as selects instead, the same operations on the
+  // same values per element (xy: rcp(1 + exp(-x)) + grid, wh: exp(x) * anchor, obj / cls:
+  // rcp(1 + exp(-x))), bit-identical to epi_io_decode.  A lane's 4 rows j of block tm are
+  // consecutive pixels: one row_to_pix per block, row_pix4 for the others.
 #pragma unroll
-  for (int tm = 0; tm < FM; ++tm)
+  for (int tm = 0; tm < FM; ++tm) {
+    const int r0 = min(m_base + tm * 16 + 4 * g, a.M - 1);
+    int n0_, oy0_, ox0_;
+    row_to_pix(a, r0, n0_, oy0_, ox0_);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int px = tm * 16 + 4 * g + j;
       int n, oy, ox;
-      row_to_pix(a, min(m_base + px, a.M - 1), n, oy, ox);
+      row_pix4(a, r0, j, n0_, oy0_, ox0_, n, oy, ox);  // (rows past M: any pixel, never stored)
 #pragma unroll
       for (int tn = 0; tn < 2; ++tn) {
         if (!cv[tn]) continue;
@@ -123,17 +131,18 @@ __global__ __launch_bounds__(256) void head1x1_f16(ConvArgs a) {
         const float x = t * sc[tn] + sh[tn];
         const int k = kk[tn];
         float o;
-        if (e.raw)
+        if (e.raw) {
           o = x;
-        else if (k < 2)
-          o = (__frcp_rn(1.f + __expf(-x)) + (float)(k == 0 ? ox : oy)) * e.ystride;
-        else if (k < 4)
-          o = (__expf(x) * anc[tn]) * e.ystride;
-        else
-          o = __frcp_rn(1.f + __expf(-x));
+        } else {
+          const bool wh = k == 2 || k == 3;
+          const float v = __expf(wh ? x : -x);
+          const float s = __frcp_rn(1.f + v);
+          o = k < 2 ? (s + (float)(k == 0 ? ox : oy)) * e.ystride : wh ? (v * anc[tn]) * e.ystride : s;
+        }
         T[(tn * 16 + fr) * PXS + px] = o;
       }
     }
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   const int rows = min(PX, a.M - m_base), no = e.no, na = a.cout / no;
