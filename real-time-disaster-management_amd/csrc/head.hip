@@ -152,11 +152,14 @@ __global__ __launch_bounds__(256) void head1x1_f16(ConvArgs a) {
   const int p0 = oy0 * a.ow + ox0;
   const bool one_image = p0 + rows <= (int)plane;  // the wave's rows are consecutive pixels of one image
   const int ne = rows * no;
+  // el / no by a multiply-shift (exact for el < 2112 and no <= 32, checked host-side in
+  // head1x1_ok): a run-time integer division per element was a third of the kernel's VALU
+  const uint32_t inv_no = (65536u + (uint32_t)no - 1u) / (uint32_t)no;
   for (int ai = 0; ai < na; ++ai) {
     const float* Ta = T + ai * no * PXS;
     float* dst = e.io + ((size_t)n0 * e.io_rows + e.io_off + (size_t)ai * plane + p0) * no;
     for (int el = lane; el < ne; el += 64) {
-      const int px = el / no, k = el - px * no;
+      const int px = (int)(((uint32_t)el * inv_no) >> 16), k = el - px * no;
       const float v = Ta[k * PXS + px];
       if (one_image) {
         dst[el] = v;
@@ -173,7 +176,7 @@ bool head1x1_ok(const ConvArgs& a) {
   return a.ks == 1 && a.stride == 1 && a.pad == 0 && !a.quad && a.in_kind == IN_NHWC && !a.w_f32 && a.w &&
          !a.head_w && epi_io_ok(a) && a.cout >= 1 && a.cout <= 32 && a.cout_pad >= 32 && a.cin % 128 == 0 &&
          a.kpad >= a.cin && (a.in_cs | a.in_co) % 8 == 0 && a.kpad % 8 == 0 && a.ih == a.oh && a.iw == a.ow &&
-         a.e.no > 0;
+         a.e.no > 0 && a.e.no <= 32;  // (the store loop's multiply-shift division: rows <= 64, no <= 32)
 }
 
 static int head_fm(const ConvArgs& a) {
