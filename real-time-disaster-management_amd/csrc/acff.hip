@@ -320,7 +320,7 @@ __device__ __forceinline__ float fma_mix_hi_v(float w, uint32_t x2, float acc) {
 constexpr int kAcffPMaxCin = 128;  // depthwise taps + biases of the whole layer in LDS
 
 // MODE: 0 fp16, 1 int8 1x1 fusion, 2 fp16 + calibration (records the concat's |x|max)
-template <int CC, int NF, int ABL = 0, int MODE = 0>  // ABL (diagnostics, wrong outputs): 1 no taps, 2 no GEMM
+template <int CC, int NF, int ABL = 0, int MODE = 0>  // ABL (diagnostics, wrong outputs): 1 no taps, 2 no GEMM, 4 no tap-weight reads
 __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a) {  // NF 2: <= 168 VGPRs, 3 waves / SIMD
   constexpr bool I8 = MODE == 1, CAL = MODE == 2;
   using G = AcffPGeom<CC>;
@@ -473,7 +473,15 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
               const int hr = py + 3 + (kh - 1) * d, hc = px + 3 + (kw - 1) * d;
               const u32x4 xv = *(const u32x4*)(xb + (hr * HW + hc) * PS + cg * 8);
               const float* wp = s_dw + (br * 9 + kh * 3 + kw) * a.cin + cbase;
-              const f4 w0 = *(const f4*)wp, w1 = *(const f4*)(wp + 4);
+              f4 w0, w1;
+              if constexpr ((ABL & 4) != 0) {  // (diagnostic: no tap-weight LDS reads)
+                w0 = f4{0.5f, 0.25f, 0.125f, 0.5f};
+                w1 = w0;
+                (void)wp;
+              } else {
+                w0 = *(const f4*)wp;
+                w1 = *(const f4*)(wp + 4);
+              }
               const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
 #pragma unroll
               for (int jj = 0; jj < 4; ++jj) {
@@ -672,6 +680,7 @@ void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int
     else if (a.amax) cout_pad == 64 ? go(acff_persist<16, 2, 0, 2>) : go(acff_persist<16, 4, 0, 2>);
     else if (abl == 1) cout_pad == 64 ? go(acff_persist<16, 2, 1>) : go(acff_persist<16, 4, 1>);
     else if (abl == 2) cout_pad == 64 ? go(acff_persist<16, 2, 2>) : go(acff_persist<16, 4, 2>);
+    else if (abl == 4) cout_pad == 64 ? go(acff_persist<16, 2, 4>) : go(acff_persist<16, 4, 4>);
     else cout_pad == 64 ? go(acff_persist<16, 2>) : go(acff_persist<16, 4>);
   }
   RTDM_HIP(hipGetLastError());
