@@ -291,7 +291,12 @@ struct AcffPGeom {
   static constexpr int AS = KC + 8;                    // A-tile row stride (halfs)
   static constexpr int HALO = HH * HW * CG;            // 16-byte vectors per halo chunk
   static constexpr int PV = (HALO + 255) / 256;        // prefetch registers per thread
-  static constexpr int XS = HH * HW * PS;              // halfs per halo buffer
+  // RP: halo row pitch (halfs), 4 past HW * PS: the depthwise reads are ds_read_b64 of 4
+  // channels for pixels of two tile rows per 32-lane half, and a row offset of 2 mod 4 dwords
+  // puts the second row on the other two banks of each 4-bank slot (conflict-free); the
+  // staging then writes 8-byte halves (a row start is only 8-byte aligned)
+  static constexpr int RP = HW * PS + 4;
+  static constexpr int XS = HH * RP;                   // halfs per halo buffer
 };
 
 // fp32 = w (SGPR f32) * x (f16, low / high half of a packed pair) + acc, exact like
@@ -324,7 +329,7 @@ template <int CC, int NF, int ABL = 0, int MODE = 0>  // ABL (diagnostics, wrong
 __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a) {  // NF 2: <= 168 VGPRs, 3 waves / SIMD
   constexpr bool I8 = MODE == 1, CAL = MODE == 2;
   using G = AcffPGeom<CC>;
-  constexpr int TH = G::TH, TW = G::TW, HW = G::HW, PS = G::PS, CG = G::CG, KC = G::KC, AS = G::AS;
+  constexpr int TH = G::TH, TW = G::TW, HW = G::HW, PS = G::PS, CG = G::CG, KC = G::KC, AS = G::AS, RP = G::RP;
   constexpr int HALO = G::HALO, PV = G::PV, XS = G::XS;
   constexpr int KC8 = (3 * CC + 63) / 64 * 64, AS8 = KC8 + 16;  // int8 A tile: K per chunk, row bytes
   static_assert(!I8 || G::NPIX * AS8 <= G::NPIX * AS * 2, "int8 A tile reuses the fp16 one");
@@ -380,7 +385,10 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
       const int i = tid + 256 * k;
       if (i < HALO) {
         const int pix = i / CG, v = i - pix * CG;
-        *(u32x4*)(xb + pix * PS + v * 8) = pre[k];
+        const int r = pix / HW, c = pix - r * HW;
+        uint2* dst = (uint2*)(xb + r * RP + c * PS + v * 8);
+        dst[0] = make_uint2(pre[k][0], pre[k][1]);
+        dst[1] = make_uint2(pre[k][2], pre[k][3]);
       }
     }
   };
@@ -442,75 +450,75 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
       cal_ok = (ty * TH + py < oh ? 1 : 0) | (ty * TH + py + 4 < oh ? 2 : 0);
       if (tx * TW + px >= ow) cal_ok = 0;
     }
-    // ---- depthwise branches -> A tile (fp16, or int8 quantised per concat channel) ----
+    // ---- depthwise branches -> A tile (fp16, or int8 quantised per concat channel).
+    //      A wave owns 4 channels (c4) of BOTH 64-pixel halves (lane = pixel m and m + 64,
+    //      4 tile rows apart): each tap's 4 weights (one broadcast ds_read_b128) serve 8 FMAs,
+    //      half the weight reads per FMA of one pixel x 8 channels per lane (the weight reads
+    //      were 57 % of the kernel's LDS instructions; without them acff1 ran 15 % faster,
+    //      r05ah).  Every output takes the same operations in the same order. ----
 #pragma unroll
-    for (int u0 = 0; u0 < 2 * CG; u0 += 4) {
-      const int u = u0 + wid;
-      if (u < 2 * CG) {
-        const int cg = u % CG, pb = u / CG;
-        const int m = pb * 64 + lane;
+    for (int u0 = 0; u0 < CC / 4; u0 += 4) {
+      const int c4 = u0 + wid;
+      if (c4 < CC / 4) {
+        const int m = lane;  // pixel block 0; block 1 is m + 64, 4 rows down
         const int q = m >> 2, dq = m & 3;
         const int py = 2 * (q >> 3) + (dq >> 1), px = 2 * (q & 7) + (dq & 1);
-        const int cbase = ch * CC + cg * 8;
+        const int cbase = ch * CC + c4 * 4;
 #pragma unroll
         for (int br = 0; br < 3; ++br) {
           const int d = br + 1;
-          const float* bp = s_dw + (27 + br) * a.cin + cbase;
-          float s8[8];
-          {
-            const f4 b0 = *(const f4*)bp, b1 = *(const f4*)(bp + 4);
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-              s8[jj] = b0[jj];
-              s8[4 + jj] = b1[jj];
-            }
-          }
+          const f4 bb = *(const f4*)(s_dw + (27 + br) * a.cin + cbase);
+          float s0[4] = {bb[0], bb[1], bb[2], bb[3]}, s1[4] = {bb[0], bb[1], bb[2], bb[3]};
 #pragma unroll
           for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
             for (int kw = 0; kw < 3; ++kw) {
               if constexpr ((ABL & 1) != 0) continue;
               const int hr = py + 3 + (kh - 1) * d, hc = px + 3 + (kw - 1) * d;
-              const u32x4 xv = *(const u32x4*)(xb + (hr * HW + hc) * PS + cg * 8);
-              const float* wp = s_dw + (br * 9 + kh * 3 + kw) * a.cin + cbase;
-              f4 w0, w1;
+              const _Float16* xp = xb + hr * RP + hc * PS + c4 * 4;
+              const uint2 x0 = *(const uint2*)xp, x1 = *(const uint2*)(xp + 4 * RP);
+              f4 w;
               if constexpr ((ABL & 4) != 0) {  // (diagnostic: no tap-weight LDS reads)
-                w0 = f4{0.5f, 0.25f, 0.125f, 0.5f};
-                w1 = w0;
-                (void)wp;
+                w = f4{0.5f, 0.25f, 0.125f, 0.5f};
               } else {
-                w0 = *(const f4*)wp;
-                w1 = *(const f4*)(wp + 4);
+                w = *(const f4*)(s_dw + (br * 9 + kh * 3 + kw) * a.cin + cbase);
               }
-              const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
-#pragma unroll
-              for (int jj = 0; jj < 4; ++jj) {
-                s8[2 * jj] = fma_mix_lo_v(wv[2 * jj], xv[jj], s8[2 * jj]);
-                s8[2 * jj + 1] = fma_mix_hi_v(wv[2 * jj + 1], xv[jj], s8[2 * jj + 1]);
-              }
+              s0[0] = fma_mix_lo_v(w[0], x0.x, s0[0]);
+              s0[1] = fma_mix_hi_v(w[1], x0.x, s0[1]);
+              s0[2] = fma_mix_lo_v(w[2], x0.y, s0[2]);
+              s0[3] = fma_mix_hi_v(w[3], x0.y, s0[3]);
+              s1[0] = fma_mix_lo_v(w[0], x1.x, s1[0]);
+              s1[1] = fma_mix_hi_v(w[1], x1.x, s1[1]);
+              s1[2] = fma_mix_lo_v(w[2], x1.y, s1[2]);
+              s1[3] = fma_mix_hi_v(w[3], x1.y, s1[3]);
             }
           if constexpr (I8) {
-            const float* ip = s_dw + (30 + br) * a.cin + cbase;
-            uint32_t lo = 0, hi = 0;
+            const f4 is = *(const f4*)(s_dw + (30 + br) * a.cin + cbase);
+            uint32_t q0 = 0, q1 = 0;
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-              int v = (int)rintf(s8[jj] * ip[jj]);
-              v = v < -127 ? -127 : (v > 127 ? 127 : v);
-              if (jj < 4)
-                lo |= ((uint32_t)v & 255u) << (8 * jj);
-              else
-                hi |= ((uint32_t)v & 255u) << (8 * (jj - 4));
+            for (int jj = 0; jj < 4; ++jj) {
+              int v0 = (int)rintf(s0[jj] * is[jj]), v1 = (int)rintf(s1[jj] * is[jj]);
+              v0 = v0 < -127 ? -127 : (v0 > 127 ? 127 : v0);
+              v1 = v1 < -127 ? -127 : (v1 > 127 ? 127 : v1);
+              q0 |= ((uint32_t)v0 & 255u) << (8 * jj);
+              q1 |= ((uint32_t)v1 & 255u) << (8 * jj);
             }
-            *(uint2*)(At8 + m * AS8 + br * CC + cg * 8) = make_uint2(lo, hi);
+            *(uint32_t*)(At8 + m * AS8 + br * CC + c4 * 4) = q0;
+            *(uint32_t*)(At8 + (m + 64) * AS8 + br * CC + c4 * 4) = q1;
           } else {
-            h8 o;
+            typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+            h4v o0, o1;
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) o[jj] = (_Float16)s8[jj];
-            *(h8*)(At + m * AS + br * CC + cg * 8) = o;
+            for (int jj = 0; jj < 4; ++jj) {
+              o0[jj] = (_Float16)s0[jj];
+              o1[jj] = (_Float16)s1[jj];
+            }
+            *(h4v*)(At + m * AS + br * CC + c4 * 4) = o0;
+            *(h4v*)(At + (m + 64) * AS + br * CC + c4 * 4) = o1;
             if constexpr (CAL) {  // calibration: per concat channel |x|max over the wave's valid pixels
 #pragma unroll
-              for (int jj = 0; jj < 8; ++jj) {
-                float v = ((cal_ok >> pb) & 1) ? fabsf(s8[jj]) : 0.f;
+              for (int jj = 0; jj < 4; ++jj) {
+                float v = fmaxf((cal_ok & 1) ? fabsf(s0[jj]) : 0.f, (cal_ok & 2) ? fabsf(s1[jj]) : 0.f);
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
                 if (lane == 0 && v > 0.f) atomicMax(a.amax + br * a.cin + cbase + jj, __float_as_uint(v));
