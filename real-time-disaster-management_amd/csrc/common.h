@@ -249,6 +249,7 @@ struct ConvArgs {
   const void* w_stem = nullptr;  // MFMA stem (Cin=3, 3x3): fp16 [cout_pad][64] (pack_stem)
   const void* zero = nullptr;    // >= 16 zero bytes in device memory (glds padding source)
   FastDiv fd_cin;                // set by conv_set_rows
+  FastDiv fd_tx, fd_ty;          // conv3_pool_small: tiles per row / per column (set at its launch)
   int glds_uni = 0;              // conv_glds_f16: uniform-tap staging (set by launch_conv)
   int pipe_corder = 0;           // conv_pipe_f16: channel-block-outer K order (set by launch_conv_pipe)
   int pipe_g = 0;                // conv_pipe: N-panels per tile-walk group (0: M-major walk; set at launch)

@@ -1205,8 +1205,10 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : (CIN == 16 || WCH == 1) &&
   // (PF 2: twice the bytes in flight per CU; these layers are HBM-latency bound)
   u32x4 pre[PV], pre2[PF > 1 ? PV : 1];
   auto prefetch_to = [&](int tile, u32x4 (&dst)[PV]) {
-    const int tx = tile % tiles_x, t1 = tile / tiles_x;
-    const int ty = t1 % tiles_y, n = t1 / tiles_y;
+    // (tile -> (n, ty, tx) by multiply-shift: as integer divisions they were ~1/3 of the
+    // kernel's VALU)
+    const int t1 = fdiv(tile, a.fd_tx), tx = tile - t1 * tiles_x;
+    const int n = fdiv(t1, a.fd_ty), ty = t1 - n * tiles_y;
     const _Float16* base = in + (size_t)n * img;
     const int y0 = ty * TH - 1, x0 = tx * TW - 1;
 #pragma unroll
@@ -1233,8 +1235,8 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : (CIN == 16 || WCH == 1) &&
       for (int k = 0; k < PV; ++k)
         if (tid + NT * k < HALO) *(u32x4*)(xb_w + soff[k]) = pre[k];
       __syncthreads();
-      const int tx = tile % tiles_x, t1 = tile / tiles_x;
-      const int ty = t1 % tiles_y, n = t1 / tiles_y;
+      const int t1 = fdiv(tile, a.fd_tx), tx = tile - t1 * tiles_x;
+      const int n = fdiv(t1, a.fd_ty), ty = t1 - n * tiles_y;
       if (tile + tstep < tend) prefetch_to(tile + tstep, pre);  // in flight during the MFMAs
       const _Float16* xb = xb_w + (wr * WROWS * HW + p) * PS;
       f4 acc[WROWS][WCH];
@@ -1308,8 +1310,8 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : (CIN == 16 || WCH == 1) &&
       for (int k = 0; k < PV; ++k)
         if (tid + NT * k < HALO) *(u32x4*)(xb_w + soff[k]) = cur[k];
       __syncthreads();
-      const int tx = tile % tiles_x, t1 = tile / tiles_x;
-      const int ty = t1 % tiles_y, n = t1 / tiles_y;
+      const int t1 = fdiv(tile, a.fd_tx), tx = tile - t1 * tiles_x;
+      const int n = fdiv(t1, a.fd_ty), ty = t1 - n * tiles_y;
       if (tile + 2 * tstep < tend) prefetch_to(tile + 2 * tstep, cur);  // two tiles in flight
       // (the tile's MFMAs + pooled epilogue as in the PF 1 loop, written out: as a shared lambda
       // the compiler allocated ~27 more VGPRs, 135 -> 162)
@@ -1416,8 +1418,11 @@ static int cu_count() {
   return n;
 }
 
-static void launch_pool_small(const ConvArgs& a, hipStream_t s) {
-  const int th = a.cin == 16 ? 16 : 8;
+static void launch_pool_small(const ConvArgs& a_in, hipStream_t s) {
+  const int th = a_in.cin == 16 ? 16 : 8;
+  ConvArgs a = a_in;
+  a.fd_tx = make_fastdiv((a.ow + 15) / 16);
+  a.fd_ty = make_fastdiv((a.oh + th - 1) / th);
   if (a.cin == 64) {  // 8 waves, one 16-channel tile each
     const int64_t tiles64 = (int64_t)a.n * ((a.oh + 7) / 8) * ((a.ow + 15) / 16);
     RTDM_REQUIRE(tiles64 < (1ll << 31), RTDM_E_CAPACITY, "conv: too many tiles");
