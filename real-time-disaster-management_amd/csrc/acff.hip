@@ -920,8 +920,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
       }
       // one (pixel m, 8-channel group v) item: bias, then the 9 taps in (kh, kw) order (fp32
       // FMAs, acff_fused's sequence) -> the A chunk (fp16, or int8 quantised)
-      auto dw_item = [&](int m, int v, const f4 (&wk)[9][2], const f4 (&bk)[2]) {
-        const int oy = m / OH, ox = m - oy * OH;
+      auto dw_item = [&](int m, int oy, int ox, int v, const f4 (&wk)[9][2], const f4 (&bk)[2]) {
         float t[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -988,7 +987,19 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
         if (tid < pstep * CG) {
           f4 wk[9][2], bk[2];
           wtaps(v, wk, bk);
-          for (int m = tid / CG; m < M; m += pstep) dw_item(m, v, wk, bk);
+          // (pixel m -> (oy, ox) stepped, not divided: an integer division per item was ~20
+          // VALU against its 72 FMAs)
+          const int m0 = tid / CG, dq = pstep / OH, dr = pstep - dq * OH;
+          int oy = m0 / OH, ox = m0 - oy * OH;
+          for (int m = m0; m < M; m += pstep) {
+            dw_item(m, oy, ox, v, wk, bk);
+            ox += dr;
+            oy += dq;
+            if (ox >= OH) {
+              ox -= OH;
+              ++oy;
+            }
+          }
         }
       }
       __syncthreads();
