@@ -10,7 +10,7 @@
 // generic implicit-GEMM tiles (conv_mfma: 128 x 64, K-blocks of 64 gathered per tap through
 // registers) and the direct kernel (16 x 16 tiles, one Cin chunk, 8-byte NHWC stores) ran
 // them at 0.11 / 0.14 ms per b16 416 frame batch, 2-3x their HBM time.  Here:
-//   * a workgroup (4 waves) loads the 64 x 288 weights into LDS once and walks output tiles
+//   * a workgroup (4 waves; 8 at stride 2) loads the 64 x 288 weights into LDS once and walks output tiles
 //     (TH x 16 pixels, grid-stride), so the weights are not re-read per tile;
 //   * per tile the (TH-1)S+3 x 15S+3 halo (32 channels = 4 x 16 B per pixel) is staged
 //     through registers: the next tile's halo loads are issued before this tile's MFMAs;
@@ -33,21 +33,22 @@ namespace rtdm {
 constexpr int kC32TW = 16;  // tile columns (one fragment of pixels)
 constexpr int kC32WP = 304;  // weight row pitch (halfs)
 
-template <int S>
+template <int S, int NW = 4>  // NW: waves per workgroup
 struct C32Geom {
-  static constexpr int TH = S == 1 ? 16 : 8;  // tile rows (4 waves x RW rows)
-  static constexpr int RW = TH / 4;
+  static constexpr int RW = S == 1 ? 4 : 2;   // tile rows per wave
+  static constexpr int TH = NW * RW;          // tile rows
+  static constexpr int NT = 64 * NW;          // threads
   static constexpr int HR = (TH - 1) * S + 3, HW = (kC32TW - 1) * S + 3;
   static constexpr int PP = S == 1 ? 48 : 40;
   static constexpr int HALO = HR * HW * PP;        // halfs
   static constexpr int NVEC = HR * HW * 4;         // 16-byte vectors per halo
-  static constexpr int NV = (NVEC + 255) / 256;    // per thread
+  static constexpr int NV = (NVEC + NT - 1) / NT;  // per thread
   static constexpr size_t LDS = (size_t)(HALO + 64 * kC32WP) * 2;
 };
 
-template <int S, bool RES>
-__global__ __launch_bounds__(256) void conv3_c32(ConvArgs a, int ntiles) {
-  using G = C32Geom<S>;
+template <int S, bool RES, int NW>
+__global__ __launch_bounds__(64 * NW) void conv3_c32(ConvArgs a, int ntiles) {
+  using G = C32Geom<S, NW>;
   extern __shared__ __attribute__((aligned(16))) _Float16 c32_lds[];
   _Float16* const hs = c32_lds;
   _Float16* const ws = c32_lds + G::HALO;
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(256) void conv3_c32(ConvArgs a, int ntiles) {
     const int iy0 = ty * G::TH * S - 1, ix0 = tx * kC32TW * S - 1;
 #pragma unroll
     for (int k = 0; k < G::NV; ++k) {
-      const int v = tid + k * 256;
+      const int v = tid + k * G::NT;
       const int pix = v >> 2, c = v & 3;
       const int hr = pix / G::HW, col = pix - hr * G::HW;
       const int y = iy0 + hr, x = ix0 + col;
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(256) void conv3_c32(ConvArgs a, int ntiles) {
   auto hstore = [&](const u32x4 (&r)[G::NV]) {
 #pragma unroll
     for (int k = 0; k < G::NV; ++k) {
-      const int v = tid + k * 256;
+      const int v = tid + k * G::NT;
       if (v < G::NVEC) *(u32x4*)(hs + (v >> 2) * G::PP + (v & 3) * 8) = r[k];
     }
   };
@@ -89,7 +90,7 @@ __global__ __launch_bounds__(256) void conv3_c32(ConvArgs a, int ntiles) {
   u32x4 pre[G::NV];
   if (t < ntiles) hload(t, pre);
   // weights -> LDS, row q = 16n + i holds output channel (i/4)*16 + 4n + i%4 (k = tap*32 + c)
-  for (int v = tid; v < 64 * 36; v += 256) {
+  for (int v = tid; v < 64 * 36; v += G::NT) {
     const int q = v / 36, kv = v - q * 36;
     const int n = q >> 4, i = q & 15;
     const int co = (i >> 2) * 16 + 4 * n + (i & 3);
@@ -353,8 +354,13 @@ bool c32_ok(const ConvArgs& a) {
   return (int64_t)a.n * a.ih * a.iw * a.in_cs < (1ll << 31) && (int64_t)a.n * a.oh * a.ow * e.full.cs < (1ll << 31);
 }
 
+// waves per workgroup: stride 1 4 (70 KB of LDS, two workgroups per CU); stride 2 8, one
+// 126 KB workgroup per CU with a 16 x 16 output tile (the 4-wave 8 x 16 tile's 84 KB fits
+// only once per CU, leaving one wave per SIMD to hide the halo loads)
+constexpr int kC32NW1 = 4, kC32NW2 = 8;
+
 static int c32_tiles(const ConvArgs& a) {
-  const int th = a.stride == 1 ? C32Geom<1>::TH : C32Geom<2>::TH;
+  const int th = a.stride == 1 ? C32Geom<1, kC32NW1>::TH : C32Geom<2, kC32NW2>::TH;
   return a.n * ((a.oh + th - 1) / th) * ((a.ow + kC32TW - 1) / kC32TW);
 }
 
@@ -395,13 +401,15 @@ const char* c32_name(const ConvArgs& a) {
 
 template <int S, bool RES>
 static void launch_c32_t(const ConvArgs& a, int ntiles, hipStream_t s) {
+  constexpr int NW = S == 1 ? kC32NW1 : kC32NW2;
+  using G = C32Geom<S, NW>;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
     cus = 256;
   // workgroups per CU the LDS allows (160 KB per CU)
-  const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / C32Geom<S>::LDS);
+  const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / G::LDS);
   const int grid = std::min(ntiles, cus * per_cu);
-  hipLaunchKernelGGL((conv3_c32<S, RES>), dim3(grid), dim3(256), C32Geom<S>::LDS, s, a, ntiles);
+  hipLaunchKernelGGL((conv3_c32<S, RES, NW>), dim3(grid), dim3(G::NT), G::LDS, s, a, ntiles);
   RTDM_HIP(hipGetLastError());
 }
 
