@@ -51,7 +51,7 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "fuse_head") t.fuse_head = v ? 1 : 0;
   else if (k == "two_streams") t.two_streams = v ? 1 : 0;
   else if (k == "conv_c32") t.conv_c32 = v ? 1 : 0;
-  else if (k == "res_fuse") t.res_fuse = v < 0 ? 0 : v > 2 ? 2 : v;
+  else if (k == "res_fuse") t.res_fuse = v < 0 ? 0 : v > 3 ? 3 : v;
   else if (k == "stem_k16") t.stem_k16 = v ? 1 : 0;
   else if (k == "pool_sep") t.pool_sep = v ? 1 : 0;
   else if (k == "pool_small64") t.pool_small64 = v ? 1 : 0;

@@ -216,7 +216,7 @@ struct Tuning {
   int pool_small_pf = 0;    // conv3_pool_small halo tiles in flight per block (0 auto | 1 | 2)
   int stem_k16 = 1;         // pooled MFMA stem: the kh = 2 third of K as a 16-deep MFMA (0: 32-deep)
   int conv_c32 = 1;         // conv3_c32 for the Cin-32 3x3 convs (conv_c32.hip)
-  int res_fuse = 1;         // conv3_c32r: Darknet-53's first residual block as one launch (1: 8 waves, 2: 4 waves)
+  int res_fuse = 1;         // conv3_c32r (+ conv3_c64r): Darknet-53's residual blocks as one launch (1: c32r on 8 waves + c64r, 2: c32r on 4 waves, 3: c32r on 8 waves only)
 };
 Tuning& default_tuning();
 const Tuning& tune();
@@ -292,6 +292,8 @@ const char* c32_name(const ConvArgs& a);
 // ... and Darknet-53's first residual block (1x1 64 -> 32, 3x3 32 -> 64, shortcut) as one launch
 bool c32r_ok(const ConvArgs& a1, const ConvArgs& a);
 void launch_c32r(const ConvArgs& a1, const ConvArgs& a, hipStream_t s);
+bool c64r_ok(const ConvArgs& a1, const ConvArgs& a);
+void launch_c64r(const ConvArgs& a1, const ConvArgs& a, hipStream_t s);
 // int8 twin (RTDM_I8): a.in = quantised contiguous int8 copy of the input, a.w8 int8
 // weights (per-channel activation scales folded in), a.deq per-output-channel scales
 bool conv_pipe_i8_ok(const ConvArgs& a);

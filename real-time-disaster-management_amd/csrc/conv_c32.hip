@@ -341,6 +341,193 @@ __global__ __launch_bounds__(64 * NW) void conv3_c32r(ConvArgs a1, ConvArgs a, i
   }
 }
 
+// conv3_c64r: Darknet-53's 104 x 104 residual blocks (yolov3 / yolov3-spp blocks 2 and 3 at
+// 416: the 1x1 reduce 128 -> 64, Darknet.forward models.py:345-347, the 3x3 64 -> 128 and the
+// shortcut add :349-354) in one launch.  The 3x3's weights (128 x 576) do not fit in LDS
+// beside a halo, so each workgroup owns one half of its output channels (64 x 576 weights
+// resident, 74 KB) and the two halves of a tile run on workgroups b and b ^ 8, which sit on
+// the same XCD: the second half's reads of the block input X hit that XCD's L2.  Per 16 x 16
+// output tile:
+//   1. the 1x1 on the 18 x 18 halo pixels inside the image (21 fragments of 16 pixels over the
+//      8 waves, 4 k-steps of 32 channels in conv_mfma's order), its B operands straight from
+//      X in HBM / L2 (loaded for the next tile under this tile's 3x3), its weights in LDS;
+//      bias -> LeakyReLU (rounded to fp32) -> fp16 into the Y halo, zero outside the image;
+//   2. the 3x3 on the Y halo, taps 0..8 x two 32-channel k-steps (conv_pipe's K-blocks for
+//      Cin 64), bias -> LeakyReLU -> + X at the output pixel -> fp16 (epi_vec8_lean<true>).
+// Both halves compute the reduce (1.27 x the 1x1's MACs per half for the halo, +28 % MFMA
+// work); the Y map never reaches HBM: per output pixel 256 B of X in, 256 B out, against
+// 256 + 128 + 128 + 256 + 256 B for the two launches.  Bit-identical (tests/test_gpu_c32.py).
+constexpr int kC64rYP = 80;                     // Y halo pixel pitch (halfs)
+constexpr int kC64rWP = 592;                    // 3x3 weight row pitch (halfs: 576 + 16)
+constexpr int kC64rW1P = 144;                   // 1x1 weight row pitch (halfs: 128 + 16)
+constexpr int kC64rHP = 324;                    // halo pixels (18 x 18)
+constexpr int kC64rNF = (kC64rHP + 15) / 16;    // halo fragments (21)
+constexpr int kC64rFW = (kC64rNF + 7) / 8;      // fragments per wave (3)
+constexpr size_t kC64rLDS = (size_t)(kC64rHP * kC64rYP + 64 * kC64rWP + 64 * kC64rW1P) * 2;
+
+__global__ __launch_bounds__(512) void conv3_c64r(ConvArgs a1, ConvArgs a, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 c64r_lds[];
+  _Float16* const ys = c64r_lds;                  // Y halo [324][80]
+  _Float16* const ws = ys + kC64rHP * kC64rYP;    // this half's 3x3 weights [64][592]
+  _Float16* const w1s = ws + 64 * kC64rWP;        // 1x1 weights [64][144]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int half = (blockIdx.x >> 3) & 1;                         // output channels 64 half ..
+  const int pair = (blockIdx.x & 7) | ((blockIdx.x >> 4) << 3);   // b and b ^ 8: one XCD
+  const int npairs = gridDim.x >> 1;
+  const int tx_n = (a.ow + 15) >> 4, ty_n = (a.oh + 15) >> 4;
+  const _Float16* __restrict__ X = (const _Float16*)a1.in + a1.in_co;
+
+  auto tile_of = [&](int t, int& n, int& ty, int& tx) {
+    tx = t % tx_n;
+    const int t2 = t / tx_n;
+    ty = t2 % ty_n;
+    n = t2 / ty_n;
+  };
+  // this lane's X operands of the wave's halo fragments (zero outside the image)
+  auto xload = [&](int t, u32x4 (&xr)[kC64rFW][4]) {
+    int n, ty, tx;
+    tile_of(t, n, ty, tx);
+#pragma unroll
+    for (int fi = 0; fi < kC64rFW; ++fi) {
+      const int q = (wid + 8 * fi) * 16 + j;
+      const int hr = q / 18, col = q - hr * 18;
+      const int y = ty * 16 - 1 + hr, x = tx * 16 - 1 + col;
+      const bool ok = q < kC64rHP && (unsigned)y < (unsigned)a1.ih && (unsigned)x < (unsigned)a1.iw;
+      const _Float16* src = X + ((size_t)(n * a1.ih + y) * a1.iw + x) * a1.in_cs + g * 8;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        xr[fi][ks] = u32x4{0u, 0u, 0u, 0u};
+        if (ok) xr[fi][ks] = *(const u32x4*)(src + ks * 32);
+      }
+    }
+  };
+
+  int t = pair;
+  u32x4 xr[kC64rFW][4];
+  if (t < ntiles) xload(t, xr);
+  // 3x3 weights of this half: row q = 16n + i holds output channel 64 half + (i/4)*16 + 4n + i%4
+  for (int v = tid; v < 64 * 72; v += 512) {
+    const int q = v / 72, kv = v - q * 72;
+    const int n = q >> 4, i = q & 15;
+    const int co = 64 * half + (i >> 2) * 16 + 4 * n + (i & 3);
+    *(u32x4*)(ws + q * kC64rWP + kv * 8) = *(const u32x4*)((const _Float16*)a.w + (size_t)co * a.kpad + kv * 8);
+  }
+  // 1x1 weights: row q = 16n + i holds reduce channel (i/4)*16 + 4n + i%4
+  for (int v = tid; v < 64 * 16; v += 512) {
+    const int q = v >> 4, kv = v & 15;
+    const int n = q >> 4, i = q & 15;
+    const int co = (i >> 2) * 16 + 4 * n + (i & 3);
+    *(u32x4*)(w1s + q * kC64rW1P + kv * 8) = *(const u32x4*)((const _Float16*)a1.w + (size_t)co * a1.kpad + kv * 8);
+  }
+  const Epilogue& e1 = a1.e;
+  const Epilogue& e = a.e;
+  const int c0 = 64 * half + 16 * g;  // this lane's 16 output channels
+  float b1[16], bias[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    b1[q] = e1.bias ? e1.bias[16 * g + q] : 0.f;
+    bias[q] = e.bias ? e.bias[c0 + q] : 0.f;
+  }
+  const bool leaky1 = e1.act == ACT_LEAKY, leaky = e.act == ACT_LEAKY;
+  __syncthreads();  // weights visible
+
+  for (; t < ntiles; t += npairs) {
+    int n, ty, tx;
+    tile_of(t, n, ty, tx);
+    // ---- 1x1 reduce over the halo pixels -> Y halo ----
+#pragma unroll
+    for (int fi = 0; fi < kC64rFW; ++fi) {
+      const int f = wid + 8 * fi;
+      if (f >= kC64rNF) break;  // wave-uniform
+      f4 acc1[4];
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn) acc1[nn] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const h8 xb = __builtin_bit_cast(h8, xr[fi][ks]);
+#pragma unroll
+        for (int nn = 0; nn < 4; ++nn) {
+          const h8 wa = *(const h8*)(w1s + (nn * 16 + j) * kC64rW1P + ks * 32 + g * 8);
+          acc1[nn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa, xb, acc1[nn], 0, 0, 0);
+        }
+      }
+      const int q = f * 16 + j;
+      const int hr = q / 18, col = q - hr * 18;
+      const int y = ty * 16 - 1 + hr, x = tx * 16 - 1 + col;
+      const bool inside = (unsigned)y < (unsigned)a1.ih && (unsigned)x < (unsigned)a1.iw;
+      h8v yv[2];
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = 4 * nn + r;  // reduce channel 16g + qq
+          float v = acc1[nn][r] + b1[qq];
+          v = leaky1 ? (v > 0.f ? v : v * e1.slope) : v;
+          asm volatile("" : "+v"(v));  // (x * slope rounds to fp32 first, as in the other epilogues)
+          v = v * 1.f + 0.f;           // epi_vec8_lean's (absent) BN affine
+          yv[qq >> 3][qq & 7] = inside ? (_Float16)v : (_Float16)0.f;
+        }
+      if (q < kC64rHP) {
+        *(h8v*)(ys + q * kC64rYP + 16 * g) = yv[0];
+        *(h8v*)(ys + q * kC64rYP + 16 * g + 8) = yv[1];
+      }
+    }
+    if (t + npairs < ntiles) xload(t + npairs, xr);  // lands under the 3x3
+    __syncthreads();  // Y halo complete
+    // ---- 3x3 on the Y halo: wave rows 2 wid, 2 wid + 1 ----
+    f4 acc[2][4];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn) acc[f][nn] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kh = tap / 3, kw = tap % 3;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        h8 wf[4];
+#pragma unroll
+        for (int nn = 0; nn < 4; ++nn) wf[nn] = *(const h8*)(ws + (nn * 16 + j) * kC64rWP + tap * 64 + ks * 32 + g * 8);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const h8 xf = *(const h8*)(ys + ((2 * wid + f + kh) * 18 + j + kw) * kC64rYP + ks * 32 + g * 8);
+#pragma unroll
+          for (int nn = 0; nn < 4; ++nn) acc[f][nn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[nn], xf, acc[f][nn], 0, 0, 0);
+        }
+      }
+    }
+    const int ox = tx * 16 + j;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const int oy = ty * 16 + 2 * wid + f;
+      if (oy >= a.oh || ox >= a.ow) continue;
+      const size_t pix = ((size_t)n * a.oh + oy) * a.ow + ox;
+      const _Float16* rp = (const _Float16*)e.res.ptr + pix * e.res.cs + e.res.co + c0;
+      h8v rv[2];
+      rv[0] = *(const h8v*)rp;
+      rv[1] = *(const h8v*)(rp + 8);
+      h8v hv[2];
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = 4 * nn + r;  // channel c0 + q
+          float x = acc[f][nn][r] + bias[q];
+          x = leaky ? (x > 0.f ? x : x * e.slope) : x;
+          asm volatile("" : "+v"(x));
+          x = x * 1.f + 0.f;
+          x += (float)rv[q >> 3][q & 7];
+          hv[q >> 3][q & 7] = (_Float16)x;
+        }
+      _Float16* op = (_Float16*)e.full.ptr + pix * e.full.cs + e.full.co + c0;
+      *(h8v*)op = hv[0];
+      *(h8v*)(op + 8) = hv[1];
+    }
+    __syncthreads();  // Y halo reads done before the next tile's 1x1 stores
+  }
+}
+
 static bool view8(const View& v) { return ((v.cs | v.co) & 7) == 0; }
 
 bool c32_ok(const ConvArgs& a) {
@@ -391,6 +578,39 @@ void launch_c32r(const ConvArgs& a1, const ConvArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(conv3_c32r<4>, grid, dim3(256), kC32rLDS, s, a1, a, nt);
   else
     hipLaunchKernelGGL(conv3_c32r<8>, grid, dim3(512), kC32rLDS, s, a1, a, nt);
+  RTDM_HIP(hipGetLastError());
+}
+
+// The 104 x 104 residual pair: a1 = the 1x1 reduce (128 -> 64, reading X), a = the 3x3
+// (64 -> 128) reading a1's output with X as its residual view.
+bool c64r_ok(const ConvArgs& a1, const ConvArgs& a) {
+  if (tune().res_fuse != 1) return false;
+  if (a.in_kind != IN_NHWC || a.w_f32 || a.cin != 64 || a.cout != 128 || a.cout_pad != 128 || a.ks != 3 ||
+      a.stride != 1 || a.pad != 1 || a.quad || a.kpad < 576 || a.oh != a.ih || a.ow != a.iw)
+    return false;
+  const Epilogue& e = a.e;
+  if (!e.full.ptr || !e.res.ptr || e.pool.ptr || e.up.ptr || e.io || e.scale || e.act == ACT_SWISH) return false;
+  if (!view8(e.full) || !view8(e.res)) return false;
+  const Epilogue& e1 = a1.e;
+  if (a1.in_kind != IN_NHWC || a1.w_f32 || a1.ks != 1 || a1.stride != 1 || a1.pad != 0 || a1.quad) return false;
+  if (a1.cin != 128 || a1.cout != 64 || a1.cout_pad != 64 || a1.kpad < 128 || (a1.in_cs | a1.in_co) & 7) return false;
+  if (a1.in_cs < a1.in_co + 128 || e.res.cs < e.res.co + 128 || e.full.cs < e.full.co + 128) return false;
+  if (!e1.full.ptr || e1.pool.ptr || e1.up.ptr || e1.io || e1.res.ptr || e1.scale || e1.act == ACT_SWISH) return false;
+  if (a1.ih != a.ih || a1.iw != a.iw || a1.oh != a.ih || a1.ow != a.iw || a1.n != a.n) return false;
+  if (a.in != e1.full.ptr || a.in_cs != e1.full.cs || a.in_co != e1.full.co) return false;
+  if (a.e.res.ptr != a1.in || a.e.res.cs != a1.in_cs || a.e.res.co != a1.in_co) return false;
+  return (int64_t)a1.n * a1.ih * a1.iw * a1.in_cs < (1ll << 31) && (int64_t)a.n * a.oh * a.ow * e.full.cs < (1ll << 31);
+}
+
+void launch_c64r(const ConvArgs& a1, const ConvArgs& a, hipStream_t s) {
+  const int nt = a.n * ((a.oh + 15) / 16) * ((a.ow + 15) / 16);
+  if (nt <= 0) return;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  // one workgroup per CU (LDS); a multiple of 16 so that b and b ^ 8 pair every workgroup
+  const int grid = 16 * std::max(1, std::min(cus, 2 * nt) / 16);
+  hipLaunchKernelGGL(conv3_c64r, dim3(grid), dim3(512), kC64rLDS, s, a1, a, nt);
   RTDM_HIP(hipGetLastError());
 }
 

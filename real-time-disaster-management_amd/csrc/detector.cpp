@@ -709,9 +709,12 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
   for (size_t i = 0; i + 1 < h.steps.size(); ++i) {
     Step& a = h.steps[i];
     const Step& b = h.steps[i + 1];
+    // (64 -> 32 -> 64: conv3_c32r; 128 -> 64 -> 128: conv3_c64r)
+    const bool c32 = a.cin == 64 && a.cout == 32 && b.cin == 32 && b.cout == 64;
+    const bool c64 = a.cin == 128 && a.cout == 64 && b.cin == 64 && b.cout == 128;
     if (a.kind != ST_CONV || b.kind != ST_CONV || a.in_t < 0 || a.full_t < 0 || a.ks != 1 || a.stride != 1 ||
-        a.cin != 64 || a.cout != 32 || a.pool_t >= 0 || a.up_t >= 0 || a.res_t >= 0 || a.yolo >= 0 || a.head ||
-        a.acff || b.ks != 3 || b.stride != 1 || b.cin != 32 || b.cout != 64 || b.in_t != a.full_t ||
+        !(c32 || c64) || a.pool_t >= 0 || a.up_t >= 0 || a.res_t >= 0 || a.yolo >= 0 || a.head ||
+        a.acff || b.ks != 3 || b.stride != 1 || b.in_t != a.full_t ||
         b.res_t != a.in_t || b.pool_t >= 0 || b.up_t >= 0 || b.yolo >= 0 || b.head || b.acff)
       continue;
     bool other = h.tensors[a.full_t].home >= 0;
@@ -1001,11 +1004,15 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
       if (st.fuse_r && tune().res_fuse && st.q < 0 && h.steps[si + 1].q < 0) {
         const Step& nx = h.steps[si + 1];
         const ConvArgs b = run_args(h, nx, x, in_kind, n, io, raw);
-        if ((!two || nx.stream == st.stream) && c32r_ok(a, b)) {
+        const bool r32 = c32r_ok(a, b), r64 = !r32 && c64r_ok(a, b);
+        if ((!two || nx.stream == st.stream) && (r32 || r64)) {
           if (two)
             for (int d : nx.deps)
               if (h.steps[d].stream != nx.stream) RTDM_HIP(hipStreamWaitEvent(s, h.step_ev[d], 0));
-          launch_c32r(a, b, s);
+          if (r32)
+            launch_c32r(a, b, s);
+          else
+            launch_c64r(a, b, s);
           fused_next = true;
           h.fused_away.push_back(st.full_t);
         }
@@ -1376,26 +1383,28 @@ rtdm_status rtdm_detector_step_info(rtdm_detector h, int step, char* name, int n
     std::string nm;
     double f = 0, b = 0;
     step_info(*h, h->steps[step], nm, f, b);
-    // a fused residual pair (run_detector's conv3_c32r choice): the first step reports the
-    // launch (both layers' FLOPs), the second an empty step
-    const auto res_pair = [&](int i) {
-      if (i < 0 || i + 1 >= (int)h->steps.size()) return false;
+    // a fused residual pair (run_detector's conv3_c32r / conv3_c64r choice): the first step
+    // reports the launch (both layers' FLOPs), the second an empty step
+    const auto res_pair = [&](int i) -> int {  // 0: no, 32: conv3_c32r, 64: conv3_c64r
+      if (i < 0 || i + 1 >= (int)h->steps.size()) return 0;
       const Step& a = h->steps[i];
       const Step& c = h->steps[i + 1];
-      return a.fuse_r && tune().res_fuse && a.q < 0 && c.q < 0 && (!(h->two_streams && h->side) || c.stream == a.stream) &&
-             c32r_ok(geom_args(*h, a), geom_args(*h, c));
+      if (!(a.fuse_r && tune().res_fuse && a.q < 0 && c.q < 0 && (!(h->two_streams && h->side) || c.stream == a.stream)))
+        return 0;
+      const ConvArgs ga = geom_args(*h, a), gc = geom_args(*h, c);
+      return c32r_ok(ga, gc) ? 32 : c64r_ok(ga, gc) ? 64 : 0;
     };
-    if (res_pair(step)) {
+    if (const int rp = res_pair(step)) {
       const Step& a = h->steps[step];
       const Step& c = h->steps[step + 1];
       std::string n2;
       double f2 = 0, b2 = 0;
       step_info(*h, c, n2, f2, b2);
-      nm = "conv3_c32r";
+      nm = rp == 32 ? "conv3_c32r" : "conv3_c64r";
       f += f2;
       b = ((double)a.ih * a.iw * a.cin + (double)c.oh * c.ow * c.cout) * (double)esize_of(h->dtype);
-    } else if (res_pair(step - 1)) {
-      nm = "conv3_c32r:fused";
+    } else if (const int rq = res_pair(step - 1)) {
+      nm = rq == 32 ? "conv3_c32r:fused" : "conv3_c64r:fused";
       f = 0;
       b = 0;
     }

@@ -2,7 +2,8 @@
 32 -> 64 + shortcut) on conv3_c32 (csrc/conv_c32.hip, rtdm_set_tuning("conv_c32"), default
 on) against the kernels they ran on before (conv_mfma for L1, conv3_direct for L3), and the
 first residual block (L2 1x1 64 -> 32, L3, the shortcut) as one conv3_c32r launch
-("res_fuse", default on) against conv_mfma + conv3_c32.  Every path takes each tap's 32
+("res_fuse", default on) against conv_mfma + conv3_c32, and the two 104 x 104 residual blocks
+(1x1 128 -> 64, 3x3 64 -> 128, shortcut) as conv3_c64r launches against conv_mfma + conv_pipe.  Every path takes each tap's 32
 channels as one 32-deep MFMA (the 1x1's 64 channels as two), in order, then bias ->
 LeakyReLU (rounded to fp32) -> (+ residual) -> fp16, so the io must be BIT-IDENTICAL;
 batches of several images (halo tiles at every image border), 416 and 608 frames, and a
@@ -53,13 +54,17 @@ def _run(settings, img, b, seed):
 @pytest.mark.parametrize("img,b", [(416, 3), (608, 2)])
 def test_c32_bit_identical(img, b):
     x, outs, names = _run([{"conv_c32": 0, "res_fuse": 0}, {"conv_c32": 1, "res_fuse": 0},
-                           {"conv_c32": 1, "res_fuse": 1}], img, b, 811)
+                           {"conv_c32": 1, "res_fuse": 1}, {"conv_c32": 1, "res_fuse": 3}], img, b, 811)
     assert not any(nm.startswith("conv3_c32") for nm in names[0])
     c32 = [nm for nm in names[1] if nm.startswith("conv3_c32")]
     assert c32 == ["conv3_c32<2,false>", "conv3_c32<1,true>"], names[1][:6]
     c32r = [nm for nm in names[2] if nm.startswith("conv3_c32")]
     assert c32r == ["conv3_c32<2,false>", "conv3_c32r", "conv3_c32r:fused"], names[2][:6]
-    for k in (1, 2):
+    # the two 104 x 104 (416) / 152 x 152 (608) blocks on conv3_c64r; res_fuse 3 keeps them apart
+    assert [nm for nm in names[2] if nm.startswith("conv3_c64r")] == ["conv3_c64r", "conv3_c64r:fused"] * 2
+    assert not any(nm.startswith("conv3_c64r") for nm in names[3])
+    assert [nm for nm in names[3] if nm.startswith("conv3_c32")] == c32r
+    for k in (1, 2, 3):
         d = (outs[0] - outs[k]).abs()
         assert torch.equal(outs[0], outs[k]), (k, float(d[..., :4].max()), float(d[..., 4:].max()))
     # a frame alone (defaults): the same rows

@@ -412,7 +412,8 @@ def _layer_outputs(m, n_layers, n):
     refusals are skipped, each by its own status and message: a layer the plan never
     materialises (its map lives only inside a fused launch: rtdm_detector_layer_output refuses
     the shape query) and a map the last detect fused away at run time -- which must be exactly
-    the 1x1 reduce of each planned conv3_c32r pair (step name "conv3_c32r").  Anything else
+    the 1x1 reduce of each planned conv3_c32r / conv3_c64r pair (step names "conv3_c32r",
+    "conv3_c64r").  Anything else
     (capacity, bad layer, a new refusal) fails the test."""
     import ctypes
     from rtdm import _lib as L
@@ -421,7 +422,7 @@ def _layer_outputs(m, n_layers, n):
     for i in range(L.lib().rtdm_detector_num_steps(h)):
         nm, layer = ctypes.create_string_buffer(64), ctypes.c_int()
         L.check(L.lib().rtdm_detector_step_info(h, i, nm, 64, ctypes.byref(layer), None, None))
-        if nm.value == b"conv3_c32r":
+        if nm.value in (b"conv3_c32r", b"conv3_c64r"):
             runtime_fused.add(layer.value)
     out, skipped = {}, set()
     for i in range(n_layers):
