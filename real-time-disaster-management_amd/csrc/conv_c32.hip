@@ -429,7 +429,9 @@ __global__ __launch_bounds__(512) void conv3_c64r(ConvArgs a1, ConvArgs a, int n
     b1[q] = e1.bias ? e1.bias[16 * g + q] : 0.f;
     bias[q] = e.bias ? e.bias[c0 + q] : 0.f;
   }
-  const bool leaky1 = e1.act == ACT_LEAKY, leaky = e.act == ACT_LEAKY;
+  // LeakyReLU as max(x, slope x) (c64r_ok: 0 < slope <= 1; linear = slope 1): the same value
+  // as x > 0 ? x : slope x for every non-NaN x, -0 included, in one compare-free op
+  const float slp1 = e1.act == ACT_LEAKY ? e1.slope : 1.f, slp = e.act == ACT_LEAKY ? e.slope : 1.f;
   __syncthreads();  // weights visible
 
   for (; t < ntiles; t += npairs) {
@@ -463,11 +465,12 @@ __global__ __launch_bounds__(512) void conv3_c64r(ConvArgs a1, ConvArgs a, int n
         for (int r = 0; r < 4; ++r) {
           const int qq = 4 * nn + r;  // reduce channel 16g + qq
           float v = acc1[nn][r] + b1[qq];
-          v = leaky1 ? (v > 0.f ? v : v * e1.slope) : v;
+          v = fmaxf(v, v * slp1);
           asm volatile("" : "+v"(v));  // (x * slope rounds to fp32 first, as in the other epilogues)
           v = v * 1.f + 0.f;           // epi_vec8_lean's (absent) BN affine
-          yv[qq >> 3][qq & 7] = inside ? (_Float16)v : (_Float16)0.f;
+          yv[qq >> 3][qq & 7] = (_Float16)v;
         }
+      if (!inside) yv[0] = yv[1] = h8v{};
       if (q < kC64rHP) {
         *(h8v*)(ys + q * kC64rYP + 16 * g) = yv[0];
         *(h8v*)(ys + q * kC64rYP + 16 * g + 8) = yv[1];
@@ -514,7 +517,7 @@ __global__ __launch_bounds__(512) void conv3_c64r(ConvArgs a1, ConvArgs a, int n
         for (int r = 0; r < 4; ++r) {
           const int q = 4 * nn + r;  // channel c0 + q
           float x = acc[f][nn][r] + bias[q];
-          x = leaky ? (x > 0.f ? x : x * e.slope) : x;
+          x = fmaxf(x, x * slp);
           asm volatile("" : "+v"(x));
           x = x * 1.f + 0.f;
           x += (float)rv[q >> 3][q & 7];
@@ -592,6 +595,8 @@ bool c64r_ok(const ConvArgs& a1, const ConvArgs& a) {
   if (!e.full.ptr || !e.res.ptr || e.pool.ptr || e.up.ptr || e.io || e.scale || e.act == ACT_SWISH) return false;
   if (!view8(e.full) || !view8(e.res)) return false;
   const Epilogue& e1 = a1.e;
+  for (const Epilogue* ep : {&e, &e1})  // the kernel's max(x, slope x) LeakyReLU
+    if (ep->act == ACT_LEAKY && !(ep->slope > 0.f && ep->slope <= 1.f)) return false;
   if (a1.in_kind != IN_NHWC || a1.w_f32 || a1.ks != 1 || a1.stride != 1 || a1.pad != 0 || a1.quad) return false;
   if (a1.cin != 128 || a1.cout != 64 || a1.cout_pad != 64 || a1.kpad < 128 || (a1.in_cs | a1.in_co) & 7) return false;
   if (a1.in_cs < a1.in_co + 128 || e.res.cs < e.res.co + 128 || e.full.cs < e.full.co + 128) return false;
