@@ -103,7 +103,7 @@ __global__ __launch_bounds__(64 * NW) void conv3_c32(ConvArgs a, int ntiles) {
   float bias[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) bias[q] = cval && e.bias ? e.bias[c0 + q] : 0.f;
-  const bool leaky = e.act == ACT_LEAKY;
+  const float slp = e.act == ACT_LEAKY ? e.slope : 1.f;  // LeakyReLU as max(x, slope x) (c32_ok)
 
   for (; t < ntiles; t += gridDim.x) {
     hstore(pre);
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(64 * NW) void conv3_c32(ConvArgs a, int ntiles) {
         for (int r = 0; r < 4; ++r) {
           const int q = 4 * nn + r;  // channel c0 + q
           float x = acc[f][nn][r] + bias[q];
-          x = leaky ? (x > 0.f ? x : x * e.slope) : x;
+          x = fmaxf(x, x * slp);
           // (opaque: x * slope rounds to fp32 before the fp16 conversion, as in the other
           // epilogues, instead of folding into one single-rounding fp16-result mix op)
           asm volatile("" : "+v"(x));
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(64 * NW) void conv3_c32r(ConvArgs a1, ConvArgs a, i
   const int c0 = 16 * g;
 #pragma unroll
   for (int q = 0; q < 16; ++q) bias[q] = e.bias ? e.bias[c0 + q] : 0.f;
-  const bool leaky1 = e1.act == ACT_LEAKY, leaky = e.act == ACT_LEAKY;
+  const float slp1 = e1.act == ACT_LEAKY ? e1.slope : 1.f, slp = e.act == ACT_LEAKY ? e.slope : 1.f;
 
   for (; t < ntiles; t += gridDim.x) {
 #pragma unroll
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(64 * NW) void conv3_c32r(ConvArgs a1, ConvArgs a, i
         for (int r = 0; r < 4; ++r) {
           const int qq = 4 * nn + r;  // reduce channel 8g + qq
           float v = acc[nn][r] + b1[qq];
-          v = leaky1 ? (v > 0.f ? v : v * e1.slope) : v;
+          v = fmaxf(v, v * slp1);
           asm volatile("" : "+v"(v));  // (x * slope rounds to fp32 first, as in the other epilogues)
           v = v * 1.f + 0.f;           // epi_vec8_lean's (absent) BN affine
           yv[qq] = inside ? (_Float16)v : (_Float16)0.f;
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(64 * NW) void conv3_c32r(ConvArgs a1, ConvArgs a, i
         for (int r = 0; r < 4; ++r) {
           const int q = 4 * nn + r;
           float x = acc[f][nn][r] + bias[q];
-          x = leaky ? (x > 0.f ? x : x * e.slope) : x;
+          x = fmaxf(x, x * slp);
           asm volatile("" : "+v"(x));
           x = x * 1.f + 0.f;
           x += (float)rv[q >> 3][q & 7];
@@ -540,6 +540,7 @@ bool c32_ok(const ConvArgs& a) {
   if (a.oh != (a.ih + 2 - 3) / a.stride + 1 || a.ow != (a.iw + 2 - 3) / a.stride + 1) return false;
   const Epilogue& e = a.e;
   if (!e.full.ptr || e.pool.ptr || e.up.ptr || e.io || e.scale || e.act == ACT_SWISH) return false;
+  if (e.act == ACT_LEAKY && !(e.slope > 0.f && e.slope <= 1.f)) return false;  // max(x, slope x)
   if (!view8(e.full) || (e.res.ptr && !view8(e.res))) return false;
   return (int64_t)a.n * a.ih * a.iw * a.in_cs < (1ll << 31) && (int64_t)a.n * a.oh * a.ow * e.full.cs < (1ll << 31);
 }
@@ -562,6 +563,7 @@ bool c32r_ok(const ConvArgs& a1, const ConvArgs& a) {
   if (a1.in_kind != IN_NHWC || a1.w_f32 || a1.ks != 1 || a1.stride != 1 || a1.pad != 0 || a1.quad) return false;
   if (a1.cin != 64 || a1.cout != 32 || a1.cout_pad != 32 || a1.kpad < 64 || (a1.in_cs | a1.in_co) & 7) return false;
   if (!e1.full.ptr || e1.pool.ptr || e1.up.ptr || e1.io || e1.res.ptr || e1.scale || e1.act == ACT_SWISH) return false;
+  if (e1.act == ACT_LEAKY && !(e1.slope > 0.f && e1.slope <= 1.f)) return false;  // max(x, slope x)
   if (a1.ih != a.ih || a1.iw != a.iw || a1.oh != a.ih || a1.ow != a.iw || a1.n != a.n) return false;
   // a reads a1's output; a's residual is a1's input (same view)
   if (a.in != e1.full.ptr || a.in_cs != e1.full.cs || a.in_co != e1.full.co) return false;
