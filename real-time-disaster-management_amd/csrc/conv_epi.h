@@ -264,7 +264,7 @@ __device__ __forceinline__ void epi_vec8_lean(const ConvArgs& a, int m0, int c0,
   for (int j = 0; j < 8; ++j) pmax[j] = -INFINITY;
   int pn, poy, pox;
   row_to_pix(a, m0, pn, poy, pox);
-  const bool leaky = e.act == ACT_LEAKY;
+  const float slp = e.act == ACT_LEAKY ? e.slope : 1.f;  // max(t, slope t), as pipe_epi_regs
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int m = m0 + r;
@@ -278,7 +278,7 @@ __device__ __forceinline__ void epi_vec8_lean(const ConvArgs& a, int m0, int c0,
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = v[r][j] + bias[j];
-      t = leaky ? (t > 0.f ? t : t * e.slope) : t;
+      t = fmaxf(t, t * slp);
       t = t * sc[j] + sh[j];
       if constexpr (RES) t += (float)rv[j];
       hv[j] = (_Float16)t;
@@ -449,8 +449,10 @@ __device__ __forceinline__ void pipe_epi_regs(const ConvArgs& a, int m_base, int
   constexpr bool I8 = !std::is_same_v<AccT, f4>;
   const Epilogue& e = a.e;
   const int fr = lane & 15, g = lane >> 4;
-  const bool leaky = e.act == ACT_LEAKY;
-  const float slope = e.slope;
+  // LeakyReLU as max(t, slope t): the planner's slopes are 0.1 / 0.01 (detector.cpp), for which
+  // it equals t > 0 ? t : slope t on every non-NaN t (-0 included) without a compare + select;
+  // linear layers take slope 1
+  const float slp = e.act == ACT_LEAKY ? e.slope : 1.f;
   typedef _Float16 h4 __attribute__((ext_vector_type(4)));
   typedef int i2 __attribute__((ext_vector_type(2)));
   if constexpr (FIXED) {
@@ -480,7 +482,7 @@ __device__ __forceinline__ void pipe_epi_regs(const ConvArgs& a, int m_base, int
           else
             t[r] = acc[tm][tn][r];
           t[r] = t[r] + rb[tn][r];
-          t[r] = leaky ? (t[r] > 0.f ? t[r] : t[r] * slope) : t[r];
+          t[r] = fmaxf(t[r], t[r] * slp);
         }
         if constexpr (RES) {
           const int ro = ok ? (pix * e.res.cs + c0) * 2 : 0x7FFFFFF8;
@@ -521,7 +523,7 @@ __device__ __forceinline__ void pipe_epi_regs(const ConvArgs& a, int m_base, int
         else
           t[r] = acc[tm][tn][r];
         t[r] = t[r] + rb[tn][r];
-        t[r] = leaky ? (t[r] > 0.f ? t[r] : t[r] * slope) : t[r];
+        t[r] = fmaxf(t[r], t[r] * slp);
       }
       if (e.scale && cv) {
         const f4 sc = *(const f4*)(e.scale + c0), sh = *(const f4*)(e.shift + c0);
