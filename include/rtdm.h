@@ -145,8 +145,10 @@ const char* rtdm_build_arch(void);
  * panels (default 2, 0 = M-major); "conv_c32" 1 = the Cin-32 3x3 convs on conv3_c32
  * (default; bit-identical to 0 = conv_mfma / conv3_direct); "res_fuse" 1 =
  * Darknet-53's first residual block (1x1 64 -> 32, 3x3 32 -> 64, shortcut) as one
- * conv3_c32r launch, 8 waves (default; 2 = 4 waves; 0 = two launches; bit-identical;
- * the reduce map is then not materialised: layer_output refuses it); "stem_k16" 1 = the
+ * conv3_c32r launch, 8 waves, and each 104x104 (at 416) block (1x1 128 -> 64, 3x3
+ * 64 -> 128, shortcut) as one conv3_c64r launch (default; 2 = conv3_c32r on 4 waves
+ * only; 3 = conv3_c32r on 8 waves only; 0 = two launches per block; bit-identical; a
+ * fused reduce map is not materialised: layer_output refuses it); "stem_k16" 1 = the
  * Cin-3 MFMA stems with the kh = 2 third of K on a 16-deep MFMA (default; bit-identical
  * to 0 = a 32-deep one); "pool_small_pf" 0 = halo tiles in flight per conv3_pool_small
  * block by Cin (default: 2 for Cin 16, 1 for Cin 32) | 1 | 2 (bit-identical);
