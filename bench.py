@@ -8,7 +8,11 @@ run at 608x608; /255 fused), YOLO decode (fused into the head convs) and per-ima
 (conf 0.3, IoU 0.4, detect.py defaults).  Frames are resident in HBM before timing.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  N>1: `python bench.py --gpus N` starts N ranks itself (fresh child processes of this
+       script, one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, before any GPU
+       call; rank 0's JSON line is the output, a failing rank fails the run), or
+       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+       (then WORLD_SIZE must equal N);
        one rank per GPU; the global batch is frame-sharded (rank r processes frames
        [r*B/N, (r+1)*B/N), SURVEY.md §8e: 8 frames per GPU at N=8), weights are
        broadcast once over RCCL and every step ends with a gather of all ranks'
@@ -56,7 +60,13 @@ METRIC = "frames/sec two-stage (ErNET→YOLOv4) 608×608 b64 @1/2/4/8 GPU; top-1
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default WORLD_SIZE or 1.  > 1 without WORLD_SIZE: this script "
+                         "starts the N ranks itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher self-test (no GPU): the ranks join a gloo group and rank 0 prints one JSON "
+                         "line with every rank's launch environment")
+    ap.add_argument("--dry-fail-rank", type=int, default=-1, help="(--dry-run) this rank exits with status 3")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=64, help="global frames per step (sharded over the ranks)")
@@ -96,6 +106,77 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="CPU oracle leg: time chunks of 16 frames until this much CPU time has passed")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`--gpus N` (N > 1) without a launcher: start N fresh processes of this script, one per
+    GPU (the reference's multi-GPU inference takes every visible GPU,
+    yolov3/test.py:42-43).  Runs before anything touches the GPU, and never replaces this
+    process (children via subprocess, no exec).  Rank 0's JSON lines are relayed to our
+    stdout (the run's one line); everything else the ranks print (library banners such as
+    gloo's) goes to stderr.  Waits for all; if one fails, the others are stopped and the
+    run exits non-zero."""
+    import subprocess
+    import threading
+    port = free_port()
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr, text=r == 0))
+
+    def relay(f):
+        for line in f:
+            (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+            (sys.stdout if line.startswith("{") else sys.stderr).flush()
+    reader = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    reader.start()
+    rc, alive = 0, list(procs)
+    while alive:
+        for p in list(alive):
+            c = p.poll()
+            if c is None:
+                continue
+            alive.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with status {c}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in alive:
+                    q.terminate()
+                deadline = time.time() + 15
+                for q in alive:
+                    try:
+                        q.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+        time.sleep(0.05)
+    reader.join(timeout=10)
+    return rc
+
+
+def dry_run(args, world, rank):
+    """Launcher self-test: the ranks meet in a gloo group (CPU), rank 0 prints one line."""
+    import torch.distributed as dist
+    env = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    if rank == args.dry_fail_rank:
+        raise SystemExit(3)
+    envs = [env]
+    if world > 1:
+        dist.init_process_group("gloo")
+        envs = [None] * world
+        dist.all_gather_object(envs, env)
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "ranks": envs}), flush=True)
 
 
 def dist_setup():
@@ -340,6 +421,18 @@ def make_frames(args, first, count, dev):
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(env_world or 1)
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus {args.gpus}: need at least one rank")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))  # parent: starts the ranks, relays rank 0's line
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={env_world} but --gpus {args.gpus}: launch one rank per GPU "
+                         f"(--nproc-per-node {args.gpus}) or drop the launcher and let bench.py start them")
+    if args.dry_run:
+        return dry_run(args, args.gpus, int(os.environ.get("RANK", "0")))
     world, rank, local = dist_setup()
     dist = None
     if world > 1:

@@ -179,9 +179,16 @@ __device__ __forceinline__ void xcd_span(int bid, int nb, int ntiles, int& first
 // compiler's hazard model inserts no wait states for a full-register SrcC overlap whatever the
 // opcodes, and back to back the 16-deep link read a stale accumulator: NaN / wrong values in
 // round 4 (the swish stem, the channel-major stem).  sched_barrier keeps every chain's first
-// link before the fence and every second link after it (>= 1 independent MFMA in between),
-// and the s_nops add 16 wait states on top; this costs a few issue cycles per tile.
+// link before the fence and every second link after it.  With several chains (NTN > 1) at
+// least one independent MFMA sits between a chain's two links; with a single chain (the
+// non-pooled stem at NTN == 1: the classifiers' conv1, conv_stem3<false, 1, k16>) the two
+// s_nop 7 (16 wait states) are the ONLY guard.  16 covers the gfx950 requirement for an XDL
+// write followed by a SrcC read of a different opcode (the 16-pass 32-deep link's latency):
+// do not lower the nop count or lengthen the first link's MFMA shape without re-checking
+// tests/test_gpu_stem.py, which asserts bit-identity for that single-chain stem.
+constexpr int kMfmaOpcodeSwitchWaitStates = 16;  // the two s_nop 7 below (8 wait states each)
 __device__ __forceinline__ void mfma_opcode_switch() {
+  static_assert(kMfmaOpcodeSwitchWaitStates == 2 * 8, "keep the s_nop count in step with the hazard note");
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7" ::);
   __builtin_amdgcn_sched_barrier(0);
@@ -209,6 +216,8 @@ struct Tuning {
   int nms_variant = 0;      // NMS diagnostics
   int acff_persist = 1;     // acff_persist for the large-map ACFF stages (> 1: ablations)
   int acff_chain = 1;       // acff_chain for the small-map suffix
+  int acff_band = 1;        // acff_band for the small-map stages + tail (fp16 handles; before acff_chain; 2: only the chain's stages)
+  int acff_band_rows = 2;   // acff_band output rows per workgroup (non-tail stages)
   int fuse_head = 0;        // fused YOLO head convs (plan time; 0: the 3x3 on the unrolled window kernel + head1x1_f16, measured faster r04h)
   int two_streams = 1;      // detector head branches on a second stream (plan time)
   int pool_sep = 1;         // separable stride-1 max pools (K 5 / 9 / 13: the SPP block)
@@ -370,6 +379,22 @@ void launch_acff_chain(const AcffChainPlan& p, const void* in, int in_cs, int in
                        int pool_pad, int ph, int pwid, const float* fcw, const float* fcb, float* logits, float* probs,
                        hipStream_t s, const AcffI8* q = nullptr /* [nst]; int8: k = branch*cin + c */);
 int acff_chain_mode();  // 1 = use acff_chain when the plan allows (default), 0 = per-stage kernels + tail
+// acff_band.hip: one small-map ACFF stage per launch over output row bands (all output
+// channels per workgroup; optional 2x2 pool), the last stage with the classifier tail
+struct AcffBandTail {
+  const float* w2 = nullptr;  // conv2 [5][cout]
+  int pool_pad = 0, ph = 0, pw = 0;
+  const float* fcw = nullptr;
+  const float* fcb = nullptr;
+  float* logits = nullptr;
+  float* probs = nullptr;
+};
+bool acff_band_ok(int h, int w, int cin, int cout, int cout_pad, int kpad, int pool, bool tail);
+void launch_acff_band(const void* in, int in_cs, int in_co, int n, int h, int w, int cin, const float* dw_wt,
+                      const float* dw_b, const void* pw, int kpad, int cout, int cout_pad, const float* bias,
+                      const float* scale, const float* shift, float slope, void* out, int out_cs, int pool,
+                      const AcffBandTail* tail, hipStream_t s);
+int acff_band_mode();  // 1 = acff_band for the classifier's small-map stages + tail (default)
 int acff_persist_mode();
 void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, int stride, int pad, int zero_pad_rb,
                     View ov, int oh, int ow, int dtype, hipStream_t s);

@@ -859,6 +859,11 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     st.h_beta = st.h_gamma = st.h_mean = st.h_var = st.h_bias = st.h_W = nullptr;
   }
   for (YoloHead& y : h.heads) y.anchor_off = blob.add_f32(y.anchor_vec);
+  // the shared epilogues compute LeakyReLU as max(t, slope t), which is the reference's
+  // t > 0 ? t : slope t only for 0 < slope <= 1 (conv_epi.h)
+  for (const Step& st : h.steps)
+    RTDM_REQUIRE(st.kind != ST_CONV || (st.act != ACT_LEAKY && !st.acff) || (st.slope > 0.f && st.slope <= 1.f),
+                 RTDM_E_INVALID, "plan: LeakyReLU slope outside (0, 1] at layer " + std::to_string(st.layer));
   if (weights) {
     RTDM_HIP(hipGetDevice(&h.dev));
     h.blob.upload(blob);
@@ -1584,7 +1589,7 @@ rtdm_status rtdm_detector_layer_output(rtdm_detector h, int layer, int n, float*
     if (!out) return;
     RTDM_REQUIRE(std::find(h->fused_away.begin(), h->fused_away.end(), t) == h->fused_away.end(), RTDM_E_UNSUPPORTED,
                  "layer_output: layer " + std::to_string(layer) +
-                     " output was fused away in the last detect (conv3_c32r; rtdm_detector_set_tuning res_fuse 0 keeps it)");
+                     " output was fused away in the last detect (conv3_c32r / conv3_c64r; rtdm_detector_set_tuning res_fuse 0 keeps it)");
     RTDM_REQUIRE(n > 0 && n <= h->last_n, RTDM_E_INVALID, "layer_output: n exceeds the last detect batch");
     RTDM_REQUIRE(out_numel >= (int64_t)n * x.c * x.h * x.w, RTDM_E_CAPACITY, "layer_output: out too small");
     launch_to_nchw_f32(tensor_view(*h, t), n, x.h, x.w, x.c, out, h->dtype, (hipStream_t)stream);

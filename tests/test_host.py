@@ -1,12 +1,13 @@
 """CPU: host-side logic — weight formats, synthetic data determinism, frame
 sharding and the multi-process (gloo, world_size 2) weight broadcast / result gather."""
 import os
+import sys
 
 import numpy as np
 import pytest
 import torch
 
-from conftest import cfg_text
+from conftest import ROOT, cfg_text
 
 
 def test_synth_frames_deterministic_and_shardable():
@@ -283,3 +284,42 @@ def test_two_rank_gloo_map_harness_shards():
             assert seen == n
             assert np.allclose(vals, g[f"eval/{name}/result"], rtol=0, atol=1e-12), (name, vals)
             assert np.allclose(maps, g[f"eval/{name}/maps"], rtol=0, atol=1e-12)
+
+
+def _bench(args, env_extra=None, timeout=180):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_bench_gpus_n_starts_n_ranks():
+    """`bench.py --gpus 2` starts two ranks itself (no torch.distributed.run), each with its
+    own RANK / LOCAL_RANK and the shared WORLD_SIZE / MASTER_*, and the parent prints exactly
+    one JSON line, rank 0's, with n_gpus 2 (yolov3/test.py:42-43)."""
+    import json
+    r = _bench(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["dry_run"] is True
+    envs = rec["ranks"]
+    assert [e["RANK"] for e in envs] == ["0", "1"] and [e["LOCAL_RANK"] for e in envs] == ["0", "1"]
+    assert all(e["WORLD_SIZE"] == "2" and e["MASTER_ADDR"] == "127.0.0.1" for e in envs)
+    assert envs[0]["MASTER_PORT"] == envs[1]["MASTER_PORT"]
+
+
+def test_bench_rank_failure_propagates():
+    r = _bench(["--gpus", "2", "--dry-run", "--dry-fail-rank", "1"])
+    assert r.returncode != 0
+    assert "rank 1 exited with status 3" in r.stderr
+    assert r.stdout.strip() == ""
+
+
+def test_bench_world_size_must_match_gpus():
+    r = _bench(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in r.stderr
+    r = _bench(["--dry-run"])  # no --gpus, no launcher: one rank
+    assert r.returncode == 0 and '"n_gpus": 1' in r.stdout
