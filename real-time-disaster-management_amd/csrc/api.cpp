@@ -58,6 +58,8 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "pool_small_pf") t.pool_small_pf = v <= 0 ? 0 : v >= 2 ? 2 : 1;
   else if (k == "acff_persist") t.acff_persist = v < 0 ? 0 : v;
   else if (k == "acff_chain") t.acff_chain = v;
+  else if (k == "acff_band") t.acff_band = v < 0 ? 0 : v > 2 ? 2 : v;
+  else if (k == "acff_band_rows") t.acff_band_rows = v < 1 ? 1 : v > 16 ? 16 : v;
   else if (k == "stem_abl") t.stem_abl = v;
   else if (k == "nms_variant") t.nms_variant = v;
   else if (k == "resize_stream") t.resize_stream = v;

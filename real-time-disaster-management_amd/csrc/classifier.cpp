@@ -66,6 +66,9 @@ struct rtdm_classifier_s {
   size_t resize_tmp_bytes = 0;
   // stages [chain_start, end) + tail run as one acff_chain launch (-1: none)
   int chain_start = -1;
+  // stages [band_start, end) run as acff_band launches, the last with the tail (-1: none;
+  // fp16 handles; takes precedence over the chain when acff_band_mode())
+  int band_start = -1;
   rtdm::AcffChainPlan chain;
   // RTDM_I8: fp16 activations everywhere, int8 1x1 fusion GEMMs in the persistent and
   // chained ACFF stages once calibrated (rtdm_classifier_calibrate); calibrating = the
@@ -324,6 +327,20 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
       }
     }
   }
+  // ---- small-map stages on acff_band (fp16): the last stage with the tail, earlier ones with
+  //      maps up to 32 rows, pooled or not, as long as each is a plain ACFF (no reducer) ----
+  if (f16 && !h.int8) {
+    int first = (int)h.stages.size();
+    while (first > 0) {
+      const AcffStage& st = h.stages[first - 1];
+      const bool last = first == (int)h.stages.size();
+      if (st.red || !st.affine || (!last && st.oh > 32) || (last && st.pool) ||
+          !acff_band_ok(st.h, st.w, st.cin, st.cout, st.pw.cout_pad, st.pw.kpad, st.pool ? 1 : 0, last))
+        break;
+      --first;
+    }
+    if (first < (int)h.stages.size()) h.band_start = first;
+  }
   if (h.int8) {  // int8 slots for the persistent stages and (all or none of) the chained ones
     bool chain_q = h.chain_start >= 0;
     for (int i = std::max(0, h.chain_start); chain_q && i < (int)h.stages.size(); ++i)
@@ -467,7 +484,11 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
     q.inv_s = h.blob.at<float>(st.inv_off);
     return &q;
   };
+  const bool band = h.band_start >= 0 && acff_band_mode() && !h.calibrating;
+  // acff_band 2 (tests): bands only from the chain's first stage, so the result is the chain's bit for bit
+  const int band_start = acff_band_mode() == 2 ? std::max(h.band_start, h.chain_start) : h.band_start;
   for (size_t si = 0; si < h.stages.size(); ++si) {
+    if (band && (int)si == band_start) break;
     if (chain && (int)si == h.chain_start) break;
     const AcffStage& st = h.stages[si];
     const int lim = st.pool || st.red_pool ? (st.oh / 2) * 2 : st.oh;
@@ -559,7 +580,8 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
     g.w_f32 = st.pw.mfma ? 0 : 1;
     g.e.bias = h.blob.at<float>(st.pw.b_off);
     g.e.act = ACT_LEAKY;
-    g.e.slope = 0.01f;
+    g.e.slope = 0.01f;  // ACFF's LeakyReLU(0.01); the epilogues' max(t, slope t) needs 0 < slope <= 1
+    RTDM_REQUIRE(g.e.slope > 0.f && g.e.slope <= 1.f, RTDM_E_INVALID, "classifier: LeakyReLU slope outside (0, 1]");
     if (st.affine) {
       g.e.scale = h.blob.at<float>(st.pw.s_off);
       g.e.shift = h.blob.at<float>(st.pw.t_off);
@@ -623,6 +645,33 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       seg_end();
       cur = View{buf(st.red_buf), st.redw.cout, 0};
     }
+  }
+  if (band) {
+    for (size_t si = band_start; si < h.stages.size(); ++si) {
+      const AcffStage& st = h.stages[si];
+      const bool last = si + 1 == h.stages.size();
+      AcffBandTail tl;
+      if (last) {
+        tl.w2 = h.blob.at<float>(h.tail_w2);
+        tl.pool_pad = h.tail_pool_pad;
+        tl.ph = h.tail_ph;
+        tl.pw = h.tail_pw;
+        tl.fcw = h.blob.at<float>(h.tail_fcw);
+        tl.fcb = h.blob.at<float>(h.tail_fcb);
+        tl.logits = logits;
+        tl.probs = probs;
+      }
+      const int lo = st.pool ? (st.oh / 2) * (st.ow / 2) : st.oh * st.ow;
+      seg("acff" + std::to_string(si + 1) + (last ? "+tail" : ""),
+          nb * ((double)st.h * st.w * st.cin * es + (last ? 2.0 * 5 * 4 : (double)lo * st.cout * es)));
+      launch_acff_band(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, h.blob.at<float>(st.dw_wt),
+                       h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pw.w_off), st.pw.kpad, st.cout, st.pw.cout_pad,
+                       h.blob.at<float>(st.pw.b_off), h.blob.at<float>(st.pw.s_off), h.blob.at<float>(st.pw.t_off),
+                       0.01f, last ? nullptr : buf(st.out_buf), st.cout, st.pool ? 1 : 0, last ? &tl : nullptr, s);
+      seg_end();
+      cur = View{buf(st.out_buf), st.cout, 0};
+    }
+    return;
   }
   if (chain) {
     const int k = h.chain.nst;
@@ -782,9 +831,12 @@ int64_t rtdm_classifier_describe(rtdm_classifier h, char* buf, int64_t buf_len) 
     s += std::string("conv1 kernel ") + conv_kernel_name(a, h->dtype) + "\n";
   }
   const bool chain = h->chain_start >= 0 && acff_chain_mode();
+  const bool band = h->band_start >= 0 && acff_band_mode();
   for (int i = 0; i < (int)h->stages.size(); ++i) {
     const AcffStage& st = h->stages[i];
-    const char* k = chain && i >= h->chain_start                     ? "acff_chain"
+    const int band_start = acff_band_mode() == 2 ? std::max(h->band_start, h->chain_start) : h->band_start;
+    const char* k = band && i >= band_start                          ? "acff_band"
+                    : chain && i >= h->chain_start                   ? "acff_chain"
                     : st.persist_cc && (acff_persist_mode() || st.q8) ? "acff_persist"
                     : st.fused                                        ? "acff_fused"
                                                                       : "dw3+gemm";

@@ -216,7 +216,7 @@ struct Tuning {
   int nms_variant = 0;      // NMS diagnostics
   int acff_persist = 1;     // acff_persist for the large-map ACFF stages (> 1: ablations)
   int acff_chain = 1;       // acff_chain for the small-map suffix
-  int acff_band = 1;        // acff_band for the small-map stages + tail (fp16 handles; before acff_chain; 2: only the chain's stages)
+  int acff_band = 0;        // acff_band for the small-map stages + tail (fp16 handles; before acff_chain; 2: only the chain's stages). Off: -2.5 % in the b64 bench, neutral at b8 (r06c)
   int acff_band_rows = 2;   // acff_band output rows per workgroup (non-tail stages)
   int fuse_head = 0;        // fused YOLO head convs (plan time; 0: the 3x3 on the unrolled window kernel + head1x1_f16, measured faster r04h)
   int two_streams = 1;      // detector head branches on a second stream (plan time)
@@ -394,7 +394,7 @@ void launch_acff_band(const void* in, int in_cs, int in_co, int n, int h, int w,
                       const float* dw_b, const void* pw, int kpad, int cout, int cout_pad, const float* bias,
                       const float* scale, const float* shift, float slope, void* out, int out_cs, int pool,
                       const AcffBandTail* tail, hipStream_t s);
-int acff_band_mode();  // 1 = acff_band for the classifier's small-map stages + tail (default)
+int acff_band_mode();  // 1 = acff_band for the classifier's small-map stages + tail, 2 = only the chain's stages, 0 = off (default)
 int acff_persist_mode();
 void launch_maxpool(const void* in, View iv, int n, int h, int w, int c, int k, int stride, int pad, int zero_pad_rb,
                     View ov, int oh, int ow, int dtype, hipStream_t s);

@@ -142,18 +142,56 @@ def test_classifier_acff_chain_matches_per_stage(dev, name, cls_weights):
     frames = torch.from_numpy(synth_frames(37, 608, 608, seed=5)).to(dev)
     out = {}
     try:
+        L.check(L.lib().rtdm_set_tuning(b"acff_band", 0))  # the chain, not the banded stages
         for mode in (0, 1):
             L.check(L.lib().rtdm_set_tuning(b"acff_chain", mode))
             m = _model(name, cls_weights[name], half=True)
+            assert ("acff_chain" in m.describe(37)) == (mode == 1)
             probs = m.classify_frames(frames)
             out[mode] = (m.logits.clone(), probs.clone())
     finally:
         L.check(L.lib().rtdm_set_tuning(b"acff_chain", 1))
+        L.check(L.lib().rtdm_set_tuning(b"acff_band", 0))
     a, b = out[0][0], out[1][0]
     scale = a.abs().max(1, keepdim=True).values
     assert bool(((a - b).abs() <= 1e-4 * scale).all()), ((a - b).abs() / scale).max()
     assert torch.equal(a.argmax(1), b.argmax(1))
     assert torch.allclose(out[0][1], out[1][1], atol=1e-4)
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_acff_band_bit_identical_to_chain(dev, name, cls_weights):
+    """acff_band (opt-in: the small-map stages one launch each over output row bands, the
+    tail fused into the last; ernet.py:25-45, acff.py:37-59) against acff_chain (one
+    workgroup per image, the default).  On the chain's own stages (acff_band 2) the two run the same operations in the
+    same order: logits and probabilities bit-identical, at b37 (ragged) and per frame.  With
+    the banded pooled stage before them as well (acff_band 1: acff3 leaves
+    acff_persist, whose 1x1 runs in another K order) the logits stay within 1e-3 of
+    max|logit| (the fp16 bar is 2e-2) with the same class ids, and every frame's row is
+    bit-identical to the frame run alone."""
+    from rtdm import _lib as L
+    from rtdm.synth import synth_frames
+    frames = torch.from_numpy(synth_frames(37, 608, 608, seed=11)).to(dev)
+    out = {}
+    try:
+        for band in (0, 2, 1):
+            L.check(L.lib().rtdm_set_tuning(b"acff_band", band))
+            m = _model(name, cls_weights[name], half=True)
+            desc = m.describe(37)
+            assert ("acff_band" in desc) == (band > 0), desc
+            probs = m.classify_frames(frames)
+            out[band] = (m.logits.clone(), probs.clone())
+            if band == 1:
+                for i in (0, 17, 36):
+                    m.classify_frames(frames[i:i + 1].contiguous())
+                    assert torch.equal(m.logits[0], out[1][0][i]), i
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"acff_band", 0))
+    assert torch.equal(out[0][0], out[2][0]) and torch.equal(out[0][1], out[2][1])
+    a, b = out[0][0], out[1][0]
+    scale = a.abs().max(1, keepdim=True).values
+    assert bool(((a - b).abs() <= 1e-3 * scale).all()), ((a - b).abs() / scale).max()
+    assert torch.equal(a.argmax(1), b.argmax(1))
 
 
 def test_redconv_config2_b32(dev, cls_weights):
