@@ -31,6 +31,8 @@
  *   rtdm_letterbox           <- letterbox()             victim_localization/yolov3/utils/datasets.py:599-631
  *   rtdm_resize_linear       <- cv2.resize(frame, (w, h)) disaster_detection/real-time-inference.py:185
  *   rtdm_preprocess_frames   <- squeeze_transforms / aider_transforms  disaster_detection/dataloaders/aider.py:412-431
+ *   rtdm_jpeg_*              <- cv2.imread(path)        victim_localization/yolov3/utils/datasets.py:97,
+ *                                                       disaster_detection/aider-predict.py:57
  *
  * Conventions
  *   - Plain C types only.  Device pointers are HIP device pointers owned by the
@@ -331,6 +333,37 @@ rtdm_status rtdm_letterbox(const uint8_t* frames, int n, int in_h, int in_w, int
  * on a pixel.  swap_rb = 1 also turns BGR into RGB (the cv2.cvtColor of :70).       */
 rtdm_status rtdm_resize_linear(const uint8_t* frames, int n, int in_h, int in_w, int pitch, int out_h, int out_w,
                                int swap_rb, uint8_t* out, void* stream);
+
+/* ---- JPEG frame decode (cv2.imread: yolov3/utils/datasets.py:97, aider-predict.py:57) ----
+ * Baseline / extended sequential 8-bit Huffman JPEGs (SOF0 / SOF1), 1 or 3 components,
+ * 4:4:4, 4:2:2 (h2v1) or 4:2:0 (h2v2) sampling, restart intervals, interleaved or
+ * per-component scans.  Split as the data dictates: the bit-serial entropy decode on the
+ * host (rtdm_jpeg_entropy_decode, into int16 coefficient blocks, natural order), the
+ * per-block / per-pixel rest on the device (rtdm_jpeg_reconstruct: dequantisation, islow
+ * IDCT, fancy upsampling, YCbCr -> RGB), bit-exact with libjpeg-turbo's default
+ * decompression (JDCT_ISLOW, do_fancy_upsampling), i.e. with what cv2.imread and Pillow
+ * return.  Progressive / arithmetic / 12-bit streams: supported = 0 and RTDM_E_UNSUPPORTED.
+ *
+ * rtdm_jpeg_info_get: geometry from the headers (no entropy decode).
+ * rtdm_jpeg_entropy_decode: coef [nblocks][64] int16 (host memory, component c's block
+ *   (by, bx) at coef_off[c] + by * bw[c] + bx), qt [ncomp][64] uint16 natural order.
+ * rtdm_jpeg_reconstruct: coef / qt device copies -> rgb [height][pitch] uint8 (3 bytes per
+ *   pixel, RGB, or BGR as cv2 with bgr = 1); planes: device workspace of
+ *   rtdm_jpeg_workspace_bytes(info) bytes (the component sample planes).              */
+typedef struct rtdm_jpeg_info {
+  int width, height, ncomp;
+  int h[3], v[3];        /* sampling factors */
+  int bw[3], bh[3];      /* coefficient block grid of each component (MCU-padded) */
+  int64_t coef_off[3];   /* first block of each component */
+  int64_t nblocks;       /* coefficient buffer: nblocks * 64 int16 */
+  int supported;         /* 1: decodable by rtdm_jpeg_entropy_decode + rtdm_jpeg_reconstruct */
+} rtdm_jpeg_info;
+rtdm_status rtdm_jpeg_info_get(const uint8_t* data, int64_t len, rtdm_jpeg_info* info);
+rtdm_status rtdm_jpeg_entropy_decode(const uint8_t* data, int64_t len, int16_t* coef, int64_t nblocks, uint16_t* qt,
+                                     rtdm_jpeg_info* info);
+int64_t rtdm_jpeg_workspace_bytes(const rtdm_jpeg_info* info);
+rtdm_status rtdm_jpeg_reconstruct(const int16_t* coef, const uint16_t* qt, const rtdm_jpeg_info* info, uint8_t* planes,
+                                  int64_t planes_bytes, uint8_t* rgb, int64_t pitch, int bgr, void* stream);
 
 #ifdef __cplusplus
 }

@@ -20,15 +20,14 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import torch  # noqa: E402
 
 from rtdm.classifier import load_model  # noqa: E402
-from rtdm.cli import calibration_frames, predict_frames, read_image_rgb, select_device  # noqa: E402
+from rtdm.cli import calibration_frames, load_image, predict_frames, read_image_rgb, select_device  # noqa: E402
 
 logger = logging.getLogger(__name__)
 
 
 def predict(model, image_path, device):
     """aider-predict.py:47-86 counterpart -> (class name, confidence %)."""
-    img = read_image_rgb(image_path)
-    frames = torch.from_numpy(img[None]).to(device)
+    frames = load_image(image_path, device)[None]  # JPEGs decoded on the device
     _, names, conf = predict_frames(model, frames)
     return names[0], conf[0]
 

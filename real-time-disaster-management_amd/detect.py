@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from rtdm.cli import list_images, read_image_rgb, select_device  # noqa: E402
+from rtdm.cli import list_images, load_image, select_device  # noqa: E402
 from rtdm.darknet import Darknet, load_darknet_weights  # noqa: E402
 from rtdm.letterbox import geometry, letterbox, letterbox_frames, scale_coords  # noqa: E402,F401
 from rtdm.nms import non_max_suppression  # noqa: E402
@@ -64,10 +64,10 @@ def detect(opt):
     t0 = time.time()
     results = {}
     for path in list_images(opt.source):
-        im0 = read_image_rgb(path)
-        # source frame up at its own size; letterbox (INTER_AREA resize + pad) on the device
-        g = geometry(im0.shape[0], im0.shape[1], opt.img_size, auto=True)
-        x = letterbox_frames(torch.from_numpy(im0[None]).to(device), g)  # uint8 NHWC; /255 fused in the stem
+        x0 = load_image(path, device)  # JPEGs decoded on the device (rtdm.jpeg), others via Pillow
+        # letterbox (INTER_AREA resize + pad) on the device
+        g = geometry(x0.shape[0], x0.shape[1], opt.img_size, auto=True)
+        x = letterbox_frames(x0[None], g)  # uint8 NHWC; /255 fused in the stem
         img_shape = (g[2], g[3])
         torch.cuda.synchronize()
         t1 = time.time()
@@ -81,7 +81,7 @@ def detect(opt):
         rows = []
         if det is not None and len(det):
             det = det.cpu()
-            det[:, :4] = scale_coords(img_shape, det[:, :4], im0.shape).round()
+            det[:, :4] = scale_coords(img_shape, det[:, :4], tuple(x0.shape)).round()
             for c in det[:, -1].unique():
                 n = int((det[:, -1] == c).sum())
                 s += '%g %ss, ' % (n, names[int(c)])
@@ -92,7 +92,7 @@ def detect(opt):
                         f.write(('%g ' * 6 + '\n') % (*xyxy, cls, conf))
             if not opt.no_save_img:
                 from PIL import Image, ImageDraw
-                im = Image.fromarray(im0)
+                im = Image.fromarray(x0.cpu().numpy())
                 d = ImageDraw.Draw(im)
                 for x1, y1, x2, y2, cls, conf in rows:
                     d.rectangle([x1, y1, x2, y2], outline=(255, 0, 0), width=2)

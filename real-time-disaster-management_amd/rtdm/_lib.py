@@ -55,6 +55,12 @@ class rtdm_detector_info(ctypes.Structure):
                 ("device_bytes", c_int64), ("flop_per_image", c_double)]
 
 
+class rtdm_jpeg_info(ctypes.Structure):
+    _fields_ = [("width", c_int), ("height", c_int), ("ncomp", c_int), ("h", c_int * 3), ("v", c_int * 3),
+                ("bw", c_int * 3), ("bh", c_int * 3), ("coef_off", c_int64 * 3), ("nblocks", c_int64),
+                ("supported", c_int)]
+
+
 # name -> (restype, argtypes); must match include/rtdm.h exactly
 SIGNATURES = {
     "rtdm_abi_version": (c_int, []),
@@ -100,6 +106,11 @@ SIGNATURES = {
     "rtdm_letterbox": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_uint32, c_int, c_void_p, c_void_p]),
     "rtdm_resize_linear": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "rtdm_jpeg_info_get": (c_int, [c_void_p, c_int64, POINTER(rtdm_jpeg_info)]),
+    "rtdm_jpeg_entropy_decode": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, POINTER(rtdm_jpeg_info)]),
+    "rtdm_jpeg_workspace_bytes": (c_int64, [POINTER(rtdm_jpeg_info)]),
+    "rtdm_jpeg_reconstruct": (c_int, [c_void_p, c_void_p, POINTER(rtdm_jpeg_info), c_void_p, c_int64, c_void_p, c_int64,
+                                      c_int, c_void_p]),
 }
 
 _lib = None

@@ -41,6 +41,22 @@ def read_image_rgb(path: str) -> np.ndarray:
         return np.array(im.convert("RGB"), dtype=np.uint8)
 
 
+def load_image(path: str, device) -> torch.Tensor:
+    """cv2.imread + COLOR_BGR2RGB (aider-predict.py:57-58, yolov3/utils/datasets.py:97) as a
+    device frame uint8 [H, W, 3] RGB: baseline JPEGs are decoded on the device (rtdm.jpeg:
+    host entropy decode, then IDCT / upsampling / colour conversion in HIP, bit-exact with
+    libjpeg-turbo); other formats (PNG, progressive JPEG, ...) decode through Pillow and
+    are uploaded."""
+    from . import jpeg
+    if not os.path.exists(path):
+        raise ValueError(f"Could not load image at {path}")
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:2] == b"\xff\xd8" and jpeg.supported(data):
+        return jpeg.decode(data, device)
+    return torch.from_numpy(read_image_rgb(path)).to(device)
+
+
 def list_images(source: str):
     if os.path.isdir(source):
         return sorted(os.path.join(source, f) for f in os.listdir(source) if f.lower().endswith(IMG_EXTS))
