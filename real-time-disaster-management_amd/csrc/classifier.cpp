@@ -370,6 +370,28 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
   h.arena.alloc(h.per_image * esize(h.dtype) * h.max_batch);
 }
 
+// conv1 (3x3/s2, 3 -> stem_cout) over n images whose input fields (in, in_kind, in_cs, in_co)
+// are already in a: the one construction classify() launches and describe() names.
+static void stem_conv_args(const rtdm_classifier_s& h, ConvArgs& a, int n, View out) {
+  a.n = n;
+  a.ih = a.iw = h.S;
+  a.cin = 3;
+  a.ks = 3;
+  a.stride = 2;
+  a.pad = 0;
+  a.oh = a.ow = h.stem_oh;
+  a.cout = h.stem_cout;
+  a.quad = 0;
+  conv_set_rows(a);
+  a.w = h.blob.at<void>(h.stem.w_off);
+  a.kpad = h.stem.kpad;
+  a.cout_pad = h.stem.cout_pad;
+  a.w_f32 = h.stem.mfma ? 0 : 1;
+  a.w_stem = h.blob.at<void>(h.stem.stem_off);
+  a.e.bias = h.blob.at<float>(h.stem.b_off);
+  a.e.full = out;
+}
+
 static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int n, int in_h, int in_w, float* logits,
                            float* probs, hipStream_t s) {
   RTDM_REQUIRE(n >= 0 && n <= h.max_batch, RTDM_E_CAPACITY,
@@ -448,23 +470,7 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
     throw Error{RTDM_E_INVALID, "classify: unknown input kind"};
   }
   // ---- stem ----
-  a.n = n;
-  a.ih = a.iw = S;
-  a.cin = 3;
-  a.ks = 3;
-  a.stride = 2;
-  a.pad = 0;
-  a.oh = a.ow = h.stem_oh;
-  a.cout = h.stem_cout;
-  a.quad = 0;
-  conv_set_rows(a);
-  a.w = h.blob.at<void>(h.stem.w_off);
-  a.kpad = h.stem.kpad;
-  a.cout_pad = h.stem.cout_pad;
-  a.w_f32 = h.stem.mfma ? 0 : 1;
-  a.w_stem = h.blob.at<void>(h.stem.stem_off);
-  a.e.bias = h.blob.at<float>(h.stem.b_off);
-  a.e.full = View{buf(h.stem_buf), h.stem_cout, 0};
+  stem_conv_args(h, a, n, View{buf(h.stem_buf), h.stem_cout, 0});
   seg("stem", nb * ((double)S * S * 3 * (x_kind == RTDM_INPUT_NCHW_F32 ? 4 : es) +
                     (double)h.stem_oh * h.stem_oh * h.stem_cout * es));
   launch_conv(a, h.dtype, s);
@@ -813,21 +819,8 @@ int64_t rtdm_classifier_describe(rtdm_classifier h, char* buf, int64_t buf_len) 
     ConvArgs a;
     a.in_kind = IN_NHWC;
     a.in_cs = 3;
-    a.n = 1;
-    a.ih = a.iw = h->S;
-    a.cin = 3;
-    a.ks = 3;
-    a.stride = 2;
-    a.pad = 0;
-    a.oh = a.ow = h->stem_oh;
-    a.cout = h->stem_cout;
-    conv_set_rows(a);
-    a.w = h->blob.at<void>(h->stem.w_off);
-    a.kpad = h->stem.kpad;
-    a.cout_pad = h->stem.cout_pad;
-    a.w_f32 = h->stem.mfma ? 0 : 1;
-    a.w_stem = h->blob.at<void>(h->stem.stem_off);
-    a.e.full = View{h->blob.at<void>(0), h->stem_cout, 0};  // (any non-null view: only its presence is read)
+    // (any non-null output view: only its presence is read)
+    stem_conv_args(*h, a, 1, View{h->blob.at<void>(0), h->stem_cout, 0});
     s += std::string("conv1 kernel ") + conv_kernel_name(a, h->dtype) + "\n";
   }
   const bool chain = h->chain_start >= 0 && acff_chain_mode();

@@ -51,7 +51,10 @@ def load_classes(path: str):
 def _process_group():
     """(torch.distributed, world, rank) of an initialised group of more than one rank;
     (None, 1, 0) otherwise.  Under torch.distributed.run (WORLD_SIZE > 1 in the environment)
-    the group is created here: 'nccl' (RCCL) when every rank has its own GPU, else 'gloo'."""
+    the group is created here and owned by the process for its lifetime (test() may be called
+    again): 'nccl' (RCCL) when every rank on this node has its own GPU (LOCAL_WORLD_SIZE <=
+    the node's device count, so a multi-node launch keeps RCCL), else 'gloo'.  Only the gloo
+    path is exercised by the tests (2 ranks sharing one GPU box); the RCCL path is unverified."""
     import torch.distributed as dist
     if not dist.is_available():
         return None, 1, 0
@@ -60,8 +63,8 @@ def _process_group():
         own_gpu = torch.cuda.is_available() and torch.cuda.device_count() > local
         if own_gpu:
             torch.cuda.set_device(local)
-        dist.init_process_group("nccl" if own_gpu and torch.cuda.device_count() >= int(os.environ["WORLD_SIZE"])
-                                else "gloo")
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ["WORLD_SIZE"]))
+        dist.init_process_group("nccl" if own_gpu and torch.cuda.device_count() >= local_world else "gloo")
     if dist.is_initialized() and dist.get_world_size() > 1:
         return dist, dist.get_world_size(), dist.get_rank()
     return None, 1, 0

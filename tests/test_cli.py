@@ -101,14 +101,15 @@ def _cls_oracle(name, sd, imgs):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["squeeze-ernet", "ernet"])
-def test_aider_predict_cli_matches_oracle(tmp_path, cls_weights, name):
+@pytest.mark.parametrize("hw", [(224, 224), (331, 297)])  # config 1's 224x224 source; a ragged one
+def test_aider_predict_cli_matches_oracle(tmp_path, cls_weights, name, hw):
     from rtdm.classifier import CLASSES
     from rtdm.synth import synth_frames
     cli = _load_cli("aider-predict")
     sd = cls_weights[name]
     wpath = tmp_path / "w.pt"
     torch.save({k: torch.from_numpy(v) for k, v in sd.items()}, wpath)
-    img = synth_frames(1, 331, 297, seed=77)[0]
+    img = synth_frames(1, hw[0], hw[1], seed=77)[0]
     ipath = tmp_path / "im.png"
     _write_png(ipath, img)
     res = cli.main(["--model", name, "--image", str(ipath), "--weights", str(wpath), "--trt", "--quant", "fp16"])
