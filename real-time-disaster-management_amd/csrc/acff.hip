@@ -816,7 +816,10 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     ++nst_;
   };
   stamp();
-  _Float16* buf[2] = {(_Float16*)chain_lds, (_Float16*)(chain_lds + a.act_bytes)};
+  // the two activation maps as byte offsets into chain_lds: a runtime-indexed array of the
+  // two pointers lost their LDS address space (every depthwise tap became a flat load that
+  // also waited on the in-flight global weight loads)
+  auto act = [&](int k) { return (_Float16*)(chain_lds + k * a.act_bytes); };
   _Float16* At = (_Float16*)(chain_lds + 2 * a.act_bytes);
   int8_t* const At8 = (int8_t*)At;  // int8 A chunk [M][C + 16] bytes (inside the fp16 one)
   float* wsm = (float*)(chain_lds + 2 * a.act_bytes + a.a_bytes);  // [3][9][C], bias [3][C] (int8: inv_s [3][C])
@@ -828,7 +831,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     const _Float16* src = a.in + (size_t)img * h * h * a.in_cs + a.in_co;
     for (int i = tid; i < h * h * CG; i += kChainThreads) {
       const int px = i / CG, v = i - px * CG;
-      *(uint4*)(buf[0] + (size_t)px * (C + 8) + v * 8) = *(const uint4*)(src + (size_t)px * a.in_cs + v * 8);
+      *(uint4*)(act(0) + (size_t)px * (C + 8) + v * 8) = *(const uint4*)(src + (size_t)px * a.in_cs + v * 8);
     }
   }
   int cur = 0;
@@ -881,8 +884,8 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
     }
     __syncthreads();  // input map + dw weights ready; the previous stage's A reads are done
     stamp();
-    const _Float16* X = buf[cur];
-    _Float16* Y = buf[cur ^ 1];
+    const _Float16* X = act(cur);
+    _Float16* Y = act(cur ^ 1);
     const int wn = st.cout_pad >> 5, wm = 8 / wn;  // wave grid: wm (M) x wn (N), 32 channels per wave
     const int wmi = wid / wn, wni = wid - wmi * wn;
     const int mtiles = (M + 15) >> 4;
@@ -927,13 +930,18 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
           t[j] = bk[0][j];
           t[4 + j] = bk[1][j];
         }
+        // the centre tap's offset once per item; each tap adds a wave-uniform shift, and the
+        // border tests are per tap row / column (d = 1 taps never leave the map: padding 0)
+        const int pc = ((oy + 1) * H + ox + 1) * (C + 8) + v * 8;
+        const int dp = d * (C + 8), dr = d * H * (C + 8);
+        const bool r0 = oy + 1 - d >= 0, r2 = oy + 1 + d < H, c0 = ox + 1 - d >= 0, c2 = ox + 1 + d < H;
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
           for (int kw = 0; kw < 3; ++kw) {
-            const int y = oy + 1 + (kh - 1) * d, x = ox + 1 + (kw - 1) * d;
+            const bool ok = (kh == 0 ? r0 : kh == 2 ? r2 : true) && (kw == 0 ? c0 : kw == 2 ? c2 : true);
             h8 xv = h8{0, 0, 0, 0, 0, 0, 0, 0};
-            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)H) xv = *(const h8*)(X + (size_t)(y * H + x) * (C + 8) + v * 8);
+            if (ok) xv = *(const h8*)(X + pc + (kh - 1) * dr + (kw - 1) * dp);
             const f4& w0 = wk[kh * 3 + kw][0];
             const f4& w1 = wk[kh * 3 + kw][1];
 #pragma unroll
@@ -1076,7 +1084,7 @@ __global__ __launch_bounds__(kChainThreads) void acff_chain(AcffChainArgs a) {
   // ---- tail on the last map: [hw][c], c = last cout ----
   const int h = a.nst > 0 ? a.st[a.nst - 1].h - 2 : a.st[0].h, hw = h * h;
   const int c = a.nst > 0 ? a.st[a.nst - 1].cout : a.st[0].cin;
-  const _Float16* X = buf[cur];
+  const _Float16* X = act(cur);
   float* conv = (float*)At;  // [5][hw]
   // conv2 1x1 (c -> 5): one (output, pixel) pair per thread, weights from LDS, four partial
   // sums over the channels (was a wave per pixel with shuffle reductions)

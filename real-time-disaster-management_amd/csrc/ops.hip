@@ -1708,7 +1708,10 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
   int npow = 1;
   while (npow < n) npow <<= 1;
   const bool lds = npow <= kNmsLdsCap;
-  uint64_t* K = lds ? s_keys : g.keys;
+  // Phases 2-5 are instantiated once with the LDS arrays and once with the workspace: a
+  // pointer selected at run time between the two loses its address space, and every key,
+  // box and mask access of the common (LDS) case became a flat instruction.
+  auto phases = [&](auto lds_tag, uint64_t* K, float4* B, float* A, uint32_t* S) {
   for (int i = n + tid; i < npow; i += kNmsThreads) K[i] = ~0ull;  // sort padding
   __syncthreads();
 
@@ -1764,9 +1767,6 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
 
   NMS_STAMP(2);
   // 3. offset boxes + areas (utils.py:547-552; torchvision areas)
-  float4* B = lds ? s_box : g.box;
-  float* A = lds ? s_area : g.area;
-  uint32_t* S = lds ? s_supp : g.supp;
   const int cls_div = nc > 1 ? nc : 1;
   for (int i = tid; i < n; i += kNmsThreads) {
     const uint32_t cand = (uint32_t)K[i];
@@ -1797,7 +1797,6 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
   if (n <= ((variant & 2) ? -1 : kNmsMaskCapG)) {
     const int W = (n + 63) >> 6;
     const bool in_lds = n <= kNmsMaskCap;
-    uint64_t* M = in_lds ? s_mask : g.mask;
     // one (row i, 16-column quarter q of word w) per thread, rows fastest: the lanes of a
     // wave share (w, q), so each B[j] / A[j] read is one broadcast LDS address, and a
     // quarter word gives every wave of the block work at the typical n of 100-300
@@ -1806,9 +1805,10 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
     const bool thr_nonneg = iou_thr >= 0.0;
     const int QS = in_lds ? 4 : 1, QW = 64 / QS;
     if (in_lds) {
-      for (int p = tid; p < n * W; p += kNmsThreads) M[p] = 0ull;
+      for (int p = tid; p < n * W; p += kNmsThreads) s_mask[p] = 0ull;
       __syncthreads();
     }
+    auto build = [&](auto in_lds_tag, uint64_t* M) {
     for (int p = tid; p < n * W * QS; p += kNmsThreads) {
       const int r = p / n, i = p - r * n;
       const int w = r / QS, q = r - w * QS;
@@ -1831,12 +1831,15 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
           if ((double)ovr > iou_thr) bits |= 1ull << (j - jw);
         }
       }
-      if (in_lds) {
+      if constexpr (decltype(in_lds_tag)::value) {
         if (bits) atomicOr((unsigned long long*)&M[(size_t)i * W + w], (unsigned long long)bits);
       } else {
         M[(size_t)i * W + w] = bits;
       }
     }
+    };
+    if (in_lds) build(std::true_type{}, s_mask);
+    else build(std::false_type{}, g.mask);
     __syncthreads();
     NMS_STAMP(4);
     int nk = 0;
@@ -1857,7 +1860,7 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
             const int i = 64 * c + tid;
             uint64_t mrow[kNmsMaskCap / 64];
 #pragma unroll
-            for (int w = 0; w < kNmsMaskCap / 64; ++w) mrow[w] = (w < W && tid < cnt) ? M[(size_t)i * W + w] : 0ull;
+            for (int w = 0; w < kNmsMaskCap / 64; ++w) mrow[w] = (w < W && tid < cnt) ? s_mask[(size_t)i * W + w] : 0ull;
             const uint64_t valid = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
             uint64_t rem = removed[c], kept = 0;
             uint64_t todo = valid & ~rem;
@@ -1981,6 +1984,9 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
     }
   }
   if (tid == 0) count[img] = nkeep;
+  };
+  if (lds) phases(std::true_type{}, s_keys, s_box, s_area, s_supp);
+  else phases(std::false_type{}, g.keys, g.box, g.area, g.supp);
   NMS_STAMP(6);
 #undef NMS_STAMP
 }
