@@ -341,8 +341,15 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
   // waited on its own s_load latency)
   extern __shared__ __attribute__((aligned(16))) float s_dw[];  // dynamic: (I8 ? 33 : 30) * cin floats
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int i = tid; i < (I8 ? 33 : 30) * a.cin; i += 256)
-    s_dw[i] = i < 27 * a.cin ? a.dw_wt[i] : i < 30 * a.cin ? a.dw_b[i - 27 * a.cin] : a.inv_s[i - 30 * a.cin];
+  // LDS layout [chunk][NW][CC]: every tap / bias / scale offset inside a chunk is a
+  // compile-time immediate from one per-item base (with [NW][cin] each read needed its own
+  // wave-uniform address moved into a VGPR)
+  constexpr int NW = I8 ? 33 : 30;
+  for (int i = tid; i < NW * a.cin; i += 256) {
+    const int chk = i / (NW * CC), r = i - chk * (NW * CC);
+    const int t = r / CC, c = chk * CC + (r - t * CC);
+    s_dw[i] = t < 27 ? a.dw_wt[t * a.cin + c] : t < 30 ? a.dw_b[(t - 27) * a.cin + c] : a.inv_s[(t - 30) * a.cin + c];
+  }
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, g = lane >> 4;
   const int oh = a.h - 2, ow = a.w - 2;
@@ -358,15 +365,46 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
     for (int i = tid; i < G::NPIX * padw; i += 256) At[(i / padw) * AS + 3 * CC + i % padw] = (_Float16)0.f;
   }
   const _Float16* __restrict__ in = a.in + a.in_co;
-  // work item j of this block: tile t0 + (j / nch) * tstep (XCD-contiguous walk: neighbouring
-  // tiles' halos share the XCD's L2), channel chunk j % nch
+  // work items of this block: tiles t0, t0 + tstep, ... < tend (XCD-contiguous walk:
+  // neighbouring tiles' halos share the XCD's L2), each over the channel chunks 0 .. nch-1.
+  // Two cursors (the item being computed, the one being prefetched two ahead) step the
+  // (chunk, tile x, tile y, image) coordinates with carries: no per-item integer divisions
+  // (each was ~10 VALU; the launch keeps every input offset below 2^31, so 32-bit offsets)
   int t0, tend, tstep;
   xcd_span(blockIdx.x, gridDim.x, ntiles, t0, tend, tstep);
-  auto item_tile = [&](int j) { return t0 + (j / nch) * tstep; };
-  auto prefetch = [&](u32x4(&pre)[PV], int j) {
-    const int tile = item_tile(j), ch = j % nch;
-    const int tx = tile % tiles_x, t1 = tile / tiles_x;
-    const int ty = t1 % tiles_y, n = t1 / tiles_y;
+  const int tpi = tiles_x * tiles_y;
+  const int sn = tstep / tpi, sy = (tstep - sn * tpi) / tiles_x, sx = tstep - sn * tpi - sy * tiles_x;
+  struct Cur {
+    int ch, tx, ty, n, tile;
+  };
+  auto cur_at = [&](int tile) {
+    Cur c;
+    c.ch = 0;
+    c.tile = tile;
+    c.tx = tile % tiles_x;
+    const int t1 = tile / tiles_x;
+    c.ty = t1 % tiles_y;
+    c.n = t1 / tiles_y;
+    return c;
+  };
+  auto advance = [&](Cur& c) {
+    if (++c.ch < nch) return;
+    c.ch = 0;
+    c.tile += tstep;
+    c.tx += sx;
+    if (c.tx >= tiles_x) {
+      c.tx -= tiles_x;
+      ++c.ty;
+    }
+    c.ty += sy;
+    if (c.ty >= tiles_y) {
+      c.ty -= tiles_y;
+      ++c.n;
+    }
+    c.n += sn;
+  };
+  auto prefetch = [&](u32x4(&pre)[PV], const Cur& it) {
+    const int ch = it.ch, tx = it.tx, ty = it.ty, n = it.n;
 #pragma unroll
     for (int k = 0; k < PV; ++k) {
       const int i = tid + 256 * k;
@@ -375,7 +413,7 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
       const int y = ty * TH - 2 + r, x = tx * TW - 2 + c;
       u32x4 d = {0u, 0u, 0u, 0u};
       if (i < HALO && (unsigned)y < (unsigned)a.h && (unsigned)x < (unsigned)a.w)
-        d = *(const u32x4*)(in + ((size_t)(n * a.h + y) * a.w + x) * a.in_cs + ch * CC + v * 8);
+        d = *(const u32x4*)(in + (unsigned)(((n * a.h + y) * a.w + x) * a.in_cs + ch * CC + v * 8));
       pre[k] = d;
     }
   };
@@ -407,8 +445,7 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
   // 1x1 weight fragments of item j's chunk (global, L2-resident; once when nch == 1).
   // Issued BEFORE the halo prefetch of j+2: vmcnt retires in order, so waiting for
   // these never waits for the prefetch.
-  auto load_bf = [&](int j) {
-    const int ch = j % nch;
+  auto load_bf = [&](int ch) {
     if (ch == bf_ch) return;
     if constexpr (I8) {
 #pragma unroll
@@ -440,11 +477,11 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
     e_t[tn] = (cv && a.scale) ? a.shift[c] : 0.f;
   }
 
-  auto process = [&](int j, const _Float16* xb) {
-    const int tile = item_tile(j), ch = j % nch;
+  auto process = [&](const Cur& it, const _Float16* xb) {
+    const int ch = it.ch;
     int cal_ok = 0;  // calibration: this lane's pixel lies inside the output map
     if constexpr (CAL) {
-      const int tx = tile % tiles_x, ty = (tile / tiles_x) % tiles_y;
+      const int tx = it.tx, ty = it.ty;
       const int m = lane, q = m >> 2, dq = m & 3;  // pixel of lane (pixel block 0 / 1 differ by 4 rows)
       const int py = 2 * (q >> 3) + (dq >> 1), px = 2 * (q & 7) + (dq & 1);
       cal_ok = (ty * TH + py < oh ? 1 : 0) | (ty * TH + py + 4 < oh ? 2 : 0);
@@ -464,10 +501,11 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
         const int q = m >> 2, dq = m & 3;
         const int py = 2 * (q >> 3) + (dq >> 1), px = 2 * (q & 7) + (dq & 1);
         const int cbase = ch * CC + c4 * 4;
+        const float* wc = s_dw + ch * (NW * CC) + c4 * 4;  // this chunk's [NW][CC] block, lane's 4 channels
 #pragma unroll
         for (int br = 0; br < 3; ++br) {
           const int d = br + 1;
-          const f4 bb = *(const f4*)(s_dw + (27 + br) * a.cin + cbase);
+          const f4 bb = *(const f4*)(wc + (27 + br) * CC);
           float s0[4] = {bb[0], bb[1], bb[2], bb[3]}, s1[4] = {bb[0], bb[1], bb[2], bb[3]};
 #pragma unroll
           for (int kh = 0; kh < 3; ++kh)
@@ -481,7 +519,7 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
               if constexpr ((ABL & 4) != 0) {  // (diagnostic: no tap-weight LDS reads)
                 w = f4{0.5f, 0.25f, 0.125f, 0.5f};
               } else {
-                w = *(const f4*)(s_dw + (br * 9 + kh * 3 + kw) * a.cin + cbase);
+                w = *(const f4*)(wc + (br * 9 + kh * 3 + kw) * CC);
               }
               s0[0] = fma_mix_lo_v(w[0], x0.x, s0[0]);
               s0[1] = fma_mix_hi_v(w[1], x0.x, s0[1]);
@@ -493,7 +531,7 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
               s1[3] = fma_mix_hi_v(w[3], x1.y, s1[3]);
             }
           if constexpr (I8) {
-            const f4 is = *(const f4*)(s_dw + (30 + br) * a.cin + cbase);
+            const f4 is = *(const f4*)(wc + (30 + br) * CC);
             uint32_t q0 = 0, q1 = 0;
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
@@ -558,8 +596,7 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
     if (ch == nch - 1) {
       // ---- epilogue: bias -> LeakyReLU (0 < slope < 1: max(x, slope x)) -> BN affine ->
       //      (2x2 max) -> fp16; 32-bit offsets from a per-image base ----
-      const int tx = tile % tiles_x, t1 = tile / tiles_x;
-      const int ty = t1 % tiles_y, n = t1 / tiles_y;
+      const int tx = it.tx, ty = it.ty, n = it.n;
       const int oy0 = ty * TH, ox0 = tx * TW;
       const int ohp = oh >> 1, owp = ow >> 1;
       _Float16* outn = a.out + (size_t)n * (a.pool ? ohp * owp : oh * ow) * a.out_cs + wn * NF * 16 + fr;
@@ -605,22 +642,27 @@ __global__ __launch_bounds__(256, NF == 2 ? 3 : 2) void acff_persist(AcffPArgs a
 
   // two register prefetch sets: item j+2's halo is in flight while item j computes
   u32x4 preA[PV], preB[PV];
-  auto valid = [&](int j) { return item_tile(j) < tend; };
-  if (valid(0)) prefetch(preA, 0);
-  if (valid(1)) prefetch(preB, 1);
-  for (int j = 0; valid(j); ++j) {
+  Cur cc = cur_at(t0), pc = cc;  // computed item, prefetched item (two ahead)
+  if (pc.tile < tend) prefetch(preA, pc);
+  advance(pc);
+  if (pc.tile < tend) prefetch(preB, pc);
+  advance(pc);
+  while (cc.tile < tend) {
     stage(preA, xs);
     __syncthreads();
-    load_bf(j);
-    if (valid(j + 2)) prefetch(preA, j + 2);
-    process(j, xs);
-    ++j;
-    if (!valid(j)) break;
+    load_bf(cc.ch);
+    if (pc.tile < tend) prefetch(preA, pc);
+    advance(pc);
+    process(cc, xs);
+    advance(cc);
+    if (cc.tile >= tend) break;
     stage(preB, xs + XS);
     __syncthreads();
-    load_bf(j);
-    if (valid(j + 2)) prefetch(preB, j + 2);
-    process(j, xs + XS);
+    load_bf(cc.ch);
+    if (pc.tile < tend) prefetch(preB, pc);
+    advance(pc);
+    process(cc, xs + XS);
+    advance(cc);
   }
 }
 
@@ -643,6 +685,7 @@ void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int
   RTDM_REQUIRE(cc > 0, RTDM_E_INVALID, "acff_persist: unsupported shape");
   RTDM_REQUIRE((in_cs % 8) == 0 && (in_co % 8) == 0, RTDM_E_INVALID, "acff_persist: input view not 16-byte aligned");
   RTDM_REQUIRE(!pool || ((lim_h | lim_w) & 1) == 0, RTDM_E_INVALID, "acff_persist: odd pooled limit");
+  RTDM_REQUIRE((int64_t)n * h * w * in_cs < (1ll << 31), RTDM_E_CAPACITY, "acff_persist: input map over 2^31 elements");
   AcffPArgs a;
   a.in = (const _Float16*)in;
   a.in_cs = in_cs;
