@@ -25,6 +25,9 @@
 //            lane's 4 accumulator rows are one quad and the pool is in-lane.
 #include "common.h"
 
+#include <map>
+#include <mutex>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -716,12 +719,30 @@ void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int
   const int64_t tiles = (int64_t)n * ((lim_h + 7) / 8) * ((lim_w + 15) / 16);
   if (tiles <= 0) return;
   RTDM_REQUIRE(tiles < (1ll << 31), RTDM_E_CAPACITY, "acff_persist: too many tiles");
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  // CU count and resident blocks per (kernel, LDS bytes) queried once per process: these
+  // host calls ran on every launch, and the small per-rank batches are launch-bound on the host
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
   const size_t lds = (size_t)(i8 ? 33 : 30) * cin * sizeof(float);
   auto go = [&](auto kern) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, size_t>, int> occ;
     int per_cu = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      const auto key = std::make_pair((const void*)kern, lds);
+      auto it = occ.find(key);
+      if (it == occ.end()) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+        occ.emplace(key, per_cu);
+      } else {
+        per_cu = it->second;
+      }
+    }
     const int64_t blocks = std::min<int64_t>(tiles, (int64_t)per_cu * cus);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, a);
   };
