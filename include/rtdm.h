@@ -28,8 +28,6 @@
  *   rtdm_yolo_layer_trt      <- YoloLayerPlugin::enqueue   tensorrt_inference/plugins/yolo_layer.cu:323-327
  *   rtdm_nms                 <- non_max_suppression()   victim_localization/yolov3/utils/utils.py:488-557
  *                               (+ torchvision.ops.boxes.nms, utils.py:552)
- *   rtdm_nms_objectness      <- the same, given io's objectness column as a contiguous array
- *                               (rtdm_detector_objectness: written beside io by the head decode)
  *   rtdm_letterbox           <- letterbox()             victim_localization/yolov3/utils/datasets.py:599-631
  *   rtdm_resize_linear       <- cv2.resize(frame, (w, h)) disaster_detection/real-time-inference.py:185
  *   rtdm_preprocess_frames   <- squeeze_transforms / aider_transforms  disaster_detection/dataloaders/aider.py:412-431
@@ -159,9 +157,7 @@ const char* rtdm_build_arch(void);
  * "pool_small64" 1 = 3x3 Cin 64 -> Cout 128 + 2x2 pool (+ full map) on conv3_pool_small
  * (default; bit-identical to 0 = conv_pipe); "pool_sep" 1 = stride-1 5 / 9 / 13 max pools
  * (SPP) and the zero-padded 2 x 2 stride-1 pool as separable band kernels (default;
- * bit-identical to 0); "objectness" 1 = the stand-alone head kernels also write the
- * objectness side array rtdm_detector_objectness returns (default; 0 = none, so NMS reads
- * io; the same survivors either way).  Variants measured slower in earlier rounds (256 x 256 conv tiles,
+ * bit-identical to 0).  Variants measured slower in earlier rounds (256 x 256 conv tiles,
  * the ping-pong K-loop, the fused stem pair, the persistent stem, register-epilogue pools)
  * were removed (DESIGN.md §3.4 keeps their numbers).
  * Unknown keys: RTDM_E_INVALID. */
@@ -267,11 +263,6 @@ rtdm_status rtdm_detect_trt(rtdm_detector h, const void* x, int x_kind, int n, f
 /* Debug/parity: copy cfg layer `layer`'s output of the LAST rtdm_detect call as
  * NCHW fp32 [n,C,H,W] into out (only for layers whose full-resolution output is
  * materialised; returns RTDM_E_UNSUPPORTED otherwise).                          */
-/* The objectness side array of the last rtdm_detect call on h ([n, n_anchors] fp32 device
- * memory owned by the handle: io[..., 4] of every anchor row, same values), or NULL when that
- * call did not write a complete one (a fused head, int8, raw output).  Valid until the next
- * call on h; stream-ordered like io.                                                      */
-rtdm_status rtdm_detector_objectness(rtdm_detector h, const float** obj);
 rtdm_status rtdm_detector_layer_output(rtdm_detector h, int layer, int n, float* out, int64_t out_numel,
                                        int* c, int* hgt, int* wid, void* stream);
 
@@ -307,15 +298,6 @@ size_t rtdm_nms_workspace_size(int n, int n_anchors, int nc);
 rtdm_status rtdm_nms(const float* io, int n, int n_anchors, int no, float conf_thres, double iou_thres,
                      int multi_label, int agnostic, uint64_t class_mask, int max_det, void* workspace,
                      size_t workspace_bytes, float* det, int32_t* idx, int32_t* count, void* stream);
-/* rtdm_nms with io's objectness column also given as a contiguous [n, n_anchors] fp32 array
- * (obj; NULL: read it from io): the candidate filter then reads 4 bytes per anchor and only
- * the rows over conf_thres.  Same results bit for bit.  The detector's decode writes such an
- * array beside io (rtdm_detector_objectness) when every head runs the stand-alone head
- * kernel; the two-stage pipeline passes it here.                                         */
-rtdm_status rtdm_nms_objectness(const float* io, const float* obj, int n, int n_anchors, int no, float conf_thres,
-                                double iou_thres, int multi_label, int agnostic, uint64_t class_mask, int max_det,
-                                void* workspace, size_t workspace_bytes, float* det, int32_t* idx, int32_t* count,
-                                void* stream);
 
 /* ---- pre-processing (CLI transform, aider.py:412-426) --------------------------
  * frames: [n, in_h, in_w, 3] uint8 RGB.  out: [n, 3, S, S] fp32 (the tensor the

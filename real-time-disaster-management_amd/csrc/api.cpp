@@ -63,7 +63,6 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "stem_abl") t.stem_abl = v;
   else if (k == "nms_variant") t.nms_variant = v;
   else if (k == "resize_stream") t.resize_stream = v;
-  else if (k == "objectness") t.objectness = v ? 1 : 0;
   else throw Error{RTDM_E_INVALID, "set_tuning: unknown key " + k};
 }
 
@@ -143,14 +142,6 @@ size_t rtdm_nms_workspace_size(int n, int n_anchors, int nc) {
 rtdm_status rtdm_nms(const float* io, int n, int n_anchors, int no, float conf_thres, double iou_thres,
                      int multi_label, int agnostic, uint64_t class_mask, int max_det, void* workspace,
                      size_t workspace_bytes, float* det, int32_t* idx, int32_t* count, void* stream) {
-  return rtdm_nms_objectness(io, nullptr, n, n_anchors, no, conf_thres, iou_thres, multi_label, agnostic, class_mask,
-                             max_det, workspace, workspace_bytes, det, idx, count, stream);
-}
-
-rtdm_status rtdm_nms_objectness(const float* io, const float* obj, int n, int n_anchors, int no, float conf_thres,
-                                double iou_thres, int multi_label, int agnostic, uint64_t class_mask, int max_det,
-                                void* workspace, size_t workspace_bytes, float* det, int32_t* idx, int32_t* count,
-                                void* stream) {
   return guard([&] {
     if (n == 0) return;
     RTDM_REQUIRE(io && det && count && workspace, RTDM_E_INVALID, "nms: NULL pointer");
@@ -160,7 +151,7 @@ rtdm_status rtdm_nms_objectness(const float* io, const float* obj, int n, int n_
     RTDM_REQUIRE(workspace_bytes >= nms_workspace_size(n, n_anchors, no - 5), RTDM_E_CAPACITY,
                  "nms: workspace too small");
     launch_nms(io, n, n_anchors, no, conf_thres, iou_thres, multi_label, agnostic, class_mask, max_det, workspace, det,
-               idx, count, (hipStream_t)stream, obj);
+               idx, count, (hipStream_t)stream);
   });
 }
 

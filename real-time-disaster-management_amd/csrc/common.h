@@ -125,10 +125,6 @@ struct Epilogue {
   // raw = 1: write the head conv's output itself (no decode) into the io rows: the
   // YOLOLayer training-branch p (models.py:249-250) that the TensorRT plugin decodes
   int raw = 0;
-  // objectness side array [n, io_rows] (head1x1_f16 only): each decoded row's obj value
-  // (io[..., 4]) again, contiguous, so the NMS candidate filter reads 4 bytes per anchor
-  // instead of every io row
-  float* obj = nullptr;
 };
 
 // Branch-free unsigned division by a runtime-invariant divisor (round-up
@@ -230,7 +226,6 @@ struct Tuning {
   int stem_k16 = 1;         // pooled MFMA stem: the kh = 2 third of K as a 16-deep MFMA (0: 32-deep)
   int conv_c32 = 1;         // conv3_c32 for the Cin-32 3x3 convs (conv_c32.hip)
   int res_fuse = 1;         // conv3_c32r (+ conv3_c64r): Darknet-53's residual blocks as one launch (1: c32r on 8 waves + c64r, 2: c32r on 4 waves, 3: c32r on 8 waves only)
-  int objectness = 1;       // head1x1_f16 writes the objectness side array (rtdm_detector_objectness; 0: none, NMS reads io)
 };
 Tuning& default_tuning();
 const Tuning& tune();
@@ -464,9 +459,8 @@ struct TrtYoloArgs {
 void launch_yolo_trt(const float* in, int n, const TrtYoloArgs& t, int nchw, float* out, hipStream_t s);
 
 size_t nms_workspace_size(int n, int n_anchors, int nc);
-// obj: the objectness side array of io ([n, n_anchors], Epilogue::obj) or nullptr (read io)
 void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label,
                 int agnostic, uint64_t class_mask, int max_det, void* ws, float* det, int32_t* idx,
-                int32_t* count, hipStream_t s, const float* obj = nullptr);
+                int32_t* count, hipStream_t s);
 
 }  // namespace rtdm

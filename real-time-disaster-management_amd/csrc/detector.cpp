@@ -12,7 +12,6 @@
 //   route (concat)               : producers write straight into channel
 //                                  slices of the concat buffer (zero copy)
 // Anything else runs as its own kernel (maxpool k/s, upsample, slice copy).
-#include <cstring>
 #include <map>
 #include <sstream>
 
@@ -196,10 +195,6 @@ struct rtdm_detector_s {
   rtdm::DevBuf arena;
   rtdm::DevBuf zero;  // 256 zero bytes: padding source of the glds conv kernel
   rtdm::DevBuf raw_buf;  // raw head rows for rtdm_detect_trt (allocated on first use)
-  // objectness side array [max_batch, n_anchors] (Epilogue::obj), complete after a decode call
-  // whose every head ran head1x1_f16 (obj_valid)
-  rtdm::DevBuf objbuf;
-  bool obj_valid = false;
   int last_n = 0;
   std::vector<int> fused_away;  // tensors the last rtdm_detect call never wrote (fused stem pairs)
   // optional per-step timing: events[call][2*step + {0,1}] recorded around each step
@@ -873,7 +868,6 @@ static void plan(rtdm_detector_s& h, const float* weights, int64_t n_floats) {
     RTDM_HIP(hipGetDevice(&h.dev));
     h.blob.upload(blob);
     h.arena.alloc(h.per_image * esize_of(h.dtype) * h.max_batch);
-    h.objbuf.alloc((size_t)h.max_batch * h.n_anchors_total * sizeof(float));
     h.zero.alloc(256);
     RTDM_HIP(hipMemset(h.zero.p, 0, 256));
     if (h.n_q) {
@@ -1001,8 +995,6 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
   hipStream_t s0 = s;
   bool fused_next = false;
   h.fused_away.clear();
-  int obj_heads = 0;  // heads that wrote the objectness side array this call
-  h.obj_valid = false;
   for (size_t si = 0; si < h.steps.size(); ++si) {
     const Step& st = h.steps[si];
     s = two && st.stream == 1 ? h.side : s0;
@@ -1044,12 +1036,6 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
         a.deq = h.blob.at<float>(st.deq_off);
         launch_conv_pipe_i8(a, s);
       } else {
-        // a decoding head on head1x1_f16 also writes the objectness side array
-        if (a.e.io && !raw && !h.calibrating && h.objbuf.p && tune().objectness &&
-            std::strncmp(conv_kernel_name(a, h.dtype), "head1x1", 7) == 0) {
-          a.e.obj = h.objbuf.as<float>();
-          ++obj_heads;
-        }
         launch_conv(a, h.dtype, s);
       }
     } else if (st.kind == ST_MAXPOOL) {
@@ -1081,7 +1067,6 @@ static void run_detector(rtdm_detector_s& h, const void* x, int x_kind, int n, f
     RTDM_HIP(hipStreamWaitEvent(s0, h.join_ev, 0));
   }
   h.last_n = n;
-  h.obj_valid = obj_heads == (int)h.heads.size() && obj_heads > 0;
 }
 
 // Geometry of tensor t's view (pointer is a non-null placeholder) for kernel selection.
@@ -1477,13 +1462,6 @@ rtdm_status rtdm_detect(rtdm_detector h, const void* x, int x_kind, int n, float
     TuningScope ts_(h ? &h->tuning : nullptr);
     RTDM_REQUIRE(h, RTDM_E_INVALID, "detect: NULL handle");
     run_detector(*h, x, x_kind, n, io, (hipStream_t)stream);
-  });
-}
-
-rtdm_status rtdm_detector_objectness(rtdm_detector h, const float** obj) {
-  return guard([&] {
-    RTDM_REQUIRE(h && obj, RTDM_E_INVALID, "objectness: NULL argument");
-    *obj = h->obj_valid ? h->objbuf.as<float>() : nullptr;
   });
 }
 

@@ -155,22 +155,6 @@ __global__ __launch_bounds__(256) void head1x1_f16(ConvArgs a) {
   // el / no by a multiply-shift (exact for el < 2112 and no <= 32, checked host-side in
   // head1x1_ok): a run-time integer division per element was a third of the kernel's VALU
   const uint32_t inv_no = (65536u + (uint32_t)no - 1u) / (uint32_t)no;
-  if (e.obj && !e.raw) {  // objectness side array: one contiguous run per anchor plane
-    for (int ai = 0; ai < na; ++ai) {
-      const float* To = T + (ai * no + 4) * PXS;
-      for (int px = lane; px < rows; px += 64) {
-        size_t r;
-        if (one_image) {
-          r = (size_t)n0 * e.io_rows + e.io_off + (size_t)ai * plane + p0 + px;
-        } else {
-          int n, oy, ox;
-          row_to_pix(a, m_base + px, n, oy, ox);
-          r = (size_t)n * e.io_rows + e.io_off + (size_t)ai * plane + (size_t)oy * a.ow + ox;
-        }
-        e.obj[r] = To[px];
-      }
-    }
-  }
   for (int ai = 0; ai < na; ++ai) {
     const float* Ta = T + ai * no * PXS;
     float* dst = e.io + ((size_t)n0 * e.io_rows + e.io_off + (size_t)ai * plane + p0) * no;

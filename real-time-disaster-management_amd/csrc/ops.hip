@@ -1584,7 +1584,7 @@ __device__ __forceinline__ bool nms_class_ok(uint64_t class_mask, int c) {
 // kNmsCandBlk anchors of one image and writes its keys to its own segment (+ count).
 __global__ __launch_bounds__(kNmsCandBlk) void nms_cand_kernel(const float* __restrict__ io, int n_anchors, int no,
                                                                float conf, int multi_label, uint64_t class_mask,
-                                                               void* ws, size_t cap, const float* __restrict__ objv) {
+                                                               void* ws, size_t cap) {
   __shared__ int s_n;
   const int img = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
   const int nc = no - 5;
@@ -1597,11 +1597,9 @@ __global__ __launch_bounds__(kNmsCandBlk) void nms_cand_kernel(const float* __re
   const int a = blk * kNmsCandBlk + tid;
   if (a < n_anchors) {
     const float* r = io + ((size_t)img * n_anchors + a) * no;
-    // (objv: the same values as r[4], contiguous; the row itself is read only for the few
-    // anchors over the threshold)
-    const float obj = objv ? objv[(size_t)img * n_anchors + a] : r[4];
-    if ((obj > conf) && (r[2] > 2.f) && (r[3] > 2.f) && (r[2] < 4096.f) && (r[3] < 4096.f)) {
-      const float w = r[2], h = r[3];
+    const float obj = r[4];
+    const float w = r[2], h = r[3];
+    if ((obj > conf) && (w > 2.f) && (h > 2.f) && (w < 4096.f) && (h < 4096.f)) {
       const float x = r[0], y = r[1];
       const float hw = w / 2.f, hh = h / 2.f;
       const bool box_finite = isfinite(x - hw) && isfinite(y - hh) && isfinite(x + hw) && isfinite(y + hh);
@@ -1995,13 +1993,13 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
 
 void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label, int agnostic,
                 uint64_t class_mask, int max_det, void* ws, float* det, int32_t* idx, int32_t* count,
-                hipStream_t s, const float* obj) {
+                hipStream_t s) {
   if (n <= 0) return;
   RTDM_REQUIRE(no >= 6, RTDM_E_INVALID, "nms: no must be >= 6 (5 + nc)");
   RTDM_REQUIRE(max_det >= 0, RTDM_E_INVALID, "nms: max_det < 0");
   const size_t cap = nms_cap(n_anchors, no - 5);
   hipLaunchKernelGGL(nms_cand_kernel, dim3(nms_nblk(n_anchors), n), dim3(kNmsCandBlk), 0, s, io, n_anchors, no, conf,
-                     multi_label, class_mask, ws, cap, obj);
+                     multi_label, class_mask, ws, cap);
   hipLaunchKernelGGL(nms_kernel, dim3(n), dim3(kNmsThreads), 0, s, io, n_anchors, no, conf, iou, multi_label,
                      agnostic, class_mask, max_det, ws, cap, det, idx, count, tune().nms_variant);
   RTDM_HIP(hipGetLastError());

@@ -101,9 +101,6 @@ SIGNATURES = {
     "rtdm_nms_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "rtdm_nms": (c_int, [c_void_p, c_int, c_int, c_int, c_float, c_double, c_int, c_int, c_uint64, c_int, c_void_p,
                          c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "rtdm_nms_objectness": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_double, c_int, c_int,
-                                    c_uint64, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "rtdm_detector_objectness": (c_int, [c_void_p, POINTER(c_void_p)]),
     "rtdm_preprocess_frames": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "rtdm_letterbox_geometry": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, POINTER(c_int)]),
     "rtdm_letterbox": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

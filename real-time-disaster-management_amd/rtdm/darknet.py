@@ -228,14 +228,6 @@ class Darknet(torch.nn.Module):
             L.check(L.lib().rtdm_detect(h, L.ptr(x), kind, n, L.ptr(out), L.stream_ptr(stream)))
         return out, None
 
-    def objectness(self, n: int):
-        """Device address of the objectness side array the last forward on the batch-n handle
-        wrote beside io ([n, n_anchors] fp32, io[..., 4] again), or None when that call did not
-        write a complete one (fused heads, int8, raw output).  For nms_batched(objectness=...)."""
-        p = ctypes.c_void_p()
-        L.check(L.lib().rtdm_detector_objectness(self.handle(n), ctypes.byref(p)))
-        return p.value
-
     def _run(self, fn, x: torch.Tensor, width: int, stream=None):
         if not x.is_cuda:
             raise RuntimeError("rtdm Darknet runs on the GPU: move the input to a cuda device")

@@ -41,15 +41,12 @@ def workspace_bytes(n, n_anchors, nc) -> int:
 
 
 def nms_batched(prediction: torch.Tensor, conf_thres: float = 0.1, iou_thres: float = 0.6, multi_label: bool = True,
-                classes=None, agnostic: bool = False, max_det: int = 300, out=None, stream=None, workspace=None,
-                objectness=None):
+                classes=None, agnostic: bool = False, max_det: int = 300, out=None, stream=None, workspace=None):
     """prediction: io [N, A, 5+nc] fp32 CUDA.  Returns (det [N,max_det,6], idx [N,max_det,2] int32
     (anchor row, class), count [N] int32 = survivors per image; rows >= min(count, max_det) are
     undefined).  No host synchronisation.  workspace: a caller-owned uint8 device buffer of
     workspace_bytes(...) (callers with work in flight on several streams need their own);
-    default: one shared per device.  objectness: device address of io[..., 4] as a contiguous
-    [N, A] fp32 array (Darknet.objectness(); same results, the candidate filter reads it
-    instead of every io row), or None."""
+    default: one shared per device."""
     if prediction.dtype != torch.float32:
         prediction = prediction.float()
     prediction = prediction.contiguous()
@@ -68,15 +65,9 @@ def nms_batched(prediction: torch.Tensor, conf_thres: float = 0.1, iou_thres: fl
                 raise ValueError(f"nms workspace has {ws.numel()} bytes, needs {need}")
         else:
             ws, need = _workspace(dev, n, a, no - 5)
-        if objectness:
-            L.check(L.lib().rtdm_nms_objectness(L.ptr(prediction), objectness, n, a, no, float(conf_thres),
-                                                float(iou_thres), 1 if multi_label else 0, 1 if agnostic else 0,
-                                                class_mask(classes), int(max_det), L.ptr(ws), need, L.ptr(det),
-                                                L.ptr(idx), L.ptr(count), L.stream_ptr(stream)))
-        else:
-            L.check(L.lib().rtdm_nms(L.ptr(prediction), n, a, no, float(conf_thres), float(iou_thres),
-                                     1 if multi_label else 0, 1 if agnostic else 0, class_mask(classes), int(max_det),
-                                     L.ptr(ws), need, L.ptr(det), L.ptr(idx), L.ptr(count), L.stream_ptr(stream)))
+        L.check(L.lib().rtdm_nms(L.ptr(prediction), n, a, no, float(conf_thres), float(iou_thres),
+                                 1 if multi_label else 0, 1 if agnostic else 0, class_mask(classes), int(max_det),
+                                 L.ptr(ws), need, L.ptr(det), L.ptr(idx), L.ptr(count), L.stream_ptr(stream)))
     return det, idx, count
 
 

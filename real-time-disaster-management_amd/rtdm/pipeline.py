@@ -59,9 +59,6 @@ class TwoStagePipeline:
         # one host call per batch instead of ~35 launches + stream/event operations, so the
         # small per-rank batches of frame-sharded multi-GPU runs are not host-bound
         self.graphs = graphs
-        # use_objectness=True: NMS reads the detector's objectness side array (bit-identical;
-        # False re-reads every io row, for A/B runs and tests)
-        self.use_objectness = True
         self._bufs = {}
         self._side = {}
         self._graphs = {}
@@ -187,11 +184,8 @@ class TwoStagePipeline:
                 hd = self.detector.handle(n)
                 L.check(L.lib().rtdm_detect(hd, L.ptr(frames), L.RTDM_INPUT_FRAME_U8, n, L.ptr(b["io"]),
                                             L.stream_ptr(crit)))
-                # the decode's objectness side array (same values as io[..., 4]): the NMS
-                # candidate filter reads 4 bytes per anchor instead of every io row
                 nms_batched(b["io"], self.conf_thres, self.iou_thres, self.multi_label, None, self.agnostic,
-                            self.max_det, out=(b["det"], b["idx"], b["count"]), stream=crit, workspace=b["ws"],
-                            objectness=self.detector.objectness(n) if self.use_objectness else None)
+                            self.max_det, out=(b["det"], b["idx"], b["count"]), stream=crit, workspace=b["ws"])
             crit_done.record(crit)
             main.wait_event(joined)
             main.wait_event(crit_done)

@@ -682,44 +682,6 @@ def _nms_compare(io, conf, iou, multi_label=True, agnostic=False, classes=None):
     return count
 
 
-def _copy_dev(ptr, numel, dev):
-    """A float32 tensor copy of numel floats at device address ptr (hipMemcpy D2D)."""
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    t = torch.empty(numel, dtype=torch.float32, device=dev)
-    torch.cuda.synchronize()
-    assert hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(4 * numel), 3) == 0
-    return t
-
-
-@pytest.mark.parametrize("cfg,size", [("yolov4-tiny-aider-416", 608), ("yolov3-aider-416", 416)])
-def test_objectness_side_array(dev, cfg, size):
-    """The head decode's objectness side array holds io[..., 4] bit for bit, and NMS given it
-    returns exactly what NMS reading io returns (det, idx, count), as the pipeline uses it."""
-    from rtdm.nms import nms_batched
-    from rtdm.synth import synth_frames
-    det, _, _ = _darknet(cfg, size, half=True, preset="cond")
-    n = 6
-    frames = torch.from_numpy(synth_frames(n, size, size, seed=77)).to(dev)
-    io, _ = det(frames)
-    ptr = det.objectness(n)
-    assert ptr, "every head of this cfg decodes on head1x1_f16: the side array must be complete"
-    obj = _copy_dev(ptr, n * det.n_anchors, dev).view(n, det.n_anchors)
-    assert torch.equal(obj, io[..., 4])
-    for conf, iou, ml in ((0.3, 0.4, True), (0.05, 0.5, False), (0.6, 0.45, True)):
-        a = nms_batched(io, conf, iou, ml, None, False, 300)
-        b = nms_batched(io, conf, iou, ml, None, False, 300, objectness=ptr)
-        torch.cuda.synchronize()
-        ca, cb = a[2].cpu(), b[2].cpu()
-        assert torch.equal(ca, cb)
-        for i in range(n):
-            k = min(int(ca[i]), 300)
-            assert torch.equal(a[0][i, :k], b[0][i, :k]) and torch.equal(a[1][i, :k], b[1][i, :k])
-    # raw head output (the TensorRT path) writes no objectness array
-    det.forward_raw(frames)
-    assert det.objectness(n) is None
-
-
 def test_nms_golden_io(dev, det_golden):
     """NMS kernel fed the reference io: bit-exact survivors vs the reference non_max_suppression."""
     key = "yolov4-tiny-aider-416@256"
