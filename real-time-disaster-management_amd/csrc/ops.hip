@@ -1627,6 +1627,19 @@ __global__ __launch_bounds__(kNmsCandBlk) void nms_cand_kernel(const float* __re
   if (tid == 0) g.segcnt[blk] = s_n;
 }
 
+// OR of v over the 64 lanes of a full wave, as a wave-uniform value: rotations inside each
+// 16-lane row (DPP row_ror 1 / 2 / 4 / 8) and the four rows' lane 0.  The __shfl_xor butterfly
+// it replaces compiled to six dependent ds_bpermute_b32 per 32-bit half, an LDS round trip
+// each, on the greedy scan's serial path.
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xf, 0xf, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xf, 0xf, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) | (uint32_t)__builtin_amdgcn_readlane((int)v, 16) |
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) | (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
 // 64-bit readlane (the builtin returns a signed int: widen it as unsigned)
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
@@ -1817,6 +1830,7 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
       uint64_t bits = 0;
       const int jw = w * 64, j0 = jw + q * QW;
       const int j1 = j0 + QW < n ? j0 + QW : n;
+#pragma unroll 4
       for (int j = j0 > i + 1 ? j0 : i + 1; j < j1; ++j) {
         const float4 bj = B[j];
         const float xx1 = fmaxf(bi.x, bj.x);
@@ -1876,13 +1890,8 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
 #pragma unroll
             for (int w = c + 1; w < kNmsMaskCap / 64; ++w) {
               if (w < W) {
-                uint32_t lo = mine ? (uint32_t)mrow[w] : 0u, hi = mine ? (uint32_t)(mrow[w] >> 32) : 0u;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) {
-                  lo |= (uint32_t)__shfl_xor((int)lo, off);
-                  hi |= (uint32_t)__shfl_xor((int)hi, off);
-                }
-                removed[w] |= ((uint64_t)hi << 32) | lo;
+                const uint32_t lo = mine ? (uint32_t)mrow[w] : 0u, hi = mine ? (uint32_t)(mrow[w] >> 32) : 0u;
+                removed[w] |= ((uint64_t)wave_or_u32(hi) << 32) | wave_or_u32(lo);
               }
             }
           }
