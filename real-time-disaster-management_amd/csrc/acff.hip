@@ -673,7 +673,7 @@ int acff_persist_mode() { return tune().acff_persist; }
 
 // Channel chunk of the persistent kernel for cin (0 = not eligible).
 int acff_persist_chunk(int cin, int cout_pad, int oh) {
-  if (cout_pad != 64 && cout_pad != 128) return 0;
+  if (cout_pad != 64 && cout_pad != 96 && cout_pad != 128) return 0;
   if (oh < 24) return 0;  // small maps: 8 x 16 tiles would mostly idle
   if (cin > kAcffPMaxCin) return 0;
   // 16-channel chunks for every cin: (CC = 32 chunks need ~40 more VGPRs and spill)
@@ -748,8 +748,11 @@ void launch_acff_persist(const void* in, int in_cs, int in_co, int n, int h, int
   };
   const int abl = acff_persist_mode() - 1;  // >1: diagnostic ablations
   if (cc == 16) {
+    RTDM_REQUIRE(cout_pad != 96 || (!i8 && abl <= 0), RTDM_E_INVALID,
+                 "acff_persist: 96 output rows are for the fp16 / calibration kernels");
     if (i8) cout_pad == 64 ? go(acff_persist<16, 2, 0, 1>) : go(acff_persist<16, 4, 0, 1>);
-    else if (a.amax) cout_pad == 64 ? go(acff_persist<16, 2, 0, 2>) : go(acff_persist<16, 4, 0, 2>);
+    else if (a.amax) cout_pad == 64 ? go(acff_persist<16, 2, 0, 2>) : cout_pad == 96 ? go(acff_persist<16, 3, 0, 2>) : go(acff_persist<16, 4, 0, 2>);
+    else if (cout_pad == 96) go(acff_persist<16, 3>);
     else if (abl == 1) cout_pad == 64 ? go(acff_persist<16, 2, 1>) : go(acff_persist<16, 4, 1>);
     else if (abl == 2) cout_pad == 64 ? go(acff_persist<16, 2, 2>) : go(acff_persist<16, 4, 2>);
     else if (abl == 4) cout_pad == 64 ? go(acff_persist<16, 2, 4>) : go(acff_persist<16, 4, 4>);

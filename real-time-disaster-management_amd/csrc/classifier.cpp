@@ -25,6 +25,8 @@ struct AcffStage {
   size_t dw_wt = 0;                     // [3][9][cin] (tap-major copy for the fused kernel)
   bool fused = false;                   // fp16 fused ACFF kernel (acff.hip)
   int persist_cc = 0;                   // acff_persist channel chunk (0 = acff_fused)
+  int persist_cp = 0;                   // acff_persist output channels padded to 32 (fp16 / calibration
+                                        // runs; int8 keeps pw.cout_pad): rows of pwc_off
   size_t pwc_off = 0;                   // 1x1 weights in (chunk, branch, channel) K order
   PackedConv pw;                        // fused 1x1 conv
   size_t d_buf = 0, out_buf = 0;        // arena offsets (elements) per image
@@ -229,9 +231,12 @@ static void build_classifier(rtdm_classifier_s& h, const ParamMap& pm) {
     st.fused = f16 && acff_fused_ok(sp.cin, st.pw.cout_pad, st.pw.kpad);
     if (st.fused && !(sp.red && sp.red_before_pool)) st.persist_cc = acff_persist_chunk(sp.cin, st.pw.cout_pad, st.oh);
     if (st.persist_cc) {
-      // [cout_pad][nch * KC] fp16, k = chunk*KC + branch*CC + c (zero K/row padding)
+      // [persist_cp][nch * KC] fp16, k = chunk*KC + branch*CC + c (zero K/row padding); rows
+      // padded to 32 only (two waves x NF 16-channel tiles): ErNET acff2's 96 outputs as NF 3
+      // instead of 128 rows of which a quarter were zero MFMA work
+      st.persist_cp = (sp.cout + 31) / 32 * 32;
       const int CCk = st.persist_cc, nch = sp.cin / CCk, KC = (3 * CCk + 31) / 32 * 32;
-      std::vector<_Float16> wc((size_t)st.pw.cout_pad * nch * KC, (_Float16)0.f);
+      std::vector<_Float16> wc((size_t)st.persist_cp * nch * KC, (_Float16)0.f);
       for (int o = 0; o < sp.cout; ++o)
         for (int chk = 0; chk < nch; ++chk)
           for (int br = 0; br < 3; ++br)
@@ -507,12 +512,13 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       // bytes: the stage input map in, its (pooled) output out
       seg("acff" + std::to_string(si + 1),
           nb * ((double)st.h * st.w * st.cin + (double)(pool_here ? (lim / 2) * (lim / 2) : lim * lim) * st.cout) * es);
-      if (st.persist_cc && (acff_persist_mode() || st.q8))
+      if (st.persist_cc && (acff_persist_mode() || st.q8)) {
+        const AcffI8* qp = q8(st, qa);
         launch_acff_persist(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_wt),
-                            h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pwc_off), st.cout, st.pw.cout_pad,
-                            h.blob.at<float>(st.pw.b_off), sc, sh, 0.01f, dst, st.cout, pool_here ? 1 : 0, s,
-                            q8(st, qa));
-      else
+                            h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pwc_off), st.cout,
+                            qp && qp->w8 ? st.pw.cout_pad : st.persist_cp, h.blob.at<float>(st.pw.b_off), sc, sh,
+                            0.01f, dst, st.cout, pool_here ? 1 : 0, s, qp);
+      } else
       launch_acff_fused(cur.ptr, cur.cs, cur.co, n, st.h, st.w, st.cin, lim, lim, h.blob.at<float>(st.dw_wt),
                         h.blob.at<float>(st.dw_b), h.blob.at<void>(st.pw.w_off), st.pw.kpad, st.cout, st.pw.cout_pad,
                         h.blob.at<float>(st.pw.b_off), sc, sh, 0.01f, dst, st.cout, pool_here ? 1 : 0, s);
