@@ -397,6 +397,13 @@ static void stem_conv_args(const rtdm_classifier_s& h, ConvArgs& a, int n, View 
   a.e.full = out;
 }
 
+// uint8 frames: the CLI transform and conv1 as one launch (launch_preprocess_stem) when the
+// stem is the fp16 16-channel one (not RedConv's folded 8-channel stem) and cls_front is on
+static bool front_fusable(const rtdm_classifier_s& h) {
+  return h.dtype == RTDM_F16 && h.stem_cout == 16 && h.stem.cout_pad == 16 && h.stem.stem_off != SIZE_MAX &&
+         tune().cls_front && tune().stem_k16;
+}
+
 static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int n, int in_h, int in_w, float* logits,
                            float* probs, hipStream_t s) {
   RTDM_REQUIRE(n >= 0 && n <= h.max_batch, RTDM_E_CAPACITY,
@@ -442,6 +449,7 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
   const int S = h.S;
   // ---- input ----
   ConvArgs a;
+  bool stem_done = false;
   if (x_kind == RTDM_INPUT_FRAME_U8) {
     auto key = std::make_pair(in_h, in_w);
     auto it = h.resize.find(key);
@@ -457,14 +465,24 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
       h.resize_tmp.alloc(need);
       h.resize_tmp_bytes = need;
     }
-    // bytes: the frames in, the S x S x 3 model input out
-    seg("preprocess", nb * ((double)in_h * in_w * 3 + (double)S * S * 3 * es));
-    launch_preprocess(rp, (const uint8_t*)x, n, h.resize_tmp.as<uint8_t>(), buf(h.x0_buf), 0, h.dtype, s);
-    seg_end();
-    a.in = buf(h.x0_buf);
-    a.in_kind = IN_NHWC;
-    a.in_cs = 3;
-    a.in_co = 0;
+    // CLI transform + conv1 in one launch (fp16, the 16-channel stem): the transformed image
+    // never leaves LDS; the stem map is bit-identical to the two-launch form's
+    if (front_fusable(h) && preprocess_stem_ok(rp, (const uint8_t*)x, h.stem_oh)) {
+      seg("preprocess+stem", nb * ((double)in_h * in_w * 3 + (double)h.stem_oh * h.stem_oh * h.stem_cout * es));
+      launch_preprocess_stem(rp, (const uint8_t*)x, n, h.blob.at<void>(h.stem.stem_off), h.blob.at<float>(h.stem.b_off),
+                             buf(h.stem_buf), h.stem_oh, s);
+      seg_end();
+      stem_done = true;
+    } else {
+      // bytes: the frames in, the S x S x 3 model input out
+      seg("preprocess", nb * ((double)in_h * in_w * 3 + (double)S * S * 3 * es));
+      launch_preprocess(rp, (const uint8_t*)x, n, h.resize_tmp.as<uint8_t>(), buf(h.x0_buf), 0, h.dtype, s);
+      seg_end();
+      a.in = buf(h.x0_buf);
+      a.in_kind = IN_NHWC;
+      a.in_cs = 3;
+      a.in_co = 0;
+    }
   } else if (x_kind == RTDM_INPUT_NCHW_F32 || x_kind == RTDM_INPUT_NCHW_F16) {
     RTDM_REQUIRE(in_h == S && in_w == S, RTDM_E_UNSUPPORTED,
                  "classify: model expects " + std::to_string(S) + "x" + std::to_string(S) + " input, got " +
@@ -475,11 +493,13 @@ static void run_classifier(rtdm_classifier_s& h, const void* x, int x_kind, int 
     throw Error{RTDM_E_INVALID, "classify: unknown input kind"};
   }
   // ---- stem ----
-  stem_conv_args(h, a, n, View{buf(h.stem_buf), h.stem_cout, 0});
-  seg("stem", nb * ((double)S * S * 3 * (x_kind == RTDM_INPUT_NCHW_F32 ? 4 : es) +
-                    (double)h.stem_oh * h.stem_oh * h.stem_cout * es));
-  launch_conv(a, h.dtype, s);
-  seg_end();
+  if (!stem_done) {
+    stem_conv_args(h, a, n, View{buf(h.stem_buf), h.stem_cout, 0});
+    seg("stem", nb * ((double)S * S * 3 * (x_kind == RTDM_INPUT_NCHW_F32 ? 4 : es) +
+                      (double)h.stem_oh * h.stem_oh * h.stem_cout * es));
+    launch_conv(a, h.dtype, s);
+    seg_end();
+  }
 
   View cur{buf(h.stem_buf), h.stem_cout, 0};
   const bool chain = h.chain_start >= 0 && acff_chain_mode();
@@ -828,6 +848,8 @@ int64_t rtdm_classifier_describe(rtdm_classifier h, char* buf, int64_t buf_len) 
     // (any non-null output view: only its presence is read)
     stem_conv_args(*h, a, 1, View{h->blob.at<void>(0), h->stem_cout, 0});
     s += std::string("conv1 kernel ") + conv_kernel_name(a, h->dtype) + "\n";
+    if (front_fusable(*h))
+      s += "conv1 on frames: fused with the transform (resize_stream_kernel<stem>, frame rows 16-byte multiples)\n";
   }
   const bool chain = h->chain_start >= 0 && acff_chain_mode();
   const bool band = h->band_start >= 0 && acff_band_mode();

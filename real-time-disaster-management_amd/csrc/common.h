@@ -226,6 +226,7 @@ struct Tuning {
   int stem_k16 = 1;         // pooled MFMA stem: the kh = 2 third of K as a 16-deep MFMA (0: 32-deep)
   int conv_c32 = 1;         // conv3_c32 for the Cin-32 3x3 convs (conv_c32.hip)
   int res_fuse = 1;         // conv3_c32r (+ conv3_c64r): Darknet-53's residual blocks as one launch (1: c32r on 8 waves + c64r, 2: c32r on 4 waves, 3: c32r on 8 waves only)
+  int cls_front = 1;        // classifier uint8 frames: CLI transform + conv1 in one launch (0: two launches)
 };
 Tuning& default_tuning();
 const Tuning& tune();
@@ -415,6 +416,7 @@ struct ResizePlan {  // Pillow 8bpc antialiased bilinear, restricted to a center
   int ksize_h = 0, ksize_v = 0;
   int row_first = 0, rows = 0;  // input rows needed by the vertical pass
   int band_rows = 0;            // max input rows of one 16-output-row band (fused kernel)
+  int band_rows17 = 0;          // ... of 17 output rows from a band start (the resize + conv1 kernel)
   int band_rows8 = 0;           // ... of one 8-output-row band (staged kernel)
   int col_first = 0, col_end = 0;  // input columns the crop reads
   DevBuf bounds_h, coef_h, bounds_v, coef_v;  // int32 device arrays
@@ -425,6 +427,11 @@ int resize_stream_mode();
 // frames -> tmp (horizontal pass) -> out (vertical pass + crop + ToTensor + Normalize)
 void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_t* tmp, void* out,
                        int out_layout /*0: NHWC dtype, 1: NCHW f32*/, int dtype, hipStream_t s);
+// The same transform with the classifiers' conv1 (3 -> 16, 3x3, stride 2, pad 0, conv_stem3's
+// packed weights + bias) fused: writes the [n, stem_oh, stem_oh, 16] fp16 stem map only.
+bool preprocess_stem_ok(const ResizePlan& p, const uint8_t* frames, int stem_oh);
+void launch_preprocess_stem(const ResizePlan& p, const uint8_t* frames, int n, const void* w_stem, const float* bias,
+                            void* stem_out, int stem_oh, hipStream_t s);
 
 // Letterbox (datasets.py:599-631): cv2 INTER_AREA resize to new_w x new_h at (left, top)
 // of an out_h x out_w canvas of pad_rgb; uint8 3-channel frames (row pitch in bytes).

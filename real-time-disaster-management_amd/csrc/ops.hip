@@ -896,9 +896,11 @@ void build_resize_plan(ResizePlan& p, int in_h, int in_w, int out_size, bool upl
     p.band_rows8 = std::max(p.band_rows8, cv[2 * y1] + cv[2 * y1 + 1] - cv[2 * y0]);
   }
   p.band_rows = 0;
+  p.band_rows17 = 0;
   for (int y0 = 0; y0 < out_size; y0 += 16) {  // kResizeBand
-    const int y1 = std::min(out_size, y0 + 16) - 1;
+    const int y1 = std::min(out_size, y0 + 16) - 1, y2 = std::min(out_size, y0 + 17) - 1;
     p.band_rows = std::max(p.band_rows, cv[2 * y1] + cv[2 * y1 + 1] - cv[2 * y0]);
+    p.band_rows17 = std::max(p.band_rows17, cv[2 * y2] + cv[2 * y2 + 1] - cv[2 * y0]);
   }
   if (!upload) return;
   auto up = [](DevBuf& d, const std::vector<int>& v) {
@@ -1145,40 +1147,52 @@ constexpr int kRsDepth2 = 4;  // rows in flight with rows taken in pairs (RP 2)
 constexpr int kRsRing = 8;    // LDS ring slots (>= kRsDepth + 2, >= kRsDepth2 + 4), power of two
 constexpr int kRsRowB = 2048; // ring slot bytes: 128 16-byte chunks (2 issuing waves)
 
+// The classifiers' conv1 fused behind the resize (STEM): 3 -> 16 channels, 3x3, stride 2,
+// pad 0 (squeeze_ernet.py:11, ernet.py:10) on the band's fp16 rows, which never reach HBM.
+struct RsStem {
+  const _Float16* w = nullptr;  // conv_stem3's packed weights [16][64] (K16: + 32 the kh = 2 link)
+  const float* bias = nullptr;  // [16]
+  _Float16* out = nullptr;      // [n, oh, oh, 16] fp16 NHWC
+  int oh = 0;
+};
+
 // ABL (diagnostic builds only, outputs wrong when non-zero): 1 = no H-pass LDS reads,
 // 2 = no V pass / output stores (one store per thread), 4 = no row DMA.
 // RP: input rows per wait + barrier (1 or 2)
-template <typename T, int ABL, int RP = 2>
+// STEM: also compute the band's conv1 rows (a band of 16 output rows + the next band's first
+// row feeds 8 stem rows) instead of storing the resized rows
+template <typename T, int ABL, int RP = 2, bool STEM = false>
 __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __restrict__ frames, int in_h, int in_w,
                                                             int row_first, int out, int kh_size, int kv_size,
                                                             int col_first, int c0b, int v16, int band_rows,
                                                             const int* __restrict__ bh, const int* __restrict__ ch,
                                                             const int* __restrict__ bv, const int* __restrict__ cv,
-                                                            T* __restrict__ dst, int nchw) {
+                                                            T* __restrict__ dst, int nchw, RsStem stp) {
+  constexpr int KB = STEM ? kRsBand + 1 : kRsBand;  // resized rows computed per block
   extern __shared__ __attribute__((aligned(16))) uint8_t rsx_lds[];
   const int rstride = kRsRowB;                             // ring slot (zero-weight taps may read past v16*16)
   uint8_t* ring = rsx_lds;                                  // [kRsRing][kRsRowB]
   uint32_t* himg = (uint32_t*)(rsx_lds + kRsRing * kRsRowB);  // [band_rows + kRsTaps][256] packed (r,g,b)
-  int* kv = (int*)(himg + (band_rows + kRsTaps) * 256);    // [kRsBand][kRsTaps]
+  int* kv = (int*)(himg + (band_rows + kRsTaps) * 256);    // [KB][kRsTaps]
   const int bands = (out + kRsBand - 1) / kRsBand;
   const int bl = xcd_block(blockIdx.x, gridDim.x);  // consecutive bands (shared tap rows) on one XCD
   const int b = bl / bands;
   const int yy0 = (bl - b * bands) * kRsBand;
-  const int nyy = out - yy0 < kRsBand ? out - yy0 : kRsBand;
+  const int nyy = out - yy0 < KB ? out - yy0 : KB;
   const int r0 = bv[2 * yy0];
   const int r1 = bv[2 * (yy0 + nyy - 1)] + bv[2 * (yy0 + nyy - 1) + 1];
   const int xx = threadIdx.x;
   const bool col = xx < out;
   // ToTensor + Normalize of the 256 possible uint8 values, per channel: the same
   // float expression as the per-pixel form, evaluated once per block
-  float* lut = (float*)(kv + kRsBand * kRsTaps);  // [3][256]
+  float* lut = (float*)(kv + KB * kRsTaps);  // [3][256]
   {
     const float mean[3] = {0.485f, 0.456f, 0.406f};
     const float stdv[3] = {0.229f, 0.224f, 0.225f};
 #pragma unroll
     for (int c = 0; c < 3; ++c) lut[c * 256 + xx] = ((float)xx / 255.f - mean[c]) / stdv[c];
   }
-  for (int i = xx; i < kRsBand * kRsTaps; i += 256) {
+  for (int i = xx; i < KB * kRsTaps; i += 256) {
     const int j = i / kRsTaps, t = i - j * kRsTaps;
     kv[i] = j < nyy && t < bv[2 * (yy0 + j) + 1] && t < kv_size ? cv[(yy0 + j) * kv_size + t] : 0;
   }
@@ -1273,6 +1287,89 @@ __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __res
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (STEM) {
+    // V pass into registers (fp16 pairs, the values the resized image would hold), then the
+    // ring / H image are dead: the stem image [KB][out + 1] of (c0, c1, c2, 0) pixels (column
+    // x + 1 = input column x, conv_stem3's LDS layout) overlays them
+    uint32_t sp0[KB], sp1[KB];
+    const int xc = col ? xx : 0;
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      // (rows past the band repeat its last row: computed, never staged; no branches, so the
+      // compiler keeps one row's loads live at a time)
+      const int jj = j < nyy ? j : nyy - 1;
+      const uint32_t* hp = himg + (bv[2 * (yy0 + jj)] - r0) * 256 + xc;
+      int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+#pragma unroll
+      for (int t = 0; t < kRsTaps; ++t) {
+        const uint32_t hv = hp[t * 256];
+        const int k = kv[jj * kRsTaps + t];
+        a0 += (int)__umul24(hv & 255u, k);
+        a1 += (int)__umul24((hv >> 8) & 255u, k);
+        a2 += (int)__umul24(hv >> 16, k);
+      }
+      const _Float16 h0 = (_Float16)lut[clip8(a0)], h1 = (_Float16)lut[256 + clip8(a1)],
+                     h2 = (_Float16)lut[512 + clip8(a2)];
+      sp0[j] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+      sp1[j] = (uint32_t)__builtin_bit_cast(uint16_t, h2);
+    }
+    __syncthreads();
+    uint2* simg = (uint2*)rsx_lds;
+    const int ls = out + 2;  // columns 0 and out + 1: zero (the kw = 3 pixel of an odd width's last tile)
+    if (col) {
+#pragma unroll
+      for (int j = 0; j < KB; ++j)
+        if (j < nyy) simg[j * ls + xx + 1] = make_uint2(sp0[j], sp1[j]);
+    }
+    if (xx < 2 * KB) simg[(xx >> 1) * ls + ((xx & 1) ? out + 1 : 0)] = make_uint2(0u, 0u);
+    __syncthreads();
+    // stem rows oy = yy0 / 2 + tr, tr < 8: input rows 2 tr .. 2 tr + 2 of the band; 16-pixel
+    // tiles on v_mfma 16x16x32 (kh 0, 1) + 16x16x16 (kh 2), conv_stem3's links and epilogue
+    typedef _Float16 h8s __attribute__((ext_vector_type(8)));
+    typedef _Float16 h4s __attribute__((ext_vector_type(4)));
+    typedef float f4s __attribute__((ext_vector_type(4)));
+    typedef unsigned int u4s __attribute__((ext_vector_type(4)));
+    const int lane = xx & 63, wid = xx >> 6, p = lane & 15, g = lane >> 4;
+    const int kh0 = g >> 1, pr0 = g & 1;
+    const h8s wa0 = *(const h8s*)(stp.w + (size_t)p * 64 + 8 * g);
+    const h4s w16 = *(const h4s*)(stp.w + (size_t)p * 64 + 32 + 4 * g);
+    float bias4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bias4[j] = stp.bias ? stp.bias[4 * g + j] : 0.f;
+    const int oh = stp.oh, tiles_x = (oh + 15) >> 4, oy0 = yy0 >> 1;
+    int one = 1;  // (two ds_read_b64, not a ds_read2_b64: conv_stem3)
+    asm volatile("" : "+v"(one));
+    for (int t = wid; t < tiles_x * 8; t += 4) {
+      const int tr = t / tiles_x, tx = t - tr * tiles_x;
+      const int oy = oy0 + tr;
+      if (oy >= oh || 2 * tr + 2 >= nyy) continue;
+      const int ox = tx * 16 + p;
+      const bool valid = ox < oh;
+      const int lx = (valid ? ox : oh - 1) * 2 + 1;
+      const uint2* rowk0 = simg + (2 * tr + kh0) * ls;
+      const uint2* rowk2 = simg + (2 * tr + 2) * ls;
+      const uint2 b00 = rowk0[lx + 2 * pr0], b01 = rowk0[lx + 2 * pr0 + one];
+      const h8s bf0 = __builtin_bit_cast(h8s, (u4s{b00.x, b00.y, b01.x, b01.y}));
+      const h4s bk = __builtin_bit_cast(h4s, rowk2[lx + g]);
+      f4s acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa0, bf0, f4s{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      mfma_opcode_switch();
+      acc = __builtin_amdgcn_mfma_f32_16x16x16f16(w16, bk, acc, 0, 0, 0);
+      if (valid) {
+        // conv_stem3's epilogue with its arguments here (in_scale 1, no activation or affine)
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float x = acc[j] * 1.f + bias4[j];
+          v[j] = x * 1.f + 0.f;
+        }
+        const _Float16 q0 = (_Float16)v[0], q1 = (_Float16)v[1], q2 = (_Float16)v[2], q3 = (_Float16)v[3];
+        _Float16* fp = stp.out + (((size_t)b * oh + oy) * oh + ox) * 16 + 4 * g;
+        *(uint2*)fp = make_uint2((uint32_t)__builtin_bit_cast(uint16_t, q0) | ((uint32_t)__builtin_bit_cast(uint16_t, q1) << 16),
+                                 (uint32_t)__builtin_bit_cast(uint16_t, q2) | ((uint32_t)__builtin_bit_cast(uint16_t, q3) << 16));
+      }
+    }
+    return;
+  }
   if (!col) return;
   if constexpr ((ABL & 2) != 0) {
     (void)lut;
@@ -1310,6 +1407,43 @@ __global__ __launch_bounds__(256) void resize_stream_kernel(const uint8_t* __res
 
 int resize_stream_mode() { return tune().resize_stream; }
 
+static size_t preprocess_stem_lds(const ResizePlan& p) {
+  const size_t lds_rs = (size_t)kRsRing * kRsRowB + (size_t)(p.band_rows17 + kRsTaps) * 256 * 4 +
+                        (kRsBand + 1) * kRsTaps * 4 + 3 * 256 * 4;
+  const size_t lds_st = (size_t)(kRsBand + 1) * (p.out + 2) * 8;  // the stem image overlays the ring
+  return std::max(lds_rs, lds_st);
+}
+
+bool preprocess_stem_ok(const ResizePlan& p, const uint8_t* frames, int stem_oh) {
+  const int c0b = (p.col_first * 3) & ~15;
+  const int col_bytes16 = (int)round_up((int64_t)p.col_end * 3 - c0b, 16);
+  return preprocess_stem_lds(p) <= 160 * 1024 && tune().cls_front && tune().stem_k16 && resize_stream_mode() == 1 && p.out <= 255 &&
+         (p.in_w * 3) % 16 == 0 && ((uintptr_t)frames & 15) == 0 && c0b + col_bytes16 <= p.in_w * 3 &&
+         p.ksize_h <= kRsTaps && p.ksize_v <= kRsTaps && col_bytes16 + 32 <= kRsRowB &&
+         (int64_t)p.in_h * p.in_w * 3 < (1ll << 31) && stem_oh == (p.out - 3) / 2 + 1;
+}
+
+void launch_preprocess_stem(const ResizePlan& p, const uint8_t* frames, int n, const void* w_stem, const float* bias,
+                            void* stem_out, int stem_oh, hipStream_t s) {
+  if (n <= 0) return;
+  RTDM_REQUIRE(preprocess_stem_ok(p, frames, stem_oh), RTDM_E_INVALID, "preprocess_stem: unsupported geometry");
+  const int c0b = (p.col_first * 3) & ~15;
+  const int col_bytes16 = (int)round_up((int64_t)p.col_end * 3 - c0b, 16);
+  const int v16 = col_bytes16 / 16;
+  const size_t lds = preprocess_stem_lds(p);
+  const int blocks = n * ((p.out + kRsBand - 1) / kRsBand);
+  RsStem st;
+  st.w = (const _Float16*)w_stem;
+  st.bias = bias;
+  st.out = (_Float16*)stem_out;
+  st.oh = stem_oh;
+  hipLaunchKernelGGL((resize_stream_kernel<_Float16, 0, 2, true>), dim3(blocks), dim3(256), lds, s, frames, p.in_h,
+                     p.in_w, p.row_first, p.out, p.ksize_h, p.ksize_v, p.col_first, c0b, v16, p.band_rows17,
+                     p.bounds_h.as<int>(), p.coef_h.as<int>(), p.bounds_v.as<int>(), p.coef_v.as<int>(),
+                     (_Float16*)nullptr, 0, st);
+  RTDM_HIP(hipGetLastError());
+}
+
 // LDS of the staged kernel: coefficients + bounds + band source rows + band tmp rows.
 static size_t resize_staged_lds(const ResizePlan& p, int col_bytes16) {
   return (size_t)p.out * p.ksize_h * 4 + (size_t)p.out * 2 * 4 + (size_t)p.band_rows8 * col_bytes16 +
@@ -1343,16 +1477,16 @@ void launch_preprocess(const ResizePlan& p, const uint8_t* frames, int n, uint8_
                                                                   : resize_stream_kernel<_Float16, 7>;
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, s, frames, p.in_h, p.in_w, p.row_first, p.out, p.ksize_h,
                          p.ksize_v, p.col_first, c0b, v16, p.band_rows, p.bounds_h.as<int>(), p.coef_h.as<int>(),
-                         p.bounds_v.as<int>(), p.coef_v.as<int>(), (_Float16*)out, 0);
+                         p.bounds_v.as<int>(), p.coef_v.as<int>(), (_Float16*)out, 0, RsStem{});
     } else if (out_layout == 1 || dtype == RTDM_F32)
       hipLaunchKernelGGL((resize_stream_kernel<float, 0>), dim3(blocks), dim3(256), lds, s, frames, p.in_h, p.in_w,
                          p.row_first, p.out, p.ksize_h, p.ksize_v, p.col_first, c0b, v16, p.band_rows, p.bounds_h.as<int>(),
                          p.coef_h.as<int>(), p.bounds_v.as<int>(), p.coef_v.as<int>(), (float*)out,
-                         out_layout == 1 ? 1 : 0);
+                         out_layout == 1 ? 1 : 0, RsStem{});
     else
       hipLaunchKernelGGL((resize_stream_kernel<_Float16, 0>), dim3(blocks), dim3(256), lds, s, frames, p.in_h, p.in_w,
                          p.row_first, p.out, p.ksize_h, p.ksize_v, p.col_first, c0b, v16, p.band_rows, p.bounds_h.as<int>(),
-                         p.coef_h.as<int>(), p.bounds_v.as<int>(), p.coef_v.as<int>(), (_Float16*)out, 0);
+                         p.coef_h.as<int>(), p.bounds_v.as<int>(), p.coef_v.as<int>(), (_Float16*)out, 0, RsStem{});
     RTDM_HIP(hipGetLastError());
     return;
   }

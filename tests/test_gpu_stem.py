@@ -90,3 +90,31 @@ def test_classifier_stem_k16_bit_identical(name, half, cls_weights):
     assert bool(torch.isfinite(logits[1]).all())
     assert torch.equal(logits[0], logits[1]), float((logits[0] - logits[1]).abs().max())
     assert np.array_equal(logits[0].argmax(1).numpy(), logits[1].argmax(1).numpy())
+
+
+@pytest.mark.parametrize("name", ["squeeze-ernet", "squeeze-redconv", "ernet"])
+@pytest.mark.parametrize("geom", [(16, 608, 608), (5, 720, 1280), (3, 100, 160), (2, 97, 131)])
+def test_classifier_front_fused_bit_identical(name, geom, cls_weights):
+    """The CLI transform + conv1 as one launch (resize_stream_kernel<.., STEM>, cls_front 1,
+    the default) against two launches (resize_stream_kernel -> model input -> conv_stem3,
+    cls_front 0): the fused kernel stages the same fp16 pixels in LDS and runs conv_stem3's
+    K16 MFMA links and epilogue on them, so logits must be BIT-IDENTICAL -- downscale
+    (608, 1280 wide), upscale (100 x 160) and a width whose rows are not 16-byte multiples
+    (131: the fused path declines, both runs take two launches).  The 8-channel squeeze
+    stem never fuses."""
+    from rtdm.classifier import build_model
+    from rtdm.synth import synth_frames
+    b, hh, ww = geom
+    frames = torch.from_numpy(synth_frames(b, hh, ww, seed=83)).cuda()
+    logits = {}
+    for v in (0, 1):
+        m = build_model(name)
+        m.load_state_dict(cls_weights[name])
+        m.half()
+        m.set_tuning("cls_front", v)
+        logits[v] = m.classify_frames(frames).cpu()
+        if v:
+            desc = m.describe(b)
+            assert ("conv1 on frames: fused with the transform" in desc) == (name != "squeeze-redconv"), desc
+    assert bool(torch.isfinite(logits[1]).all())
+    assert torch.equal(logits[0], logits[1]), float((logits[0] - logits[1]).abs().max())
