@@ -1894,22 +1894,68 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
     for (int q = 0; q < kNmsRankCap / kNmsThreads; ++q)
       if (tid + q * kNmsThreads < n) K[rk[q]] = mine[q];
     __syncthreads();
-  } else
-  for (int k = 2; k <= npow; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < npow; i += kNmsThreads) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t a = K[i], b = K[ixj];
-          const bool up = (i & k) == 0;
-          if ((a > b) == up) {
-            K[i] = b;
-            K[ixj] = a;
-          }
+  } else {
+  // bitonic network.  LDS keys (npow <= kNmsLdsCap): a thread keeps its keys in registers and
+  // every stage of partner distance j < 64 runs inside the wave on lane shuffles with no
+  // barrier; only the stages j >= 64 go through LDS, a barrier each (npow 512: 15 barriers,
+  // not 45).  Keys are unique, so any correct sort yields the same order.
+  auto cx_lds = [&](int k, int j) {
+    for (int i = tid; i < npow; i += kNmsThreads) {
+      const int ixj = i ^ j;
+      if (ixj > i) {
+        const uint64_t a = K[i], b = K[ixj];
+        const bool up = (i & k) == 0;
+        if ((a > b) == up) {
+          K[i] = b;
+          K[ixj] = a;
         }
       }
-      __syncthreads();
     }
+    __syncthreads();
+  };
+  if constexpr (decltype(lds_tag)::value) {
+    constexpr int EPT = kNmsLdsCap / kNmsThreads;
+    uint64_t v[EPT];
+#pragma unroll
+    for (int m = 0; m < EPT; ++m) {
+      const int i = tid + m * kNmsThreads;
+      v[m] = i < npow ? K[i] : ~0ull;
+    }
+    for (int k = 2; k <= npow; k <<= 1) {
+      if (k > 64) {
+#pragma unroll
+        for (int m = 0; m < EPT; ++m)
+          if (tid + m * kNmsThreads < npow) K[tid + m * kNmsThreads] = v[m];
+        __syncthreads();
+        for (int j = k >> 1; j >= 64; j >>= 1) cx_lds(k, j);
+#pragma unroll
+        for (int m = 0; m < EPT; ++m)
+          if (tid + m * kNmsThreads < npow) v[m] = K[tid + m * kNmsThreads];
+      }
+      const int j0 = (k >> 1) < 32 ? (k >> 1) : 32;
+#pragma unroll
+      for (int m = 0; m < EPT; ++m) {
+        if (m * kNmsThreads + (tid & ~63) >= npow) continue;  // wave-uniform: no key of this wave
+        const int i = tid + m * kNmsThreads;
+        const bool up = (i & k) == 0;
+        for (int j = j0; j > 0; j >>= 1) {
+          const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v[m], j);
+          const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v[m] >> 32), j);
+          const uint64_t p = ((uint64_t)hi << 32) | lo;
+          const bool take_min = ((i & j) == 0) == up;  // the pair's lower index keeps min iff ascending
+          v[m] = take_min ? (p < v[m] ? p : v[m]) : (p > v[m] ? p : v[m]);
+        }
+      }
+    }
+    __syncthreads();  // every wave's last LDS-stage reads are done before the write-back
+#pragma unroll
+    for (int m = 0; m < EPT; ++m)
+      if (tid + m * kNmsThreads < npow) K[tid + m * kNmsThreads] = v[m];
+    __syncthreads();
+  } else {
+    for (int k = 2; k <= npow; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) cx_lds(k, j);
+  }
   }
 
   NMS_STAMP(2);
@@ -2010,13 +2056,18 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
 #pragma unroll
             for (int w = 0; w < kNmsMaskCap / 64; ++w) mrow[w] = (w < W && tid < cnt) ? s_mask[(size_t)i * W + w] : 0ull;
             const uint64_t valid = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
-            uint64_t rem = removed[c], kept = 0;
-            uint64_t todo = valid & ~rem;
+            // todo: the unvisited, unsuppressed candidates of this word.  A row's mask holds
+            // only columns j > i, so visiting the lowest bit b and clearing it together with
+            // b's mask row leaves todo exact (6 scalar ops + 2 readlanes per kept box on the
+            // serial chain; the loop it replaces recomputed todo from valid, rem and a
+            // shifted range mask: 15)
+            uint64_t kept = 0;
+            uint64_t todo = valid & ~removed[c];
             while (todo) {
               const int b = __builtin_ctzll(todo);
-              kept |= 1ull << b;
-              rem |= readlane_u64(mrow[c], b);
-              todo = valid & ~rem & (b == 63 ? 0ull : ~((2ull << b) - 1ull));
+              const uint64_t bit = 1ull << b;
+              kept |= bit;
+              todo &= ~(readlane_u64(mrow[c], b) | bit);
             }
             if ((kept >> tid) & 1ull) g.keep[nk + __popcll(kept & ((1ull << tid) - 1ull))] = i;
             nk += __popcll(kept);

@@ -714,6 +714,25 @@ def test_nms_modes_and_edges(dev):
         _nms_compare(io, conf, iou, classes=[0, 2])
 
 
+def test_nms_candidate_counts_sort_sizes(dev):
+    """Per-image candidate counts around every power of two of the LDS path's sort (npow 1 ..
+    4096: lane-shuffle stages j < 64, LDS stages j >= 64, 1 .. 4 keys per thread) and around
+    the IoU-bitmask capacities (512 in LDS, 2048 in the workspace), one image each, scores
+    with ties broken by the anchor index: survivors bit-exact against the oracle."""
+    counts = [0, 1, 2, 3, 31, 33, 63, 64, 65, 127, 129, 255, 257, 511, 512, 513, 1023, 1025,
+              2047, 2048, 2049, 4095, 4096]
+    rng = np.random.default_rng(5)
+    a = 4200
+    io = np.zeros((len(counts), a, 6), np.float32)
+    for b, c in enumerate(counts):
+        io[b, :, 0:2] = rng.uniform(0, 900, (a, 2))
+        io[b, :, 2:4] = rng.uniform(3, 40, (a, 2))
+        io[b, :c, 4] = rng.choice(np.linspace(0.5, 1.0, 64, dtype=np.float32), c)  # score ties
+        io[b, :c, 5] = 1.0
+    got = _nms_compare(io, 0.3, 0.45)
+    assert got[-1] > 1000
+
+
 def test_nms_large_candidate_set(dev):
     """> 4096 candidates per image exercises the global-memory path."""
     rng = np.random.default_rng(1)
