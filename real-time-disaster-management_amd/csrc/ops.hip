@@ -2010,19 +2010,32 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
       uint64_t bits = 0;
       const int jw = w * 64, j0 = jw + q * QW;
       const int j1 = j0 + QW < n ? j0 + QW : n;
-#pragma unroll 4
-      for (int j = j0 > i + 1 ? j0 : i + 1; j < j1; ++j) {
-        const float4 bj = B[j];
-        const float xx1 = fmaxf(bi.x, bj.x);
-        const float yy1 = fmaxf(bi.y, bj.y);
-        const float xx2 = fminf(bi.z, bj.z);
-        const float yy2 = fminf(bi.w, bj.w);
-        const float w2 = fmaxf(0.f, xx2 - xx1);
-        const float h2 = fmaxf(0.f, yy2 - yy1);
-        const float inter = w2 * h2;
-        if (inter > 0.f || !thr_nonneg) {  // inter == 0: IoU 0 is never > a threshold >= 0
-          const float ovr = inter / ((ai + A[j]) - inter);
-          if ((double)ovr > iou_thr) bits |= 1ull << (j - jw);
+      // four columns per step with their box / area reads issued together (one LDS
+      // latency per four IoUs; the per-column loop waited on each read behind the previous
+      // column's divergent division branch)
+      for (int jb = j0 > i + 1 ? j0 : i + 1; jb < j1; jb += 4) {
+        float4 bq[4];
+        float aq[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = jb + u < j1 ? jb + u : j1 - 1;
+          bq[u] = B[j];
+          aq[u] = A[j];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 bj = bq[u];
+          const float xx1 = fmaxf(bi.x, bj.x);
+          const float yy1 = fmaxf(bi.y, bj.y);
+          const float xx2 = fminf(bi.z, bj.z);
+          const float yy2 = fminf(bi.w, bj.w);
+          const float w2 = fmaxf(0.f, xx2 - xx1);
+          const float h2 = fmaxf(0.f, yy2 - yy1);
+          const float inter = w2 * h2;
+          if (jb + u < j1 && (inter > 0.f || !thr_nonneg)) {  // inter == 0: IoU 0 is never > a threshold >= 0
+            const float ovr = inter / ((ai + aq[u]) - inter);
+            if ((double)ovr > iou_thr) bits |= 1ull << (jb + u - jw);
+          }
         }
       }
       if constexpr (decltype(in_lds_tag)::value) {
