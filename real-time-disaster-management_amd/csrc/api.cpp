@@ -64,6 +64,7 @@ void tuning_set(Tuning& t, const char* key, int v) {
   else if (k == "nms_variant") t.nms_variant = v;
   else if (k == "resize_stream") t.resize_stream = v;
   else if (k == "cls_front") t.cls_front = v ? 1 : 0;
+  else if (k == "nms_split") t.nms_split = v ? 1 : 0;
   else throw Error{RTDM_E_INVALID, "set_tuning: unknown key " + k};
 }
 

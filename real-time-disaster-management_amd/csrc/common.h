@@ -213,6 +213,7 @@ struct Tuning {
   int pipe_wloop = 1;       // conv_pipe tap-unrolled 3x3 K-loops
   int dw3_tile = 1;         // YOLO-ACFF depthwise on the LDS-tiled kernel (1) or the vector one (0)
   int resize_stream = 1;    // classifier preprocessing kernel
+  int nms_split = 1;        // NMS: bitmask + scan of <= 512-candidate images in two more launches (0: one launch)
   int nms_variant = 0;      // NMS diagnostics
   int acff_persist = 1;     // acff_persist for the large-map ACFF stages (> 1: ablations)
   int acff_chain = 1;       // acff_chain for the small-map suffix

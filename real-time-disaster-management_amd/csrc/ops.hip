@@ -1781,11 +1781,93 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// The greedy scan of an n <= kNmsMaskCap candidate bitmask (row i's word w at
+// mask[i * W + w], columns j > i only), by one full wave (lane = tid < 64): lane b holds every
+// mask word of row 64c + b in registers while word block c is scanned.  In-word greedy pass:
+// jump from kept candidate to the next unsuppressed one (find-first-set), so the serial chain
+// is as long as the survivors, not the candidates; the kept rows' masks reach the later words
+// through one wave-wide OR per word.  Writes the kept rows to keep[] in score order and
+// returns their count (wave-uniform).
+template <typename MaskT>
+__device__ __forceinline__ int nms_scan_wave(const MaskT* mask, int n, int W, int lane, int* __restrict__ keep) {
+  int nk = 0;
+  uint64_t removed[kNmsMaskCap / 64];
+#pragma unroll
+  for (int w = 0; w < kNmsMaskCap / 64; ++w) removed[w] = 0;
+#pragma unroll
+  for (int c = 0; c < kNmsMaskCap / 64; ++c) {
+    if (c < W) {
+      const int cnt = n - 64 * c < 64 ? n - 64 * c : 64;
+      const int i = 64 * c + lane;
+      uint64_t mrow[kNmsMaskCap / 64];
+#pragma unroll
+      for (int w = 0; w < kNmsMaskCap / 64; ++w) mrow[w] = (w >= c && w < W && lane < cnt) ? mask[(size_t)i * W + w] : 0ull;
+      const uint64_t valid = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
+      // todo: the unvisited, unsuppressed candidates of this word.  A row's mask holds only
+      // columns j > i, so visiting the lowest bit b and clearing it together with b's mask
+      // row leaves todo exact (6 scalar ops + 2 readlanes per kept box on the serial chain)
+      uint64_t kept = 0;
+      uint64_t todo = valid & ~removed[c];
+      while (todo) {
+        const int b = __builtin_ctzll(todo);
+        const uint64_t bit = 1ull << b;
+        kept |= bit;
+        todo &= ~(readlane_u64(mrow[c], b) | bit);
+      }
+      if ((kept >> lane) & 1ull) keep[nk + __popcll(kept & ((1ull << lane) - 1ull))] = i;
+      nk += __popcll(kept);
+      const bool mine = (kept >> lane) & 1ull;
+#pragma unroll
+      for (int w = c + 1; w < kNmsMaskCap / 64; ++w) {
+        if (w < W) {
+          const uint32_t lo = mine ? (uint32_t)mrow[w] : 0u, hi = mine ? (uint32_t)(mrow[w] >> 32) : 0u;
+          removed[w] |= ((uint64_t)wave_or_u32(hi) << 32) | wave_or_u32(lo);
+        }
+      }
+    }
+  }
+  return nk;
+}
+
+// 5. rows [x1,y1,x2,y2,conf,cls] in kept (descending score) order (utils.py:553-557)
+__device__ __forceinline__ void nms_emit(const float* __restrict__ P, int no, int cls_div, const uint64_t* K,
+                                         const int* __restrict__ keep, int nkeep, int max_det, int img, int tid,
+                                         int nthreads, float* __restrict__ det, int32_t* __restrict__ idx_out,
+                                         int32_t* __restrict__ count) {
+  const int nout = nkeep < max_det ? nkeep : max_det;
+  for (int r = tid; r < nout; r += nthreads) {
+    const int i = keep[r];
+    const uint64_t key = K[i];
+    const uint32_t cand = (uint32_t)key;
+    const int a = cand / cls_div, j = cand - (cand / cls_div) * cls_div;
+    const float* rr = P + (size_t)a * no;
+    const float x = rr[0], y = rr[1], w = rr[2], h = rr[3];
+    float* d = det + ((size_t)img * max_det + r) * 6;
+    d[0] = x - w / 2.f;
+    d[1] = y - h / 2.f;
+    d[2] = x + w / 2.f;
+    d[3] = y + h / 2.f;
+    d[4] = __uint_as_float(~(uint32_t)(key >> 32));
+    d[5] = (float)j;
+    if (idx_out) {
+      idx_out[((size_t)img * max_det + r) * 2 + 0] = a;
+      idx_out[((size_t)img * max_det + r) * 2 + 1] = j;
+    }
+  }
+  if (tid == 0) count[img] = nkeep;
+}
+
+// split mode: the per-image candidate count the prep launch leaves for the mask / scan
+// launches (-1: the prep launch finished the image itself), in the slice's slack bytes
+__device__ __forceinline__ int* nms_split_n(const NmsWs& g, size_t cap) {
+  return (int*)((char*)g.supp + (cap / 32 + 1) * 4 + 128);
+}
+
 __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restrict__ io, int n_anchors, int no,
                                                           float conf, double iou_thr, int multi_label, int agnostic,
                                                           uint64_t class_mask, int max_det, void* ws, size_t cap,
                                                           float* __restrict__ det, int32_t* __restrict__ idx_out,
-                                                          int32_t* __restrict__ count, int variant) {
+                                                          int32_t* __restrict__ count, int variant, int split) {
 #pragma clang fp contract(off)
   __shared__ uint64_t s_keys[kNmsLdsCap];
   __shared__ float4 s_box[kNmsLdsCap];
@@ -1978,6 +2060,21 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
   for (int i = tid; i < (n + 31) / 32; i += kNmsThreads) S[i] = 0u;
   __syncthreads();
 
+  if (split) {
+    // split mode: an image whose bitmask fits the register scan hands its sorted keys,
+    // boxes and areas to nms_mask_kernel / nms_scan_kernel; larger ones finish here
+    if (decltype(lds_tag)::value && n <= kNmsMaskCap && !(variant & 2)) {
+      for (int i = tid; i < n; i += kNmsThreads) {
+        g.keys[i] = K[i];
+        g.box[i] = B[i];
+        g.area[i] = A[i];
+      }
+      if (tid == 0) *nms_split_n(g, cap) = n;
+      return;
+    }
+    if (tid == 0) *nms_split_n(g, cap) = -1;
+  }
+
   NMS_STAMP(3);
   // 4. greedy suppression.
   // n <= kNmsMaskCap: the torchvision-CUDA formulation — every (i, 64-column
@@ -2051,50 +2148,7 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
     NMS_STAMP(4);
     int nk = 0;
     if (in_lds) {
-      // n <= 512 (W <= 8 words): wave 0, lane b holding every mask word of row 64c + b in
-      // registers while word block c is scanned.  In-word greedy pass: jump from kept
-      // candidate to the next unsuppressed one (find-first-set), so the serial chain is as
-      // long as the survivors, not the candidates; the kept rows' masks reach the later
-      // words through one wave-wide OR per word.
-      if (tid < 64) {
-        uint64_t removed[kNmsMaskCap / 64];
-#pragma unroll
-        for (int w = 0; w < kNmsMaskCap / 64; ++w) removed[w] = 0;
-#pragma unroll
-        for (int c = 0; c < kNmsMaskCap / 64; ++c) {
-          if (c < W) {
-            const int cnt = n - 64 * c < 64 ? n - 64 * c : 64;
-            const int i = 64 * c + tid;
-            uint64_t mrow[kNmsMaskCap / 64];
-#pragma unroll
-            for (int w = 0; w < kNmsMaskCap / 64; ++w) mrow[w] = (w < W && tid < cnt) ? s_mask[(size_t)i * W + w] : 0ull;
-            const uint64_t valid = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
-            // todo: the unvisited, unsuppressed candidates of this word.  A row's mask holds
-            // only columns j > i, so visiting the lowest bit b and clearing it together with
-            // b's mask row leaves todo exact (6 scalar ops + 2 readlanes per kept box on the
-            // serial chain; the loop it replaces recomputed todo from valid, rem and a
-            // shifted range mask: 15)
-            uint64_t kept = 0;
-            uint64_t todo = valid & ~removed[c];
-            while (todo) {
-              const int b = __builtin_ctzll(todo);
-              const uint64_t bit = 1ull << b;
-              kept |= bit;
-              todo &= ~(readlane_u64(mrow[c], b) | bit);
-            }
-            if ((kept >> tid) & 1ull) g.keep[nk + __popcll(kept & ((1ull << tid) - 1ull))] = i;
-            nk += __popcll(kept);
-            const bool mine = (kept >> tid) & 1ull;
-#pragma unroll
-            for (int w = c + 1; w < kNmsMaskCap / 64; ++w) {
-              if (w < W) {
-                const uint32_t lo = mine ? (uint32_t)mrow[w] : 0u, hi = mine ? (uint32_t)(mrow[w] >> 32) : 0u;
-                removed[w] |= ((uint64_t)wave_or_u32(hi) << 32) | wave_or_u32(lo);
-              }
-            }
-          }
-        }
-      }
+      if (tid < 64) nk = nms_scan_wave(s_mask, n, W, tid, g.keep);
     } else {
       // kMaskCap < n <= kNmsMaskCapG: the bitmask in the workspace, scanned in chunks of
       // whole 64-candidate words staged through the LDS mask buffer
@@ -2169,33 +2223,82 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
   __syncthreads();  // g.keep written by wave 0 / thread 0 -> read by all below
 
   NMS_STAMP(5);
-  // 5. rows [x1,y1,x2,y2,conf,cls] in kept (descending score) order
-  const int nout = nkeep < max_det ? nkeep : max_det;
-  for (int r = tid; r < nout; r += kNmsThreads) {
-    const int i = g.keep[r];
-    const uint64_t key = K[i];
-    const uint32_t cand = (uint32_t)key;
-    const int a = cand / cls_div, j = cand - (cand / cls_div) * cls_div;
-    const float* rr = P + (size_t)a * no;
-    const float x = rr[0], y = rr[1], w = rr[2], h = rr[3];
-    float* d = det + ((size_t)img * max_det + r) * 6;
-    d[0] = x - w / 2.f;
-    d[1] = y - h / 2.f;
-    d[2] = x + w / 2.f;
-    d[3] = y + h / 2.f;
-    d[4] = __uint_as_float(~(uint32_t)(key >> 32));
-    d[5] = (float)j;
-    if (idx_out) {
-      idx_out[((size_t)img * max_det + r) * 2 + 0] = a;
-      idx_out[((size_t)img * max_det + r) * 2 + 1] = j;
-    }
-  }
-  if (tid == 0) count[img] = nkeep;
+  nms_emit(P, no, cls_div, K, g.keep, nkeep, max_det, img, tid, kNmsThreads, det, idx_out, count);
   };
   if (lds) phases(std::true_type{}, s_keys, s_box, s_area, s_supp);
   else phases(std::false_type{}, g.keys, g.box, g.area, g.supp);
   NMS_STAMP(6);
 #undef NMS_STAMP
+}
+
+// Split mode, launch 2: the IoU bitmask of every image the prep launch handed over, one
+// 256-thread block per (64-column word w, 64-row block r <= w, image): lane = row, wave =
+// 16-column quarter of the word (broadcast column reads), quarters ORed through LDS.  Same
+// IoU arithmetic as nms_kernel's mask, so the same bits; the worst image's mask spreads over
+// up to 36 blocks instead of one.
+__global__ __launch_bounds__(256) void nms_mask_kernel(int n_anchors, int nc, double iou_thr, void* ws, size_t cap) {
+#pragma clang fp contract(off)
+  __shared__ float4 s_b[64];
+  __shared__ float s_a[64];
+  __shared__ uint64_t s_part[4][64];
+  const int w = blockIdx.x, r = blockIdx.y, img = blockIdx.z, tid = threadIdx.x;
+  if (r > w) return;
+  NmsWs g = nms_ws(ws, img, cap, n_anchors, nc);
+  const int n = *nms_split_n(g, cap);
+  if (n < 0 || 64 * w >= n) return;
+  const int W = (n + 63) >> 6, jw = 64 * w, j1 = n < jw + 64 ? n : jw + 64;
+  if (tid < j1 - jw) {
+    s_b[tid] = g.box[jw + tid];
+    s_a[tid] = g.area[jw + tid];
+  }
+  __syncthreads();
+  const int lane = tid & 63, q = tid >> 6;
+  const int i = 64 * r + lane;
+  const bool thr_nonneg = iou_thr >= 0.0;
+  uint64_t bits = 0;
+  if (i < n) {
+    const float4 bi = g.box[i];
+    const float ai = g.area[i];
+    const int c0 = jw + 16 * q, c1 = c0 + 16 < j1 ? c0 + 16 : j1;
+    for (int j = c0 > i + 1 ? c0 : i + 1; j < c1; ++j) {
+      const float4 bj = s_b[j - jw];
+      const float xx1 = fmaxf(bi.x, bj.x);
+      const float yy1 = fmaxf(bi.y, bj.y);
+      const float xx2 = fminf(bi.z, bj.z);
+      const float yy2 = fminf(bi.w, bj.w);
+      const float w2 = fmaxf(0.f, xx2 - xx1);
+      const float h2 = fmaxf(0.f, yy2 - yy1);
+      const float inter = w2 * h2;
+      if (inter > 0.f || !thr_nonneg) {  // inter == 0: IoU 0 is never > a threshold >= 0
+        const float ovr = inter / ((ai + s_a[j - jw]) - inter);
+        if ((double)ovr > iou_thr) bits |= 1ull << (j - jw);
+      }
+    }
+  }
+  s_part[q][lane] = bits;
+  __syncthreads();
+  if (q == 0 && i < n) g.mask[(size_t)i * W + w] = s_part[0][lane] | s_part[1][lane] | s_part[2][lane] | s_part[3][lane];
+}
+
+// Split mode, launch 3: the greedy scan (one wave) and the output rows of every image the prep
+// launch handed over.
+__global__ __launch_bounds__(256) void nms_scan_kernel(const float* __restrict__ io, int n_anchors, int no,
+                                                       int max_det, void* ws, size_t cap, float* __restrict__ det,
+                                                       int32_t* __restrict__ idx_out, int32_t* __restrict__ count) {
+  __shared__ int s_n;
+  const int img = blockIdx.x, tid = threadIdx.x;
+  const int nc = no - 5;
+  NmsWs g = nms_ws(ws, img, cap, n_anchors, nc);
+  const int n = *nms_split_n(g, cap);
+  if (n < 0) return;
+  const int W = (n + 63) >> 6;
+  if (tid < 64) {
+    const int nk = nms_scan_wave(g.mask, n, W, tid, g.keep);
+    if (tid == 0) s_n = nk;
+  }
+  __syncthreads();  // g.keep written by wave 0 -> read by all below
+  nms_emit(io + (size_t)img * n_anchors * no, no, nc > 1 ? nc : 1, g.keys, g.keep, s_n, max_det, img, tid, 256,
+           det, idx_out, count);
 }
 
 void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label, int agnostic,
@@ -2207,8 +2310,17 @@ void launch_nms(const float* io, int n, int n_anchors, int no, float conf, doubl
   const size_t cap = nms_cap(n_anchors, no - 5);
   hipLaunchKernelGGL(nms_cand_kernel, dim3(nms_nblk(n_anchors), n), dim3(kNmsCandBlk), 0, s, io, n_anchors, no, conf,
                      multi_label, class_mask, ws, cap);
+  // split (default): images of <= kNmsMaskCap candidates take their IoU bitmask over many
+  // blocks (nms_mask_kernel) and their scan in a third launch; 0 = one launch per image
+  const int split = tune().nms_split && !(tune().nms_variant & 4) ? 1 : 0;
   hipLaunchKernelGGL(nms_kernel, dim3(n), dim3(kNmsThreads), 0, s, io, n_anchors, no, conf, iou, multi_label,
-                     agnostic, class_mask, max_det, ws, cap, det, idx, count, tune().nms_variant);
+                     agnostic, class_mask, max_det, ws, cap, det, idx, count, tune().nms_variant, split);
+  if (split) {
+    const int wmax = (int)std::min<size_t>(cap, kNmsMaskCap) / 64;
+    hipLaunchKernelGGL(nms_mask_kernel, dim3(wmax, wmax, n), dim3(256), 0, s, n_anchors, no - 5, iou, ws, cap);
+    hipLaunchKernelGGL(nms_scan_kernel, dim3(n), dim3(256), 0, s, io, n_anchors, no, max_det, ws, cap, det, idx,
+                       count);
+  }
   RTDM_HIP(hipGetLastError());
 }
 

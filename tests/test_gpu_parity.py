@@ -697,7 +697,17 @@ def test_nms_golden_io(dev, det_golden):
         _nms_compare(io, conf, iou)
 
 
-def test_nms_modes_and_edges(dev):
+@pytest.mark.parametrize("split", [1, 0])
+def test_nms_modes_and_edges(dev, split):
+    from rtdm import _lib as L
+    L.check(L.lib().rtdm_set_tuning(b"nms_split", split))
+    try:
+        _nms_modes_case()
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"nms_split", 1))
+
+
+def _nms_modes_case():
     rng = np.random.default_rng(0)
     n, a, nc = 3, 3000, 3
     io = np.zeros((n, a, 5 + nc), np.float32)
@@ -714,11 +724,23 @@ def test_nms_modes_and_edges(dev):
         _nms_compare(io, conf, iou, classes=[0, 2])
 
 
-def test_nms_candidate_counts_sort_sizes(dev):
+@pytest.mark.parametrize("split", [1, 0])
+def test_nms_candidate_counts_sort_sizes(dev, split):
     """Per-image candidate counts around every power of two of the LDS path's sort (npow 1 ..
     4096: lane-shuffle stages j < 64, LDS stages j >= 64, 1 .. 4 keys per thread) and around
     the IoU-bitmask capacities (512 in LDS, 2048 in the workspace), one image each, scores
-    with ties broken by the anchor index: survivors bit-exact against the oracle."""
+    with ties broken by the anchor index: survivors bit-exact against the oracle, with the
+    <= 512-candidate images split over three launches (nms_split 1, the default: bitmask on
+    (word, row block) blocks) and in one launch per image (0)."""
+    from rtdm import _lib as L
+    L.check(L.lib().rtdm_set_tuning(b"nms_split", split))
+    try:
+        _nms_counts_case()
+    finally:
+        L.check(L.lib().rtdm_set_tuning(b"nms_split", 1))
+
+
+def _nms_counts_case():
     counts = [0, 1, 2, 3, 31, 33, 63, 64, 65, 127, 129, 255, 257, 511, 512, 513, 1023, 1025,
               2047, 2048, 2049, 4095, 4096]
     rng = np.random.default_rng(5)
