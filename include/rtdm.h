@@ -153,7 +153,9 @@ const char* rtdm_build_arch(void);
  * fused reduce map is not materialised: layer_output refuses it); "stem_k16" 1 = the
  * Cin-3 MFMA stems with the kh = 2 third of K on a 16-deep MFMA (default; bit-identical
  * to 0 = a 32-deep one); "cls_front" 1 = a classifier's uint8-frame transform and its
- * 16-channel conv1 as one launch (default; bit-identical to 0 = two launches); "pool_small_pf" 0 = halo tiles in flight per conv3_pool_small
+ * 16-channel conv1 as one launch (default; bit-identical to 0 = two launches); "nms_split"
+ * 1 = NMS images of <= 512 candidates take their IoU bitmask over many blocks and the greedy
+ * scan in a third launch (default; identical survivors to 0 = one launch per image); "pool_small_pf" 0 = halo tiles in flight per conv3_pool_small
  * block by Cin (default: 2 for Cin 16, 1 for Cin 32) | 1 | 2 (bit-identical);
  * "pool_small64" 1 = 3x3 Cin 64 -> Cout 128 + 2x2 pool (+ full map) on conv3_pool_small
  * (default; bit-identical to 0 = conv_pipe); "pool_sep" 1 = stride-1 5 / 9 / 13 max pools
