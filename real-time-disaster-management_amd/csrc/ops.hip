@@ -2232,7 +2232,7 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
 }
 
 // Split mode, launch 2: the IoU bitmask of every image the prep launch handed over, one
-// 256-thread block per (64-column word w, 64-row block r <= w, image): lane = row, wave =
+// 256-thread block per (64-column word w, 64-row block r <= w, image; a triangular grid): lane = row, wave =
 // 16-column quarter of the word (broadcast column reads), quarters ORed through LDS.  Same
 // IoU arithmetic as nms_kernel's mask, so the same bits; the worst image's mask spreads over
 // up to 36 blocks instead of one.
@@ -2241,8 +2241,11 @@ __global__ __launch_bounds__(256) void nms_mask_kernel(int n_anchors, int nc, do
   __shared__ float4 s_b[64];
   __shared__ float s_a[64];
   __shared__ uint64_t s_part[4][64];
-  const int w = blockIdx.x, r = blockIdx.y, img = blockIdx.z, tid = threadIdx.x;
-  if (r > w) return;
+  // blockIdx.x enumerates the (w, r <= w) pairs row by row: t = w (w + 1) / 2 + r
+  const int t = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  int w = 0;
+  while ((w + 1) * (w + 2) / 2 <= t) ++w;
+  const int r = t - w * (w + 1) / 2;
   NmsWs g = nms_ws(ws, img, cap, n_anchors, nc);
   const int n = *nms_split_n(g, cap);
   if (n < 0 || 64 * w >= n) return;
@@ -2317,7 +2320,8 @@ void launch_nms(const float* io, int n, int n_anchors, int no, float conf, doubl
                      agnostic, class_mask, max_det, ws, cap, det, idx, count, tune().nms_variant, split);
   if (split) {
     const int wmax = (int)std::min<size_t>(cap, kNmsMaskCap) / 64;
-    hipLaunchKernelGGL(nms_mask_kernel, dim3(wmax, wmax, n), dim3(256), 0, s, n_anchors, no - 5, iou, ws, cap);
+    hipLaunchKernelGGL(nms_mask_kernel, dim3(wmax * (wmax + 1) / 2, n), dim3(256), 0, s, n_anchors, no - 5, iou, ws,
+                       cap);
     hipLaunchKernelGGL(nms_scan_kernel, dim3(n), dim3(256), 0, s, io, n_anchors, no, max_det, ws, cap, det, idx,
                        count);
   }
