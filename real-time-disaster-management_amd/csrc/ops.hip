@@ -1783,10 +1783,8 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
 
 // The greedy scan of an n <= kNmsMaskCap candidate bitmask (row i's word w at
 // mask[i * W + w], columns j > i only), by one full wave (lane = tid < 64): lane b holds every
-// mask word of row 64c + b in registers while word block c is scanned.  In-word greedy pass:
-// jump from kept candidate to the next unsuppressed one (find-first-set), so the serial chain
-// is as long as the survivors, not the candidates; the kept rows' masks reach the later words
-// through one wave-wide OR per word.  Writes the kept rows to keep[] in score order and
+// mask word of row 64c + b in registers while word block c is scanned; the kept rows' masks
+// reach the later words through one wave-wide OR per word.  Writes the kept rows to keep[] in score order and
 // returns their count (wave-uniform).
 template <typename MaskT>
 __device__ __forceinline__ int nms_scan_wave(const MaskT* mask, int n, int W, int lane, int* __restrict__ keep) {
@@ -1803,16 +1801,25 @@ __device__ __forceinline__ int nms_scan_wave(const MaskT* mask, int n, int W, in
 #pragma unroll
       for (int w = 0; w < kNmsMaskCap / 64; ++w) mrow[w] = (w >= c && w < W && lane < cnt) ? mask[(size_t)i * W + w] : 0ull;
       const uint64_t valid = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
-      // todo: the unvisited, unsuppressed candidates of this word.  A row's mask holds only
-      // columns j > i, so visiting the lowest bit b and clearing it together with b's mask
-      // row leaves todo exact (6 scalar ops + 2 readlanes per kept box on the serial chain)
+      // The in-word greedy pass, wave-parallel.  sup (lane b): the rows a < b of this word
+      // whose IoU with b is over the threshold -- the word's bit-matrix transposed, built from
+      // the rows with any in-word bit only (usually few).  Then rounds over the undecided set
+      // U: b is kept once none of its suppressors is kept or undecided, removed once one is
+      // kept; the lowest undecided candidate is always decided, and the result is the serial
+      // greedy's (each decision depends only on the decisions below it).
+      uint64_t sup = 0;
+      for (uint64_t nz = __builtin_amdgcn_ballot_w64(mrow[c] != 0ull); nz; nz &= nz - 1) {
+        const int a = __builtin_ctzll(nz);
+        sup |= ((readlane_u64(mrow[c], a) >> lane) & 1ull) << a;
+      }
       uint64_t kept = 0;
-      uint64_t todo = valid & ~removed[c];
-      while (todo) {
-        const int b = __builtin_ctzll(todo);
-        const uint64_t bit = 1ull << b;
-        kept |= bit;
-        todo &= ~(readlane_u64(mrow[c], b) | bit);
+      uint64_t und = valid & ~removed[c];
+      while (und) {
+        const bool in = (und >> lane) & 1ull;
+        const uint64_t kk = __builtin_amdgcn_ballot_w64(in && (sup & (kept | und)) == 0ull);
+        kept |= kk;
+        const uint64_t rr = __builtin_amdgcn_ballot_w64(in && !((kk >> lane) & 1ull) && (sup & kept) != 0ull);
+        und &= ~(kk | rr);
       }
       if ((kept >> lane) & 1ull) keep[nk + __popcll(kept & ((1ull << lane) - 1ull))] = i;
       nk += __popcll(kept);
