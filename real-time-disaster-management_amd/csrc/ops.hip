@@ -1774,6 +1774,29 @@ __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
          (uint32_t)__builtin_amdgcn_readlane((int)v, 32) | (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
+// v of lane (lane ^ J) for the bitonic stages inside a wave (lane = i & 63): J = 1, 2 one DPP
+// quad permutation, J = 4, 8 a DPP row shift each way and a select (no LDS round trip),
+// J = 16, 32 ds_bpermute (__shfl_xor)
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor_u32(uint32_t v, int i) {
+  if constexpr (J == 1) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4 || J == 8) {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + J, 0xf, 0xf, false);  // row_shl: lane + J
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + J, 0xf, 0xf, false);  // row_shr: lane - J
+    return (i & J) ? dn : up;
+  } else {
+    return (uint32_t)__shfl_xor((int)v, J);
+  }
+}
+
+template <int J>
+__device__ __forceinline__ uint64_t lane_xor_u64(uint64_t v, int i) {
+  return ((uint64_t)lane_xor_u32<J>((uint32_t)(v >> 32), i) << 32) | lane_xor_u32<J>((uint32_t)v, i);
+}
+
 // 64-bit readlane (the builtin returns a signed int: widen it as unsigned)
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
@@ -2027,13 +2050,18 @@ __global__ __launch_bounds__(kNmsThreads) void nms_kernel(const float* __restric
         if (m * kNmsThreads + (tid & ~63) >= npow) continue;  // wave-uniform: no key of this wave
         const int i = tid + m * kNmsThreads;
         const bool up = (i & k) == 0;
-        for (int j = j0; j > 0; j >>= 1) {
-          const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v[m], j);
-          const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v[m] >> 32), j);
-          const uint64_t p = ((uint64_t)hi << 32) | lo;
+        auto stage = [&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const uint64_t p = lane_xor_u64<j>(v[m], i);
           const bool take_min = ((i & j) == 0) == up;  // the pair's lower index keeps min iff ascending
           v[m] = take_min ? (p < v[m] ? p : v[m]) : (p > v[m] ? p : v[m]);
-        }
+        };
+        if (j0 >= 32) stage(std::integral_constant<int, 32>{});
+        if (j0 >= 16) stage(std::integral_constant<int, 16>{});
+        if (j0 >= 8) stage(std::integral_constant<int, 8>{});
+        if (j0 >= 4) stage(std::integral_constant<int, 4>{});
+        if (j0 >= 2) stage(std::integral_constant<int, 2>{});
+        stage(std::integral_constant<int, 1>{});
       }
     }
     __syncthreads();  // every wave's last LDS-stage reads are done before the write-back
