@@ -2324,14 +2324,22 @@ __global__ __launch_bounds__(256) void nms_scan_kernel(const float* __restrict__
                                                        int max_det, void* ws, size_t cap, float* __restrict__ det,
                                                        int32_t* __restrict__ idx_out, int32_t* __restrict__ count) {
   __shared__ int s_n;
+  __shared__ uint64_t s_mask[kNmsMaskCap * (kNmsMaskCap / 64)];
   const int img = blockIdx.x, tid = threadIdx.x;
   const int nc = no - 5;
   NmsWs g = nms_ws(ws, img, cap, n_anchors, nc);
   const int n = *nms_split_n(g, cap);
   if (n < 0) return;
   const int W = (n + 63) >> 6;
+  // the bitmask into LDS by the whole block first: read from the workspace inside the scan,
+  // each word block's rows waited on a global load behind the previous block's keep stores
+  for (int p = tid; p < n * W; p += 256) {
+    const int i = p / W, w = p - i * W;
+    if (w >= (i >> 6)) s_mask[p] = g.mask[p];  // (words left of the row's block: never written, never read)
+  }
+  __syncthreads();
   if (tid < 64) {
-    const int nk = nms_scan_wave(g.mask, n, W, tid, g.keep);
+    const int nk = nms_scan_wave(s_mask, n, W, tid, g.keep);
     if (tid == 0) s_n = nk;
   }
   __syncthreads();  // g.keep written by wave 0 -> read by all below
