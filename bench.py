@@ -295,9 +295,10 @@ def pmc_traffic(kernel, workload):
     passes over this bench command; FETCH_SIZE doubled per the gfx950 correction).  None
     when no pass covers it."""
     import glob
-    def tag_key(path):  # rNN + a letter tag that runs a..z, aa..az, ...: by round, then tag length, then tag
-        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(path))
-        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    def tag_key(path):  # rNN + a letter tag that runs a..z, aa..az, ... (+ a repeat number: fin, fin2, ...):
+        # by round, then tag length, then tag, then repeat
+        m = re.match(r"r(\d+)([a-z]*)(\d*)", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2), int(m.group(3) or 0)) if m else (-1, 0, "", 0)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), key=tag_key)
     for path in reversed(files):
         try:
