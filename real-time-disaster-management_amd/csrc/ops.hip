@@ -2325,26 +2325,29 @@ __global__ __launch_bounds__(256) void nms_scan_kernel(const float* __restrict__
                                                        int32_t* __restrict__ idx_out, int32_t* __restrict__ count) {
   __shared__ int s_n;
   __shared__ uint64_t s_mask[kNmsMaskCap * (kNmsMaskCap / 64)];
+  __shared__ uint64_t s_key[kNmsMaskCap];
+  __shared__ int s_keep[kNmsMaskCap];
   const int img = blockIdx.x, tid = threadIdx.x;
   const int nc = no - 5;
   NmsWs g = nms_ws(ws, img, cap, n_anchors, nc);
   const int n = *nms_split_n(g, cap);
   if (n < 0) return;
   const int W = (n + 63) >> 6;
-  // the bitmask into LDS by the whole block first: read from the workspace inside the scan,
-  // each word block's rows waited on a global load behind the previous block's keep stores
-  for (int p = tid; p < n * W; p += 256) {
-    const int i = p / W, w = p - i * W;
-    if (w >= (i >> 6)) s_mask[p] = g.mask[p];  // (words left of the row's block: never written, never read)
+  // the bitmask and the sorted keys into LDS by the whole block first, and the kept list kept
+  // there: the launch is a chain of dependent memory round trips (count -> mask -> scan ->
+  // kept rows -> keys -> io rows -> det), each global one ~1-2 us
+  for (int i = tid; i < n; i += 256) {
+    s_key[i] = g.keys[i];
+    for (int w = i >> 6; w < W; ++w) s_mask[i * W + w] = g.mask[(size_t)i * W + w];  // (words left of the row's block: never read)
   }
   __syncthreads();
   if (tid < 64) {
-    const int nk = nms_scan_wave(s_mask, n, W, tid, g.keep);
+    const int nk = nms_scan_wave(s_mask, n, W, tid, s_keep);
     if (tid == 0) s_n = nk;
   }
-  __syncthreads();  // g.keep written by wave 0 -> read by all below
-  nms_emit(io + (size_t)img * n_anchors * no, no, nc > 1 ? nc : 1, g.keys, g.keep, s_n, max_det, img, tid, 256,
-           det, idx_out, count);
+  __syncthreads();  // s_keep written by wave 0 -> read by all below
+  nms_emit(io + (size_t)img * n_anchors * no, no, nc > 1 ? nc : 1, s_key, s_keep, s_n, max_det, img, tid, 256, det,
+           idx_out, count);
 }
 
 void launch_nms(const float* io, int n, int n_anchors, int no, float conf, double iou, int multi_label, int agnostic,
