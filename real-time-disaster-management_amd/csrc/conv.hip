@@ -236,6 +236,12 @@ __host__ __device__ constexpr int stem_rows(bool pool) { return pool ? kStemRows
 // x <= qw + 10 -> column <= (ow + 21) * s + 4, i.e. 22 * s + pad past the staged columns
 __host__ __device__ constexpr int stem_xcols(bool pool, int s) { return pool ? 22 * s + 2 : 0; }
 
+// two byte values as an fp16 pair: one v_cvt_pkrtz (0..255 are exact in fp16, so the
+// round-toward-zero conversion gives pack_h2's bits)
+__device__ __forceinline__ uint32_t pack_u8x2(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz((float)a, (float)b));
+}
+
 __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
   const _Float16 ha = (_Float16)a, hb = (_Float16)b;
   return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
@@ -303,7 +309,7 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
         uint2* dst = stem_lds + rk[k] * ls + 4 * gk[k] + 1;
 #pragma unroll
         for (int p = 0; p < 4; ++p)
-          dst[p] = make_uint2(pack_h2((float)b[3 * p], (float)b[3 * p + 1]), pack_h2((float)b[3 * p + 2], 0.f));
+          dst[p] = make_uint2(pack_u8x2(b[3 * p], b[3 * p + 1]), pack_u8x2(b[3 * p + 2], 0u));
       }
     }
     const int npad = cols - W;  // LDS column 0 and columns W+1 .. cols-1 are padding
@@ -380,7 +386,7 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
     // tiles are 4 consecutive quads, striding by 2 tiles.
     static_assert(!POOL || ROWS == 4, "two waves per quad row");
     const int qw = a.ow >> 1, qh = a.oh >> 1;
-    const int tr = wid >> 1;
+    const int tr = __builtin_amdgcn_readfirstlane(wid >> 1);  // wave-uniform: the pooled row's buffer base in SGPRs
     const int py = (oy0 >> 1) + tr;
     if (py >= qh) return;
     const int d = p & 3;
@@ -394,6 +400,10 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
     const uint2* rk2 = stem_lds + (ly * s + 2) * ls + lx0 + 2 * (g & 1);
     const uint2* rk2s = stem_lds + (ly * s + 2) * ls + lx0 + g;
     _Float16* pool_row = (_Float16*)e.pool.ptr + ((size_t)n * qh + py) * qw * e.pool.cs + e.pool.co;
+    // the pooled row as a buffer (wave-uniform base, 32-bit lane offsets); a lane with no
+    // output stores at an offset past the row's records, which the buffer unit drops
+    const __amdgpu_buffer_rsrc_t rs_pool =
+        __builtin_amdgcn_make_buffer_rsrc((void*)pool_row, 0, qw * e.pool.cs * 2, 0x00020000);
     // Darknet stem (no BN affine after the fold, LeakyReLU / linear): LeakyReLU as
     // max(x, slope x) (0 < slope < 1; 1 = linear), no per-value branches
     const bool lean = !e.scale && act != ACT_SWISH && (act != ACT_LEAKY || (slope > 0.f && slope <= 1.f));
@@ -467,7 +477,10 @@ __global__ __launch_bounds__(256, 5) void conv_stem3(ConvArgs a) {  // 5: the LD
                     ? fmaxf(fmaxf(epi(acc[u][0], t, 0), epi(acc[u][1], t, 0)), fmaxf(epi(acc[u][2], t, 0), epi(acc[u][3], t, 0)))
                     : epi(fmaxf(fmaxf(acc[u][0], acc[u][1]), fmaxf(acc[u][2], acc[u][3])), t, 0);
           }
-          if (oq[u] < qw && c < a.cout && (!(ABL & 2) || m == 12345.f)) pool_row[(size_t)oq[u] * e.pool.cs + c] = (_Float16)m;
+          if (!(ABL & 2) || m == 12345.f) {
+            const int po = oq[u] < qw && c < a.cout ? (oq[u] * e.pool.cs + c) * 2 : 0x7FFFFFF0;
+            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)m), rs_pool, po, 0, 0);
+          }
         }
       }
     }
